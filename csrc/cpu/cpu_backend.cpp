@@ -1,0 +1,390 @@
+// xflow-amd: CpuBackend — host implementation of xflow::Backend.
+//
+// Executes the same per-element recipes (common.h / types.h / synth.h) as the
+// gfx950 kernels, single threaded and in a fixed order, so it is
+// deterministic.  Used for the reference's CPU "plumbing" configuration, for
+// multi-rank gloo tests, and as the numerics oracle of the HIP kernels.
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "xflow/backend.h"
+#include "xflow/synth.h"
+
+namespace xflow {
+
+namespace {
+
+constexpr u32 kNoSlot = 0xFFFFFFFFu;
+
+inline int64_t count_of(const int64_t* n_dev, int64_t n_host, int64_t n_max) {
+  int64_t n = n_dev ? *n_dev : n_host;
+  return n < n_max ? n : n_max;
+}
+
+struct RowRange {
+  int64_t beg, end;
+};
+
+inline RowRange row_range(const BatchView& b, int64_t r) {
+  if (b.row_ptr) return {b.row_ptr[r], b.row_ptr[r + 1]};
+  return {r * b.nnz_per_row, (r + 1) * b.nnz_per_row};
+}
+
+inline int slice_of(const BatchView& b, int64_t r, int S) {
+  if (b.slice_rows <= 0) return 0;
+  int64_t s = r / b.slice_rows;
+  return (int)(s < S ? s : S - 1);
+}
+
+inline float norm_grad(float raw, const int32_t* slice_rows, int s) {
+  return slice_rows ? (float)((double)raw / (double)slice_rows[s]) : raw;
+}
+
+void add_stats(LossStats* st, float p, float y) {
+  if (!st) return;
+  float pc = std::fmin(std::fmax(p, 1e-7f), 1.0f - 1e-7f);
+  st->ln_loss += (y > 0.5f) ? -(double)std::log(pc) : -(double)std::log(1.0f - pc);
+  st->log2_lik += (y > 0.5f) ? (double)std::log2(p) : (double)std::log2(1.0f - p);
+  st->rows += 1.0;
+  st->positives += (y > 0.5f) ? 1.0 : 0.0;
+}
+
+u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
+  const u64 mask = t.cap - 1;
+  u64 s = fmix64(key) & mask;
+  for (u64 n = 0; n < t.cap; ++n) {
+    u64* kp = reinterpret_cast<u64*>(t.words + s * (u64)t.L.stride);
+    if (*kp == key) return (u32)s;
+    if (*kp == kEmptyKey) {
+      if (!insert) return kNoSlot;
+      *kp = key;
+      claimed = true;
+      return (u32)s;
+    }
+    s = (s + 1) & mask;
+  }
+  *t.overflow = 1u;
+  return kNoSlot;
+}
+
+class CpuBackend final : public Backend {
+ public:
+  bool is_gpu() const override { return false; }
+  std::string name() const override { return "cpu"; }
+
+  void* alloc(size_t bytes) override {
+    void* p = std::aligned_alloc(64, ((bytes ? bytes : 16) + 63) & ~size_t(63));
+    if (!p) throw std::bad_alloc();
+    return p;
+  }
+  void free(void* p) override { std::free(p); }
+  void memset(void* p, int v, size_t bytes) override { std::memset(p, v, bytes); }
+  void fill_u64(u64* p, u64 v, size_t n) override {
+    for (size_t i = 0; i < n; ++i) p[i] = v;
+  }
+  void copy_h2d(void* d, const void* s, size_t b) override { std::memcpy(d, s, b); }
+  void copy_d2h(void* d, const void* s, size_t b) override { std::memcpy(d, s, b); }
+  void copy_d2d(void* d, const void* s, size_t b) override { std::memmove(d, s, b); }
+  void synchronize() override {}
+  void set_stream(void*) override {}
+  void* stream() const override { return nullptr; }
+
+  void table_clear(const TableView& t) override {
+    for (u64 s = 0; s < t.cap; ++s) {
+      u32* sp = t.words + s * (u64)t.L.stride;
+      sp[0] = 0xFFFFFFFFu;
+      sp[1] = 0xFFFFFFFFu;
+      for (int w = 2; w < t.L.stride; ++w) sp[w] = 0u;
+    }
+  }
+  void dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o) override {
+    const u64 mask = s.cap - 1;
+    for (int64_t i = 0; i < nnz; ++i) {
+      u64 k = sanitize_key(keys[i]);
+      u64 p = fmix64(k) & mask;
+      u64 n = 0;
+      for (; n < s.cap; ++n) {
+        if (s.keys[p] == k) break;
+        if (s.keys[p] == kEmptyKey) {
+          s.keys[p] = k;
+          int64_t idx = (*o.n_uniq)++;
+          o.uniq_keys[idx] = k;
+          o.uniq_pos[idx] = (u32)p;
+          break;
+        }
+        p = (p + 1) & mask;
+      }
+      if (n == s.cap) { *o.overflow = 1u; p = 0; }
+      o.pos[i] = (u32)p;
+    }
+  }
+
+  void scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max) override {
+    int64_t n = count_of(n_dev, n_max, n_max);
+    for (int64_t i = 0; i < n; ++i) s.keys[pos[i]] = kEmptyKey;
+  }
+
+  void table_pull(const PullArgs& a) override {
+    int64_t n = count_of(a.n_dev, a.n_host, a.n_max);
+    const TableView& t = a.table;
+    const TableLayout& L = t.L;
+    for (int64_t i = 0; i < n; ++i) {
+      u64 key = sanitize_key(a.keys[i]);
+      bool claimed = false;
+      u32 slot = probe(t, key, a.insert, claimed);
+      if (claimed) ++*t.size;
+      if (a.out_slot) a.out_slot[i] = slot;
+      if (a.out_vals) {
+        float* dst = a.out_vals + (size_t)(a.out_map ? a.out_map[i] : i) * a.pstride;
+        if (slot == kNoSlot) {
+          for (int p = 0; p < L.P; ++p) dst[p] = absent_weight(key, p, L, a.opt);
+        } else {
+          const u32* sp = t.words + (u64)slot * L.stride;
+          for (int p = 0; p < L.P; ++p) dst[p] = slot_weight(sp, key, p, L, a.opt);
+        }
+      }
+    }
+  }
+
+  void table_apply(const ApplyArgs& a) override {
+    int64_t n = count_of(a.n_dev, a.n_host, a.n_max);
+    const TableView& t = a.table;
+    const TableLayout& L = t.L;
+    const int S = a.S, ps = a.pstride, P = a.P;
+    const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
+    for (int64_t i = 0; i < n; ++i) {
+      u32 slot = a.slots[i];
+      u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+      float* g = a.grads + (size_t)row * S * ps;
+      u32 m = a.masks ? a.masks[row] : all;
+      if (slot != kNoSlot) {
+        u32* sp = t.words + (u64)slot * L.stride;
+        u64 key = *reinterpret_cast<u64*>(sp);
+        if (a.sum_slices) {
+          for (int p = 0; p < P; ++p) {
+            float acc = 0.0f;
+            for (int s = 0; s < S; ++s)
+              if (m & (1u << s)) acc += norm_grad(g[s * ps + p], a.slice_rows, s);
+            slot_push(sp, key, p, acc, L, a.opt);
+          }
+          if (L.has_flag) sp[L.flag_word] = 1u;
+        } else {
+          for (int s = 0; s < S; ++s) {
+            if (!(m & (1u << s))) continue;
+            for (int p = 0; p < P; ++p)
+              slot_push(sp, key, p, norm_grad(g[s * ps + p], a.slice_rows, s), L, a.opt);
+            if (L.has_flag) sp[L.flag_word] = 1u;
+          }
+        }
+      }
+      if (a.zero_after) {
+        for (int j = 0; j < S * ps; ++j) g[j] = 0.0f;
+        if (a.masks_rw) a.masks_rw[row] = 0u;
+      }
+      if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
+    }
+  }
+
+  void forward_backward(const FwdArgs& a) override {
+    const BatchView& b = a.batch;
+    const ModelSpec& m = a.model;
+    const int ps = m.pstride();
+    const int D = m.v_dim;
+    std::vector<float> vs(D > 0 ? D : 1), M(D > 0 ? D : 1);
+    std::vector<float> S;
+    for (int64_t r = 0; r < b.rows; ++r) {
+      RowRange rr = row_range(b, r);
+      float y = 0.0f;
+      float vsum = 0.0f;
+      int maxf = 0, G = 0;
+      if (m.kind == kLR) {
+        for (int64_t o = rr.beg; o < rr.end; ++o) y += a.wpull[a.pos[o]];
+      } else if (m.kind == kFM) {
+        float wx = 0.0f, vp = 0.0f;
+        for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+        for (int64_t o = rr.beg; o < rr.end; ++o) {
+          const float* w = a.wpull + (size_t)a.pos[o] * ps;
+          wx += w[0];
+          for (int k = 0; k < D; ++k) {
+            float v = w[1 + k];
+            vs[k] += v;
+            vp += v * v;
+          }
+        }
+        if (m.fm_math == kFmStandard) {
+          float sq = 0.0f;
+          for (int k = 0; k < D; ++k) sq += vs[k] * vs[k];
+          y = wx + 0.5f * (sq - vp);
+        } else {
+          for (int k = 0; k < D; ++k) vsum += vs[k];
+          y = wx + (vsum * vsum - vp);
+        }
+      } else {  // MVM
+        if (!b.fgid) throw std::runtime_error("MVM needs field ids (fgid)");
+        for (int64_t o = rr.beg; o < rr.end; ++o) maxf = std::max(maxf, (int)b.fgid[o]);
+        G = (m.mvm_math == kMvmCompat) ? maxf : maxf + 1;
+        S.assign((size_t)(maxf + 1) * D, 0.0f);
+        for (int k = 0; k < D; ++k) {
+          for (int64_t o = rr.beg; o < rr.end; ++o)
+            S[(size_t)b.fgid[o] * D + k] += a.wpull[(size_t)a.pos[o] * ps + k];
+          float prod = 1.0f;
+          for (int g = 0; g < G; ++g) prod *= S[(size_t)g * D + k];
+          M[k] = prod;
+          y += prod;
+        }
+      }
+      float p = sigmoid_ref(y);
+      float lab = b.labels[r];
+      float loss = p - lab;
+      if (a.pctr) a.pctr[r] = p;
+      add_stats(a.stats, p, lab);
+      if (!a.grad) continue;
+      const int s = slice_of(b, r, a.S);
+      for (int64_t o = rr.beg; o < rr.end; ++o) {
+        float* g = a.grad + ((size_t)a.pos[o] * a.S + s) * ps;
+        if (m.kind == kLR) {
+          g[0] += loss;
+        } else if (m.kind == kFM) {
+          const float* w = a.wpull + (size_t)a.pos[o] * ps;
+          bool standard = m.fm_math == kFmStandard;
+          g[0] += standard ? loss : loss * (float)D;
+          for (int k = 0; k < D; ++k)
+            g[1 + k] += loss * ((standard ? vs[k] : vsum) - w[1 + k]);
+        } else {
+          for (int k = 0; k < D; ++k) {
+            float sg = S[(size_t)b.fgid[o] * D + k];
+            float gr = (sg == 0.0f) ? 0.0f
+                                    : (float)((double)loss * ((double)M[k] / (1.0 + (double)sg)));
+            g[k] += gr;
+          }
+        }
+      }
+    }
+  }
+
+  void slice_masks(const BatchView& b, const u32* pos, u32* tmask) override {
+    int S = b.slice_rows > 0 ? (int)((b.rows + b.slice_rows - 1) / b.slice_rows) : 1;
+    for (int64_t r = 0; r < b.rows; ++r) {
+      RowRange rr = row_range(b, r);
+      u32 bit = 1u << slice_of(b, r, S);
+      for (int64_t o = rr.beg; o < rr.end; ++o) tmask[pos[o]] |= bit;
+    }
+  }
+
+  void bucket(const BucketArgs& a) override {
+    int64_t n = count_of(a.n_dev, a.n_max, a.n_max);
+    std::vector<int64_t> cnt(a.world, 0), off(a.world, 0);
+    for (int64_t i = 0; i < n; ++i) ++cnt[owner_of(a.uniq_keys[i], (u32)a.world)];
+    for (int o = 1; o < a.world; ++o) off[o] = off[o - 1] + cnt[o - 1];
+    for (int o = 0; o < a.world; ++o) a.counts[o] = cnt[o];
+    for (int64_t i = 0; i < n; ++i) {
+      int o = (int)owner_of(a.uniq_keys[i], (u32)a.world);
+      int64_t d = off[o]++;
+      a.send_keys[d] = a.uniq_keys[i];
+      a.send_pos[d] = a.uniq_pos[i];
+    }
+  }
+
+  void gather_grads(const GatherGradArgs& a) override {
+    int64_t n = count_of(a.n_dev, a.n_max, a.n_max);
+    const int W = a.S * a.pstride;
+    for (int64_t i = 0; i < n; ++i) {
+      u32 row = a.map[i];
+      float* src = a.grad_rw + (size_t)row * W;
+      float* dst = a.out + (size_t)i * W;
+      for (int s = 0; s < a.S; ++s)
+        for (int p = 0; p < a.pstride; ++p) {
+          dst[s * a.pstride + p] = norm_grad(src[s * a.pstride + p], a.slice_rows, s);
+          src[s * a.pstride + p] = 0.0f;
+        }
+      if (a.tmask_rw) {
+        a.out_mask[i] = a.tmask_rw[row];
+        a.tmask_rw[row] = 0u;
+      }
+    }
+  }
+
+  void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                    int64_t n_max, int width) override {
+    int64_t n = count_of(n_dev, n_max, n_max);
+    for (int64_t i = 0; i < n; ++i) {
+      int64_t r = map ? map[i] : i;
+      std::memcpy(dst + r * width, src + i * width, sizeof(float) * width);
+    }
+  }
+  void gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                   int64_t n_max, int width, bool zero_src) override {
+    int64_t n = count_of(n_dev, n_max, n_max);
+    for (int64_t i = 0; i < n; ++i) {
+      float* s = const_cast<float*>(src) + (int64_t)map[i] * width;
+      std::memcpy(dst + i * width, s, sizeof(float) * width);
+      if (zero_src) std::memset(s, 0, sizeof(float) * width);
+    }
+  }
+  void gather_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev, int64_t n_max,
+                  bool zero_src) override {
+    int64_t n = count_of(n_dev, n_max, n_max);
+    for (int64_t i = 0; i < n; ++i) {
+      dst[i] = src[map[i]];
+      if (zero_src) const_cast<u32*>(src)[map[i]] = 0u;
+    }
+  }
+  void scatter_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
+                   int64_t n_max) override {
+    int64_t n = count_of(n_dev, n_max, n_max);
+    for (int64_t i = 0; i < n; ++i) dst[map[i]] = src[i];
+  }
+
+  void synth_batch(const SynthArgs& a) override {
+    if (a.fields > kSynthMaxFields) throw std::runtime_error("synth: at most 64 fields");
+    for (int64_t r = 0; r < a.rows; ++r) {
+      const u64 rs = synth_row_seed(a.seed, a.step, r);
+      float logit = a.planted_bias;
+      for (int f = 0; f < a.fields; ++f) {
+        u64 v = a.vocab[f] ? a.vocab[f] : 1;
+        u64 key = synth_key(rs, f, v, (double)a.zipf_s[f], a.hash_space);
+        a.keys[r * a.fields + f] = key;
+        if (a.fgid) a.fgid[r * a.fields + f] = f;
+        logit += synth_planted_weight(key, a.planted_scale);
+      }
+      a.labels[r] = synth_label(rs, logit);
+    }
+  }
+
+  int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
+                       int64_t max_rows) override {
+    const int W = t.L.stride - 2;
+    int64_t n = 0;
+    for (u64 s = 0; s < t.cap; ++s) {
+      const u32* sp = t.words + s * (u64)t.L.stride;
+      u64 key = *reinterpret_cast<const u64*>(sp);
+      if (key == kEmptyKey) continue;
+      if (n < max_rows) {
+        keys_out[n] = key;
+        std::memcpy(words_out + n * W, sp + 2, sizeof(u32) * W);
+      }
+      ++n;
+    }
+    return n;
+  }
+  void table_import(const TableView& t, const u64* keys, const u32* words, int64_t n) override {
+    const int W = t.L.stride - 2;
+    for (int64_t i = 0; i < n; ++i) {
+      bool claimed = false;
+      u32 slot = probe(t, sanitize_key(keys[i]), true, claimed);
+      if (claimed) ++*t.size;
+      if (slot == kNoSlot) continue;
+      std::memcpy(t.words + (u64)slot * t.L.stride + 2, words + i * W, sizeof(u32) * W);
+    }
+  }
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_cpu_backend() { return std::unique_ptr<Backend>(new CpuBackend()); }
+
+}  // namespace xflow

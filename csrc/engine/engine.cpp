@@ -1,0 +1,530 @@
+// xflow-amd: Engine implementation (device agnostic; talks to a Backend).
+#include "xflow/engine.h"
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <stdexcept>
+
+namespace xflow {
+
+namespace {
+
+uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+template <typename T>
+T* balloc(Backend& be, size_t n) {
+  return static_cast<T*>(be.alloc(sizeof(T) * (n ? n : 1)));
+}
+
+constexpr char kMagic[8] = {'X', 'F', 'L', 'O', 'W', 'T', 'B', '1'};
+
+}  // namespace
+
+Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
+  if (cfg_.table_log2_cap < 4 || cfg_.table_log2_cap > 31)
+    throw std::invalid_argument("table_log2_cap must be in [4, 31]");
+  if (cfg_.max_slices < 1 || cfg_.max_slices > 32)
+    throw std::invalid_argument("max_slices must be in [1, 32]");
+  if (cfg_.model.kind != kLR && (cfg_.model.v_dim < 1 || cfg_.model.v_dim > 32))
+    throw std::invalid_argument("v_dim must be in [1, 32]");
+  be_ = cfg_.device >= 0 ? make_hip_backend(cfg_.device) : make_cpu_backend();
+  Backend& be = *be_;
+
+  // persistent table
+  table_.L = TableLayout::make(cfg_.model, cfg_.opt);
+  table_.cap = 1ull << cfg_.table_log2_cap;
+  table_bytes_ = (size_t)table_.cap * table_.L.stride * sizeof(u32);
+  table_.words = static_cast<u32*>(be.alloc(table_bytes_));
+  table_.size = balloc<unsigned long long>(be, 1);
+  overflow_ = balloc<u32>(be, 2);
+  table_.overflow = overflow_ + 1;
+  be.memset(table_.size, 0, sizeof(unsigned long long));
+  be.memset(overflow_, 0, 2 * sizeof(u32));
+  be.table_clear(table_);
+
+  // per-step dedup scratch
+  const int64_t nnz = cfg_.max_nnz;
+  scratch_.cap = next_pow2((uint64_t)((double)nnz * cfg_.scratch_factor) + 1);
+  if (scratch_.cap > (1ull << 31)) throw std::invalid_argument("max_nnz too large");
+  scratch_.keys = balloc<u64>(be, scratch_.cap);
+  be.fill_u64(scratch_.keys, kEmptyKey, scratch_.cap);
+
+  const int ps = cfg_.model.pstride();
+  pos_ = balloc<u32>(be, nnz);
+  uniq_keys_ = balloc<u64>(be, nnz);
+  uniq_pos_ = balloc<u32>(be, nnz);
+  uniq_slot_ = balloc<u32>(be, nnz);
+  send_pos_ = balloc<u32>(be, nnz);
+  n_uniq_ = balloc<int64_t>(be, 1);
+  be.memset(n_uniq_, 0, sizeof(int64_t));
+  wpull_ = balloc<float>(be, scratch_.cap * ps);
+  grad_ = balloc<float>(be, scratch_.cap * cfg_.max_slices * ps);
+  be.memset(grad_, 0, sizeof(float) * scratch_.cap * cfg_.max_slices * ps);
+  tmask_ = balloc<u32>(be, scratch_.cap);
+  be.memset(tmask_, 0, sizeof(u32) * scratch_.cap);
+  stats_ = balloc<LossStats>(be, 2);
+  be.memset(stats_, 0, 2 * sizeof(LossStats));
+  bucket_ws_ = balloc<int64_t>(be, 512);
+  slice_rows_ = balloc<int32_t>(be, 32);
+
+  st_keys_ = balloc<u64>(be, nnz);
+  st_fgid_ = balloc<int32_t>(be, nnz);
+  st_rowptr_ = balloc<int32_t>(be, cfg_.max_rows + 1);
+  st_labels_ = balloc<float>(be, cfg_.max_rows);
+  be.synchronize();
+}
+
+Engine::~Engine() {
+  Backend& be = *be_;
+  be.synchronize();
+  void* ptrs[] = {table_.words, table_.size, overflow_, scratch_.keys, pos_, uniq_keys_,
+                  uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
+                  bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
+                  srv_slots_, host_keys_dev_, host_vals_dev_};
+  for (void* p : ptrs) be.free(p);
+}
+
+int Engine::slices_of(const BatchView& b) const {
+  if (b.slice_rows <= 0 || b.rows <= 0) return 1;
+  return (int)((b.rows + b.slice_rows - 1) / b.slice_rows);
+}
+
+const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
+  if (b.rows == cached_rows_ && b.slice_rows == cached_slice_rows_) return slice_rows_;
+  int32_t h[32];
+  for (int s = 0; s < S; ++s) {
+    int64_t sr = b.slice_rows > 0 ? b.slice_rows : b.rows;
+    int64_t rem = b.rows - (int64_t)s * sr;
+    h[s] = (int32_t)(rem < sr ? rem : sr);
+  }
+  be_->copy_h2d(slice_rows_, h, sizeof(int32_t) * S);
+  cached_rows_ = b.rows;
+  cached_slice_rows_ = b.slice_rows;
+  return slice_rows_;
+}
+
+void Engine::dedup_(const BatchView& b) {
+  if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
+  if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
+  be_->memset(n_uniq_, 0, sizeof(int64_t));
+  DedupOut o;
+  o.pos = pos_;
+  o.uniq_keys = uniq_keys_;
+  o.uniq_pos = uniq_pos_;
+  o.n_uniq = n_uniq_;
+  o.overflow = overflow_;
+  be_->dedup(b.keys, b.nnz, scratch_, o);
+}
+
+void Engine::train_step(const BatchView& b) {
+  const int S = slices_of(b);
+  if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  const int ps = pstride();
+  const bool masks = S > 1 && !cfg_.sum_slices;
+  const int32_t* srows = slice_rows_dev(b, S);
+  dedup_(b);
+
+  PullArgs pa;
+  pa.table = table_;
+  pa.opt = cfg_.opt;
+  pa.keys = uniq_keys_;
+  pa.n_dev = n_uniq_;
+  pa.n_max = b.nnz;
+  pa.insert = true;
+  pa.out_slot = uniq_slot_;
+  pa.out_vals = wpull_;
+  pa.out_map = uniq_pos_;
+  pa.pstride = ps;
+  be_->table_pull(pa);
+
+  if (masks) be_->slice_masks(b, pos_, tmask_);
+
+  FwdArgs fa;
+  fa.batch = b;
+  fa.pos = pos_;
+  fa.wpull = wpull_;
+  fa.grad = grad_;
+  fa.stats = stats_;
+  fa.model = cfg_.model;
+  fa.S = S;
+  be_->forward_backward(fa);
+
+  ApplyArgs aa;
+  aa.table = table_;
+  aa.opt = cfg_.opt;
+  aa.keys = uniq_keys_;
+  aa.slots = uniq_slot_;
+  aa.n_dev = n_uniq_;
+  aa.n_max = b.nnz;
+  aa.grads = grad_;
+  aa.grad_map = uniq_pos_;
+  aa.masks = masks ? tmask_ : nullptr;
+  aa.masks_rw = masks ? tmask_ : nullptr;
+  aa.zero_after = true;
+  aa.S = S;
+  aa.pstride = ps;
+  aa.P = cfg_.model.P();
+  aa.sum_slices = cfg_.sum_slices;
+  aa.slice_rows = srows;
+  aa.scratch = scratch_;
+  aa.reset_pos = uniq_pos_;
+  be_->table_apply(aa);
+}
+
+void Engine::eval_step(const BatchView& b, float* pctr) {
+  dedup_(b);
+  PullArgs pa;
+  pa.table = table_;
+  pa.opt = cfg_.opt;
+  pa.keys = uniq_keys_;
+  pa.n_dev = n_uniq_;
+  pa.n_max = b.nnz;
+  pa.insert = false;
+  pa.out_slot = uniq_slot_;
+  pa.out_vals = wpull_;
+  pa.out_map = uniq_pos_;
+  pa.pstride = pstride();
+  be_->table_pull(pa);
+
+  FwdArgs fa;
+  fa.batch = b;
+  fa.pos = pos_;
+  fa.wpull = wpull_;
+  fa.grad = nullptr;
+  fa.pctr = pctr;
+  fa.stats = stats_ + 1;
+  fa.model = cfg_.model;
+  fa.S = 1;
+  be_->forward_backward(fa);
+  be_->scratch_reset(scratch_, uniq_pos_, n_uniq_, b.nnz);
+}
+
+void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& grads) {
+  const int64_t n = (int64_t)keys.size();
+  const int P = cfg_.model.P();
+  if ((int64_t)grads.size() != n * P) throw std::invalid_argument("push_host: grads != keys*P");
+  if (n == 0) return;
+  if (n > host_cap_) {
+    be_->synchronize();
+    be_->free(host_keys_dev_);
+    be_->free(host_vals_dev_);
+    host_cap_ = n;
+    host_keys_dev_ = balloc<u64>(*be_, n);
+    host_vals_dev_ = balloc<float>(*be_, n * P);
+  }
+  ensure_server_capacity(n);
+  be_->copy_h2d(host_keys_dev_, keys.data(), sizeof(u64) * n);
+  be_->copy_h2d(host_vals_dev_, grads.data(), sizeof(float) * n * P);
+  PullArgs pa;
+  pa.table = table_;
+  pa.opt = cfg_.opt;
+  pa.keys = host_keys_dev_;
+  pa.n_host = n;
+  pa.n_max = n;
+  pa.insert = true;
+  pa.out_slot = srv_slots_;
+  be_->table_pull(pa);
+  // Pushes of one call are applied one key at a time in order; duplicate keys
+  // inside one call are applied sequentially by separate launches.
+  ApplyArgs aa;
+  aa.table = table_;
+  aa.opt = cfg_.opt;
+  aa.keys = host_keys_dev_;
+  aa.S = 1;
+  aa.pstride = P;
+  aa.P = P;
+  for (int64_t i = 0; i < n; ++i) {
+    aa.slots = srv_slots_ + i;
+    aa.grads = host_vals_dev_ + i * P;
+    aa.n_host = 1;
+    aa.n_max = 1;
+    be_->table_apply(aa);
+  }
+  be_->synchronize();
+}
+
+std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
+  const int64_t n = (int64_t)keys.size();
+  const int P = cfg_.model.P();
+  std::vector<float> out((size_t)n * P);
+  if (n == 0) return out;
+  if (n > host_cap_) {
+    be_->synchronize();
+    be_->free(host_keys_dev_);
+    be_->free(host_vals_dev_);
+    host_cap_ = n;
+    host_keys_dev_ = balloc<u64>(*be_, n);
+    host_vals_dev_ = balloc<float>(*be_, n * P);
+  }
+  ensure_server_capacity(n);
+  be_->copy_h2d(host_keys_dev_, keys.data(), sizeof(u64) * n);
+  PullArgs pa;
+  pa.table = table_;
+  pa.opt = cfg_.opt;
+  pa.keys = host_keys_dev_;
+  pa.n_host = n;
+  pa.n_max = n;
+  pa.insert = false;
+  pa.out_slot = srv_slots_;
+  pa.out_vals = host_vals_dev_;
+  pa.pstride = P;
+  be_->table_pull(pa);
+  be_->copy_d2h(out.data(), host_vals_dev_, sizeof(float) * n * P);
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// multi-rank phases
+// ---------------------------------------------------------------------------
+void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out) {
+  const int S = slices_of(b);
+  if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  dedup_(b);
+  BucketArgs ba;
+  ba.uniq_keys = uniq_keys_;
+  ba.uniq_pos = uniq_pos_;
+  ba.n_dev = n_uniq_;
+  ba.n_max = b.nnz;
+  ba.world = world;
+  ba.counts = counts_out;
+  ba.send_keys = send_keys_out;
+  ba.send_pos = send_pos_;
+  ba.scratch = bucket_ws_;
+  be_->bucket(ba);
+  if (S > 1 && !cfg_.sum_slices) be_->slice_masks(b, pos_, tmask_);
+}
+
+void Engine::ensure_server_capacity(int64_t n) {
+  if (n <= srv_cap_) return;
+  be_->synchronize();
+  be_->free(srv_slots_);
+  srv_cap_ = n + n / 4 + 1024;
+  srv_slots_ = balloc<u32>(*be_, srv_cap_);
+}
+
+void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals) {
+  ensure_server_capacity(n);
+  srv_n_ = n;
+  if (n == 0) return;
+  PullArgs pa;
+  pa.table = table_;
+  pa.opt = cfg_.opt;
+  pa.keys = recv_keys;
+  pa.n_host = n;
+  pa.n_max = n;
+  pa.insert = true;
+  pa.out_slot = srv_slots_;
+  pa.out_vals = out_vals;
+  pa.pstride = pstride();
+  be_->table_pull(pa);
+}
+
+void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
+                                float* grads_out, u32* masks_out) {
+  const int S = slices_of(b);
+  const int ps = pstride();
+  const bool masks = S > 1 && !cfg_.sum_slices;
+  const int32_t* srows = slice_rows_dev(b, S);
+  be_->scatter_rows(pulled, wpull_, send_pos_, nullptr, n_send, ps);
+  FwdArgs fa;
+  fa.batch = b;
+  fa.pos = pos_;
+  fa.wpull = wpull_;
+  fa.grad = grad_;
+  fa.stats = stats_;
+  fa.model = cfg_.model;
+  fa.S = S;
+  be_->forward_backward(fa);
+  GatherGradArgs ga;
+  ga.grad = grad_;
+  ga.grad_rw = grad_;
+  ga.tmask = masks ? tmask_ : nullptr;
+  ga.tmask_rw = masks ? tmask_ : nullptr;
+  ga.map = send_pos_;
+  ga.n_max = n_send;
+  ga.S = S;
+  ga.pstride = ps;
+  ga.slice_rows = srows;
+  ga.out = grads_out;
+  ga.out_mask = masks ? masks_out : nullptr;
+  be_->gather_grads(ga);
+  last_nsend_ = n_send;
+}
+
+void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
+                     const std::vector<int64_t>& src_offsets, int S) {
+  const int ps = pstride();
+  for (size_t src = 0; src + 1 < src_offsets.size(); ++src) {
+    int64_t off = src_offsets[src];
+    int64_t cnt = src_offsets[src + 1] - off;
+    if (cnt <= 0) continue;
+    if (src_offsets[src + 1] > srv_n_) throw std::invalid_argument("s_apply: offsets beyond pull");
+    ApplyArgs aa;
+    aa.table = table_;
+    aa.opt = cfg_.opt;
+    aa.keys = recv_keys + off;
+    aa.slots = srv_slots_ + off;
+    aa.n_host = cnt;
+    aa.n_max = cnt;
+    aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * ps;
+    aa.masks = recv_masks ? recv_masks + off : nullptr;
+    aa.zero_after = false;
+    aa.S = S;
+    aa.pstride = ps;
+    aa.P = cfg_.model.P();
+    aa.sum_slices = cfg_.sum_slices;
+    aa.slice_rows = nullptr;
+    be_->table_apply(aa);
+  }
+}
+
+void Engine::w_finish() { be_->scratch_reset(scratch_, uniq_pos_, n_uniq_, cfg_.max_nnz); }
+
+// ---------------------------------------------------------------------------
+LossStats Engine::read_stats(bool reset, int which) {
+  if (which < 0 || which > 1) throw std::invalid_argument("read_stats: which must be 0 or 1");
+  LossStats h;
+  be_->copy_d2h(&h, stats_ + which, sizeof(h));
+  if (reset) be_->memset(stats_ + which, 0, sizeof(LossStats));
+  return h;
+}
+
+int64_t Engine::n_unique() {
+  int64_t n = 0;
+  be_->copy_d2h(&n, n_uniq_, sizeof(n));
+  return n;
+}
+
+int64_t Engine::table_size() {
+  unsigned long long n = 0;
+  be_->copy_d2h(&n, table_.size, sizeof(n));
+  return (int64_t)n;
+}
+
+bool Engine::overflowed() {
+  u32 o[2] = {0, 0};
+  be_->copy_d2h(o, overflow_, sizeof(o));
+  return o[0] || o[1];
+}
+
+BatchView Engine::synth_batch(const SynthArgs& a0, int64_t slice_rows) {
+  SynthArgs a = a0;
+  if (a.rows > cfg_.max_rows || a.rows * a.fields > cfg_.max_nnz)
+    throw std::invalid_argument("synth batch exceeds engine capacity");
+  // caller-provided outputs (e.g. torch tensors) or the engine's staging buffers
+  a.keys = a0.keys ? a0.keys : st_keys_;
+  a.labels = a0.labels ? a0.labels : st_labels_;
+  if (!a0.fgid) a.fgid = cfg_.model.kind == kMVM ? st_fgid_ : nullptr;
+  be_->synth_batch(a);
+  BatchView b;
+  b.keys = a.keys;
+  b.labels = a.labels;
+  b.fgid = a.fgid;
+  b.rows = a.rows;
+  b.nnz = a.rows * a.fields;
+  b.nnz_per_row = a.fields;
+  b.slice_rows = slice_rows;
+  return b;
+}
+
+BatchView Engine::stage_host_batch(const BatchView& h) {
+  if (h.rows > cfg_.max_rows || h.nnz > cfg_.max_nnz)
+    throw std::invalid_argument("host batch exceeds engine capacity");
+  BatchView b = h;
+  be_->copy_h2d(st_keys_, h.keys, sizeof(u64) * h.nnz);
+  b.keys = st_keys_;
+  if (h.row_ptr) {
+    be_->copy_h2d(st_rowptr_, h.row_ptr, sizeof(int32_t) * (h.rows + 1));
+    b.row_ptr = st_rowptr_;
+  }
+  if (h.fgid) {
+    be_->copy_h2d(st_fgid_, h.fgid, sizeof(int32_t) * h.nnz);
+    b.fgid = st_fgid_;
+  }
+  be_->copy_h2d(st_labels_, h.labels, sizeof(float) * h.rows);
+  b.labels = st_labels_;
+  return b;
+}
+
+// ---------------------------------------------------------------------------
+// checkpoint
+// ---------------------------------------------------------------------------
+void Engine::export_table(std::vector<u64>& keys, std::vector<u32>& words) {
+  const int W = state_words();
+  int64_t n = table_size();
+  keys.assign((size_t)n, 0);
+  words.assign((size_t)n * W, 0);
+  if (n == 0) return;
+  u64* dk = balloc<u64>(*be_, n);
+  u32* dw = balloc<u32>(*be_, n * W);
+  int64_t got = be_->table_export(table_, dk, dw, n);
+  if (got != n) {
+    be_->free(dk);
+    be_->free(dw);
+    throw std::runtime_error("export_table: live slot count mismatch");
+  }
+  be_->copy_d2h(keys.data(), dk, sizeof(u64) * n);
+  be_->copy_d2h(words.data(), dw, sizeof(u32) * n * W);
+  be_->free(dk);
+  be_->free(dw);
+}
+
+void Engine::import_table(const std::vector<u64>& keys, const std::vector<u32>& words) {
+  const int W = state_words();
+  const int64_t n = (int64_t)keys.size();
+  if ((int64_t)words.size() != n * W) throw std::invalid_argument("import_table: size mismatch");
+  if (n == 0) return;
+  u64* dk = balloc<u64>(*be_, n);
+  u32* dw = balloc<u32>(*be_, n * W);
+  be_->copy_h2d(dk, keys.data(), sizeof(u64) * n);
+  be_->copy_h2d(dw, words.data(), sizeof(u32) * n * W);
+  be_->table_import(table_, dk, dw, n);
+  be_->synchronize();
+  be_->free(dk);
+  be_->free(dw);
+}
+
+void Engine::save(const std::string& path) {
+  std::vector<u64> keys;
+  std::vector<u32> words;
+  export_table(keys, words);
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  int32_t hdr[8] = {1, cfg_.model.kind, cfg_.model.v_dim, table_.L.P,
+                    table_.L.p_w, table_.L.opt, table_.L.stride, 0};
+  uint64_t n = keys.size();
+  f.write(kMagic, 8);
+  f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
+  f.write(reinterpret_cast<const char*>(&n), sizeof(n));
+  f.write(reinterpret_cast<const char*>(keys.data()), sizeof(u64) * n);
+  f.write(reinterpret_cast<const char*>(words.data()), sizeof(u32) * words.size());
+  if (!f) throw std::runtime_error("write failed: " + path);
+}
+
+void Engine::load(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  char magic[8];
+  int32_t hdr[8];
+  uint64_t n = 0;
+  f.read(magic, 8);
+  f.read(reinterpret_cast<char*>(hdr), sizeof(hdr));
+  f.read(reinterpret_cast<char*>(&n), sizeof(n));
+  if (!f || std::memcmp(magic, kMagic, 8) != 0) throw std::runtime_error("bad checkpoint " + path);
+  if (hdr[1] != cfg_.model.kind || hdr[3] != table_.L.P || hdr[5] != table_.L.opt ||
+      hdr[6] != table_.L.stride)
+    throw std::runtime_error("checkpoint layout does not match this model/optimizer");
+  std::vector<u64> keys(n);
+  std::vector<u32> words(n * (size_t)state_words());
+  f.read(reinterpret_cast<char*>(keys.data()), sizeof(u64) * n);
+  f.read(reinterpret_cast<char*>(words.data()), sizeof(u32) * words.size());
+  if (!f) throw std::runtime_error("truncated checkpoint " + path);
+  import_table(keys, words);
+}
+
+}  // namespace xflow

@@ -1,0 +1,129 @@
+// xflow-amd: HipBackend — the gfx950 implementation of xflow::Backend.
+// Memory comes straight from hipMalloc (the parameter table is tens of GB and
+// lives for the whole run); all work is queued on one HIP stream that the
+// caller may replace (e.g. with PyTorch's current stream) so engine kernels and
+// RCCL collectives are ordered without extra events.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "hip_util.h"
+#include "kernels.h"
+#include "xflow/backend.h"
+
+namespace xflow {
+
+namespace {
+
+class HipBackend final : public Backend {
+ public:
+  explicit HipBackend(int device) : device_(device) {
+    XF_HIP_CHECK(hipSetDevice(device_));
+    XF_HIP_CHECK(hipStreamCreateWithFlags(&own_stream_, hipStreamNonBlocking));
+    stream_ = own_stream_;
+    XF_HIP_CHECK(hipMalloc(&counter_, sizeof(unsigned long long)));
+  }
+  ~HipBackend() override {
+    hipSetDevice(device_);
+    if (counter_) (void)hipFree(counter_);
+    if (own_stream_) (void)hipStreamDestroy(own_stream_);
+  }
+
+  bool is_gpu() const override { return true; }
+  std::string name() const override { return "hip:gfx950:" + std::to_string(device_); }
+
+  void* alloc(size_t bytes) override {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 16;
+    XF_HIP_CHECK(hipSetDevice(device_));
+    XF_HIP_CHECK(hipMalloc(&p, bytes));
+    return p;
+  }
+  void free(void* p) override {
+    if (p) (void)hipFree(p);
+  }
+  void memset(void* p, int v, size_t bytes) override {
+    if (bytes) XF_HIP_CHECK(hipMemsetAsync(p, v, bytes, stream_));
+  }
+  void fill_u64(u64* p, u64 v, size_t n) override { hip::launch_fill_u64(p, v, n, stream_); }
+  void copy_h2d(void* dst, const void* src, size_t bytes) override {
+    if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream_));
+    // host buffer may be reused by the caller right away
+    XF_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  void copy_d2h(void* dst, const void* src, size_t bytes) override {
+    if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream_));
+    XF_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  void copy_d2d(void* dst, const void* src, size_t bytes) override {
+    if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
+  }
+  void synchronize() override { XF_HIP_CHECK(hipStreamSynchronize(stream_)); }
+  // nullptr selects the null (default) stream, which is what torch reports as
+  // its default current stream.
+  void set_stream(void* s) override { stream_ = reinterpret_cast<hipStream_t>(s); }
+  void* stream() const override { return stream_; }
+
+  void table_clear(const TableView& t) override { hip::launch_table_clear(t, stream_); }
+  void dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o) override {
+    hip::launch_dedup(keys, nnz, s, o, stream_);
+  }
+  void scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max) override {
+    hip::launch_scratch_reset(s, pos, n_dev, n_max, stream_);
+  }
+  void table_pull(const PullArgs& a) override { hip::launch_table_pull(a, stream_); }
+  void table_apply(const ApplyArgs& a) override { hip::launch_table_apply(a, stream_); }
+  void forward_backward(const FwdArgs& a) override { hip::launch_forward_backward(a, stream_); }
+  void slice_masks(const BatchView& b, const u32* pos, u32* tmask) override {
+    hip::launch_slice_masks(b, pos, tmask, stream_);
+  }
+  void bucket(const BucketArgs& a) override { hip::launch_bucket(a, stream_); }
+  void gather_grads(const GatherGradArgs& a) override { hip::launch_gather_grads(a, stream_); }
+  void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                    int64_t n_max, int width) override {
+    hip::launch_scatter_rows(src, dst, map, n_dev, n_max, width, stream_);
+  }
+  void gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                   int64_t n_max, int width, bool zero_src) override {
+    hip::launch_gather_rows(src, dst, map, n_dev, n_max, width, zero_src, stream_);
+  }
+  void gather_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev, int64_t n_max,
+                  bool zero_src) override {
+    hip::launch_gather_u32(src, dst, map, n_dev, n_max, zero_src, stream_);
+  }
+  void scatter_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
+                   int64_t n_max) override {
+    hip::launch_scatter_u32(src, dst, map, n_dev, n_max, stream_);
+  }
+  void synth_batch(const SynthArgs& a) override { hip::launch_synth(a, stream_); }
+  int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
+                       int64_t max_rows) override {
+    hip::launch_table_export(t, keys_out, words_out, max_rows, counter_, stream_);
+    unsigned long long n = 0;
+    copy_d2h(&n, counter_, sizeof(n));
+    return (int64_t)n;
+  }
+  void table_import(const TableView& t, const u64* keys, const u32* words, int64_t n) override {
+    hip::launch_table_import(t, keys, words, n, stream_);
+  }
+
+ private:
+  int device_;
+  hipStream_t own_stream_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  unsigned long long* counter_ = nullptr;
+};
+
+}  // namespace
+
+std::unique_ptr<Backend> make_hip_backend(int device) {
+  return std::unique_ptr<Backend>(new HipBackend(device));
+}
+
+bool hip_backend_available() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return false;
+  return n > 0;
+}
+
+}  // namespace xflow

@@ -1,0 +1,74 @@
+// xflow-amd: gfx950 HIP helpers (wave64 primitives, launch sizing, errors).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#include "xflow/common.h"
+
+#define XF_HIP_CHECK(expr)                                                        \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess) {                                                       \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(_e) + \
+                               " at " __FILE__ ":" + std::to_string(__LINE__) +   \
+                               " (" #expr ")");                                   \
+    }                                                                             \
+  } while (0)
+
+namespace xflow {
+namespace hip {
+
+constexpr int kWave = 64;        // CDNA wavefront width
+constexpr int kBlock = 256;      // 4 waves per workgroup
+// Memory-bound grid cap: 256 CUs x 8 resident 256-thread blocks.
+constexpr int kMaxGrid = 2048;
+
+inline int grid_for(int64_t n, int block = kBlock, int cap = kMaxGrid) {
+  if (n <= 0) return 1;
+  int64_t g = (n + block - 1) / block;
+  return (int)(g < cap ? g : cap);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Wave-aggregated append: every lane with `pred` gets a unique index from one
+// atomicAdd per wave on `counter`.  Lanes without pred receive -1.
+template <typename T>
+__device__ __forceinline__ T wave_append(T* counter, bool pred) {
+  unsigned long long m = __ballot(pred);
+  if (m == 0ull) return (T)-1;
+  int lane = lane_id();
+  int leader = __ffsll((long long)m) - 1;
+  T base = 0;
+  if (lane == leader) base = atomicAdd(counter, (T)__popcll(m));
+  base = __shfl(base, leader);
+  unsigned long long below = (lane == 0) ? 0ull : (m & ((~0ull) >> (64 - lane)));
+  return pred ? base + (T)__popcll(below) : (T)-1;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Read a device-side element count, clamped to the launch's upper bound.
+__device__ __forceinline__ int64_t dev_count(const int64_t* n_dev, int64_t n_host,
+                                             int64_t n_max) {
+  int64_t n = n_dev ? *n_dev : n_host;
+  return n < n_max ? n : n_max;
+}
+
+}  // namespace hip
+}  // namespace xflow

@@ -1,0 +1,42 @@
+// xflow-amd: host launchers of the gfx950 kernels (implemented in *.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "xflow/backend.h"
+
+namespace xflow {
+namespace hip {
+
+// kernels_table.hip
+void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st);
+void launch_scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max,
+                          hipStream_t st);
+void launch_table_pull(const PullArgs& a, hipStream_t st);
+void launch_table_apply(const ApplyArgs& a, hipStream_t st);
+void launch_gather_grads(const GatherGradArgs& a, hipStream_t st);
+void launch_bucket(const BucketArgs& a, hipStream_t st);
+void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                         int64_t n_max, int width, hipStream_t st);
+void launch_gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                        int64_t n_max, int width, bool zero_src, hipStream_t st);
+void launch_gather_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
+                       int64_t n_max, bool zero_src, hipStream_t st);
+void launch_scatter_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
+                        int64_t n_max, hipStream_t st);
+void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st);
+void launch_table_clear(const TableView& t, hipStream_t st);
+void launch_table_export(const TableView& t, u64* keys_out, u32* words_out, int64_t max_rows,
+                         unsigned long long* counter, hipStream_t st);
+void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,
+                         hipStream_t st);
+
+// kernels_model.hip
+void launch_forward_backward(const FwdArgs& a, hipStream_t st);
+void launch_slice_masks(const BatchView& b, const u32* pos, u32* tmask, hipStream_t st);
+
+// kernels_synth.hip
+void launch_synth(const SynthArgs& a, hipStream_t st);
+
+}  // namespace hip
+}  // namespace xflow

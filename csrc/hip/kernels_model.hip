@@ -1,0 +1,291 @@
+// xflow-amd: fused forward + backward kernels for LR / FM / MVM (gfx950).
+//
+// One lane per row.  The pulled parameters of the batch's unique keys live in
+// a dense buffer indexed by the key's dedup-scratch slot (`wpull[pos]`), so a
+// row gathers its features with one dependent load each and never touches the
+// persistent table.  The loss-weighted gradient contributions are added
+// (un-normalised, like the reference's running sums) into `grad[pos][slice]`;
+// the per-slice division by row count happens when the gradients are pushed.
+//
+// Reference math:
+//   LR   lr_worker.cc:121-143 (loss), :100-119 (gradient)
+//   FM   fm_worker.cc:159-202 (loss), :126-157 (gradient)      [kFmReference]
+//   MVM  mvm_worker.cc:172-218 (loss), :137-170 (gradient)
+#include "kernels.h"
+#include "hip_util.h"
+
+namespace xflow {
+namespace hip {
+
+struct RowRange {
+  int64_t beg, end;
+};
+
+__device__ __forceinline__ RowRange row_range(const BatchView& b, int64_t r) {
+  if (b.row_ptr) return {b.row_ptr[r], b.row_ptr[r + 1]};
+  return {r * b.nnz_per_row, (r + 1) * b.nnz_per_row};
+}
+
+__device__ __forceinline__ int slice_of(const BatchView& b, int64_t r, int S) {
+  if (b.slice_rows <= 0) return 0;
+  int64_t s = r / b.slice_rows;
+  return (int)(s < S ? s : S - 1);
+}
+
+// Per-row loss statistics, reduced per workgroup then one f64 atomic each.
+struct StatAcc {
+  double ln = 0, l2 = 0, rows = 0, pos = 0;
+  __device__ void add(float p, float y) {
+    float pc = fminf(fmaxf(p, 1e-7f), 1.0f - 1e-7f);
+    ln += (y > 0.5f) ? -(double)logf(pc) : -(double)logf(1.0f - pc);
+    l2 += (y > 0.5f) ? (double)log2f(p) : (double)log2f(1.0f - p);
+    rows += 1.0;
+    pos += (y > 0.5f) ? 1.0 : 0.0;
+  }
+};
+
+template <int BLOCK>
+__device__ void flush_stats(StatAcc a, LossStats* out) {
+  if (!out) return;
+  __shared__ double red[4][BLOCK / kWave];
+  a.ln = wave_sum(a.ln);
+  a.l2 = wave_sum(a.l2);
+  a.rows = wave_sum(a.rows);
+  a.pos = wave_sum(a.pos);
+  int w = threadIdx.x / kWave, l = threadIdx.x % kWave;
+  if (l == 0) {
+    red[0][w] = a.ln;
+    red[1][w] = a.l2;
+    red[2][w] = a.rows;
+    red[3][w] = a.pos;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double s = 0;
+    for (int i = 0; i < BLOCK / kWave; ++i) s += red[threadIdx.x][i];
+    double* dst = threadIdx.x == 0 ? &out->ln_loss
+                  : threadIdx.x == 1 ? &out->log2_lik
+                  : threadIdx.x == 2 ? &out->rows
+                                     : &out->positives;
+    if (s != 0.0) atomicAdd(dst, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LR
+// ---------------------------------------------------------------------------
+template <bool kGrad>
+__global__ void __launch_bounds__(kBlock) k_lr(FwdArgs a) {
+  const BatchView& b = a.batch;
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  StatAcc st;
+  if (r < b.rows) {
+    RowRange rr = row_range(b, r);
+    float wx = 0.0f;
+    for (int64_t o = rr.beg; o < rr.end; ++o) wx += a.wpull[a.pos[o]];
+    float p = sigmoid_ref(wx);
+    float y = b.labels[r];
+    float loss = p - y;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, y);
+    if (kGrad) {
+      const int s = slice_of(b, r, a.S);
+      for (int64_t o = rr.beg; o < rr.end; ++o)
+        atomicAdd(&a.grad[(size_t)a.pos[o] * a.S + s], loss);
+    }
+  }
+  flush_stats<kBlock>(st, a.stats);
+}
+
+// ---------------------------------------------------------------------------
+// FM: pulled row = [w, v_0 .. v_{D-1}, pad] (pstride floats)
+// ---------------------------------------------------------------------------
+template <int D, bool kGrad>
+__global__ void __launch_bounds__(kBlock) k_fm(FwdArgs a) {
+  const BatchView& b = a.batch;
+  const int ps = a.model.pstride();
+  const bool standard = a.model.fm_math == kFmStandard;
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  StatAcc st;
+  if (r < b.rows) {
+    RowRange rr = row_range(b, r);
+    float wx = 0.0f, vp = 0.0f;
+    float vs[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+    for (int64_t o = rr.beg; o < rr.end; ++o) {
+      const float* w = a.wpull + (size_t)a.pos[o] * ps;
+      wx += w[0];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        float v = w[1 + k];
+        vs[k] += v;
+        vp += v * v;
+      }
+    }
+    float vsum = 0.0f, y;
+    if (standard) {
+      float sq = 0.0f;
+#pragma unroll
+      for (int k = 0; k < D; ++k) sq += vs[k] * vs[k];
+      y = wx + 0.5f * (sq - vp);
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) vsum += vs[k];
+      y = wx + (vsum * vsum - vp);
+    }
+    float p = sigmoid_ref(y);
+    float lab = b.labels[r];
+    float loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+    if (kGrad) {
+      const int s = slice_of(b, r, a.S);
+      const float gw = standard ? loss : loss * (float)D;
+      for (int64_t o = rr.beg; o < rr.end; ++o) {
+        const float* w = a.wpull + (size_t)a.pos[o] * ps;
+        float* g = a.grad + ((size_t)a.pos[o] * a.S + s) * ps;
+        atomicAdd(&g[0], gw);
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          float ref = standard ? vs[k] : vsum;
+          atomicAdd(&g[1 + k], loss * (ref - w[1 + k]));
+        }
+      }
+    }
+  }
+  flush_stats<kBlock>(st, a.stats);
+}
+
+// ---------------------------------------------------------------------------
+// MVM: per-row field buckets in LDS, laid out [field][lane] (conflict-free).
+// ---------------------------------------------------------------------------
+constexpr int kMvmBlock = 64;
+constexpr int kMvmMaxFields = 128;
+
+template <int D, bool kGrad>
+__global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
+  __shared__ float S[kMvmMaxFields + 1][kMvmBlock];
+  const BatchView& b = a.batch;
+  const int ps = a.model.pstride();
+  const bool compat = a.model.mvm_math == kMvmCompat;
+  const int t = threadIdx.x;
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + t;
+  StatAcc st;
+  if (r < b.rows) {
+    RowRange rr = row_range(b, r);
+    int maxf = 0;
+    for (int64_t o = rr.beg; o < rr.end; ++o) maxf = max(maxf, (int)b.fgid[o]);
+    maxf = min(maxf, kMvmMaxFields);
+    const int G = compat ? maxf : maxf + 1;
+    float M[D];
+    float y = 0.0f;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      for (int g = 0; g <= maxf; ++g) S[g][t] = 0.0f;
+      for (int64_t o = rr.beg; o < rr.end; ++o) {
+        int f = b.fgid[o];
+        if (f <= kMvmMaxFields) S[f][t] += a.wpull[(size_t)a.pos[o] * ps + k];
+      }
+      float m = 1.0f;
+      for (int g = 0; g < G; ++g) m *= S[g][t];
+      M[k] = m;
+      y += m;
+    }
+    float p = sigmoid_ref(y);
+    float lab = b.labels[r];
+    float loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+    if (kGrad) {
+      const int s = slice_of(b, r, a.S);
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        for (int g = 0; g <= maxf; ++g) S[g][t] = 0.0f;
+        for (int64_t o = rr.beg; o < rr.end; ++o) {
+          int f = b.fgid[o];
+          if (f <= kMvmMaxFields) S[f][t] += a.wpull[(size_t)a.pos[o] * ps + k];
+        }
+        for (int64_t o = rr.beg; o < rr.end; ++o) {
+          int f = b.fgid[o];
+          float sg = (f <= kMvmMaxFields) ? S[f][t] : 0.0f;
+          float gr = (sg == 0.0f) ? 0.0f
+                                  : (float)((double)loss * ((double)M[k] / (1.0 + (double)sg)));
+          atomicAdd(&a.grad[((size_t)a.pos[o] * a.S + s) * ps + k], gr);
+        }
+      }
+    }
+  }
+  flush_stats<kMvmBlock>(st, a.stats);
+}
+
+template <bool kGrad>
+static void dispatch_fm(const FwdArgs& a, int grid, hipStream_t st) {
+  switch (a.model.v_dim) {
+#define XF_FM_CASE(DD) \
+  case DD: hipLaunchKernelGGL((k_fm<DD, kGrad>), dim3(grid), dim3(kBlock), 0, st, a); break;
+    XF_FM_CASE(1) XF_FM_CASE(2) XF_FM_CASE(4) XF_FM_CASE(8) XF_FM_CASE(10) XF_FM_CASE(16)
+    XF_FM_CASE(32)
+#undef XF_FM_CASE
+    default:
+      throw std::runtime_error("FM: unsupported v_dim (1,2,4,8,10,16,32)");
+  }
+}
+
+template <bool kGrad>
+static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
+  int grid = (int)((a.batch.rows + kMvmBlock - 1) / kMvmBlock);
+  switch (a.model.v_dim) {
+#define XF_MVM_CASE(DD) \
+  case DD: hipLaunchKernelGGL((k_mvm<DD, kGrad>), dim3(grid), dim3(kMvmBlock), 0, st, a); break;
+    XF_MVM_CASE(1) XF_MVM_CASE(2) XF_MVM_CASE(4) XF_MVM_CASE(8) XF_MVM_CASE(10) XF_MVM_CASE(16)
+    XF_MVM_CASE(32)
+#undef XF_MVM_CASE
+    default:
+      throw std::runtime_error("MVM: unsupported v_dim (1,2,4,8,10,16,32)");
+  }
+}
+
+void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
+  if (a.batch.rows <= 0) return;
+  const bool grad = a.grad != nullptr;
+  int grid = (int)((a.batch.rows + kBlock - 1) / kBlock);
+  switch (a.model.kind) {
+    case kLR:
+      if (grad) hipLaunchKernelGGL((k_lr<true>), dim3(grid), dim3(kBlock), 0, st, a);
+      else hipLaunchKernelGGL((k_lr<false>), dim3(grid), dim3(kBlock), 0, st, a);
+      break;
+    case kFM:
+      if (grad) dispatch_fm<true>(a, grid, st);
+      else dispatch_fm<false>(a, grid, st);
+      break;
+    case kMVM:
+      if (!a.batch.fgid) throw std::runtime_error("MVM needs field ids (fgid)");
+      if (grad) dispatch_mvm<true>(a, st);
+      else dispatch_mvm<false>(a, st);
+      break;
+    default:
+      throw std::runtime_error("unknown model kind");
+  }
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void k_slice_masks(BatchView b, const u32* __restrict__ pos, u32* __restrict__ tmask,
+                              int S) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= b.rows) return;
+  RowRange rr = row_range(b, r);
+  u32 bit = 1u << slice_of(b, r, S);
+  for (int64_t o = rr.beg; o < rr.end; ++o) atomicOr(&tmask[pos[o]], bit);
+}
+
+void launch_slice_masks(const BatchView& b, const u32* pos, u32* tmask, hipStream_t st) {
+  if (b.rows <= 0) return;
+  int S = b.slice_rows > 0 ? (int)((b.rows + b.slice_rows - 1) / b.slice_rows) : 1;
+  hipLaunchKernelGGL(k_slice_masks, dim3((int)((b.rows + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     st, b, pos, tmask, S);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace xflow

@@ -1,0 +1,548 @@
+// xflow-amd: gfx950 kernels for the HBM-resident sparse parameter store.
+//
+// Replaces the ps-lite KVServer + unordered_map store of the reference
+// (/root/reference/src/optimizer/ftrl.h:38-152, server.h:20-35) and the
+// worker-side sort/unique key preparation (lr_worker.cc:146-166):
+//
+//   dedup        per-step open-addressing scratch table: each occurrence finds
+//                or claims its key's slot; claimers append (key, slot) to the
+//                unique list with one atomic per wave.  No sort at all.
+//   table_pull   probe/insert of unique keys into the persistent table and
+//                evaluation of the reference pull value (FTRL weight closed form
+//                from (n,z), lazy N(0,1)*1e-2 latent init).
+//   table_apply  per-coordinate FTRL-Proximal / SGD push, one lane per key,
+//                contributions applied in (slice) order -> deterministic.
+//
+// All kernels are memory-latency bound (random 16-64 B accesses); they are
+// written as grid-stride loops over <= 2048 workgroups of 4 waves and read
+// device-side element counts so a whole step runs without host syncs.
+#include "kernels.h"
+#include "hip_util.h"
+
+namespace xflow {
+namespace hip {
+
+constexpr u32 kNoSlot = 0xFFFFFFFFu;
+
+// ---------------------------------------------------------------------------
+// dedup
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_dedup(const u64* __restrict__ keys, int64_t nnz,
+                                                  u64* __restrict__ skeys, u64 cap,
+                                                  u32* __restrict__ pos, u64* __restrict__ uk,
+                                                  u32* __restrict__ up,
+                                                  unsigned long long* __restrict__ n_uniq,
+                                                  u32* __restrict__ overflow) {
+  const u64 mask = cap - 1;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += stride) {
+    u64 k = sanitize_key(keys[i]);
+    u64 s = fmix64(k) & mask;
+    bool claimed = false;
+    u64 n = 0;
+    for (; n < cap; ++n) {
+      u64 cur = skeys[s];
+      if (cur == k) break;
+      if (cur == kEmptyKey) {
+        u64 prev = atomicCAS((unsigned long long*)&skeys[s], (unsigned long long)kEmptyKey,
+                             (unsigned long long)k);
+        if (prev == kEmptyKey) { claimed = true; break; }
+        if (prev == k) break;
+      }
+      s = (s + 1) & mask;
+    }
+    if (n == cap) { *overflow = 1u; s = 0; }
+    pos[i] = (u32)s;
+    unsigned long long idx = wave_append(n_uniq, claimed);
+    if (claimed) {
+      uk[idx] = k;
+      up[idx] = (u32)s;
+    }
+  }
+}
+
+void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(k_dedup, dim3(grid_for(nnz)), dim3(kBlock), 0, st, keys, nnz, s.keys,
+                     s.cap, o.pos, o.uniq_keys, o.uniq_pos,
+                     reinterpret_cast<unsigned long long*>(o.n_uniq), o.overflow);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void k_scratch_reset(u64* __restrict__ skeys, const u32* __restrict__ pos,
+                                const int64_t* n_dev, int64_t n_max) {
+  int64_t n = dev_count(n_dev, n_max, n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    skeys[pos[i]] = kEmptyKey;
+}
+
+void launch_scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max,
+                          hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_scratch_reset, dim3(grid_for(n_max)), dim3(kBlock), 0, st, s.keys, pos,
+                     n_dev, n_max);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void k_fill_u64(u64* p, u64 v, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_fill_u64, dim3(grid_for((int64_t)n)), dim3(kBlock), 0, st, p, v, n);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void k_table_clear(TableView t) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const int W = t.L.stride;
+  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += stride) {
+    u32* sp = t.words + s * (u64)W;
+    sp[0] = 0xFFFFFFFFu;
+    sp[1] = 0xFFFFFFFFu;
+    for (int w = 2; w < W; ++w) sp[w] = 0u;
+  }
+}
+
+void launch_table_clear(const TableView& t, hipStream_t st) {
+  hipLaunchKernelGGL(k_table_clear, dim3(grid_for((int64_t)t.cap)), dim3(kBlock), 0, st, t);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// persistent table probe
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
+  const u64 mask = t.cap - 1;
+  u64 s = fmix64(key) & mask;
+  const int stride = t.L.stride;
+  for (u64 n = 0; n < t.cap; ++n) {
+    u64* kp = reinterpret_cast<u64*>(t.words + s * (u64)stride);
+    u64 cur = *kp;
+    if (cur == key) return (u32)s;
+    if (cur == kEmptyKey) {
+      if (!insert) return kNoSlot;
+      u64 prev = atomicCAS((unsigned long long*)kp, (unsigned long long)kEmptyKey,
+                           (unsigned long long)key);
+      if (prev == kEmptyKey) { claimed = true; return (u32)s; }
+      if (prev == key) return (u32)s;
+    }
+    s = (s + 1) & mask;
+  }
+  *t.overflow = 1u;
+  return kNoSlot;
+}
+
+// LR-FTRL fast path: 16-byte slots {key, n, z}; one dwordx4 load yields the
+// key and the optimizer state together.
+__global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp,
+                                                      const u64* __restrict__ keys,
+                                                      const int64_t* n_dev, int64_t n_host,
+                                                      int64_t n_max, bool insert,
+                                                      u32* __restrict__ out_slot,
+                                                      float* __restrict__ out_vals,
+                                                      const u32* __restrict__ out_map) {
+  int64_t n = dev_count(n_dev, n_host, n_max);
+  const u64 mask = t.cap - 1;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint4* slots = reinterpret_cast<uint4*>(t.words);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 key = sanitize_key(keys[i]);
+    u64 s = fmix64(key) & mask;
+    bool claimed = false;
+    u32 slot = kNoSlot;
+    float w = 0.0f;
+    for (u64 c = 0; c < t.cap; ++c) {
+      uint4 v = slots[s];
+      u64 cur = (u64)v.x | ((u64)v.y << 32);
+      if (cur == key) {
+        slot = (u32)s;
+        w = ftrl_weight(__uint_as_float(v.w), __uint_as_float(v.z), fp);
+        break;
+      }
+      if (cur == kEmptyKey) {
+        if (!insert) break;
+        u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[s]),
+                             (unsigned long long)kEmptyKey, (unsigned long long)key);
+        if (prev == kEmptyKey) { claimed = true; slot = (u32)s; break; }  // fresh state: w = 0
+        if (prev == key) {
+          slot = (u32)s;
+          // claimed by another lane this launch: state is still zero -> w = 0
+          break;
+        }
+      }
+      s = (s + 1) & mask;
+    }
+    if (insert && slot == kNoSlot) *t.overflow = 1u;
+    wave_append(t.size, claimed);
+    if (out_slot) out_slot[i] = slot;
+    if (out_vals) out_vals[out_map ? out_map[i] : i] = w;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_pull_generic(PullArgs a) {
+  int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const TableView& t = a.table;
+  const TableLayout& L = t.L;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u64 key = sanitize_key(a.keys[i]);
+    bool claimed = false;
+    u32 slot = probe(t, key, a.insert, claimed);
+    wave_append(t.size, claimed);
+    if (a.out_slot) a.out_slot[i] = slot;
+    if (a.out_vals) {
+      float* dst = a.out_vals + (size_t)(a.out_map ? a.out_map[i] : i) * a.pstride;
+      if (slot == kNoSlot) {
+        for (int p = 0; p < L.P; ++p) dst[p] = absent_weight(key, p, L, a.opt);
+      } else {
+        const u32* sp = t.words + (u64)slot * L.stride;
+        for (int p = 0; p < L.P; ++p) dst[p] = slot_weight(sp, key, p, L, a.opt);
+      }
+    }
+  }
+}
+
+void launch_table_pull(const PullArgs& a, hipStream_t st) {
+  if (a.n_max <= 0) return;
+  const TableLayout& L = a.table.L;
+  int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
+  if (L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag) {
+    hipLaunchKernelGGL(k_pull_lr16, dim3(grid), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
+                       a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map);
+  } else {
+    hipLaunchKernelGGL(k_pull_generic, dim3(grid), dim3(kBlock), 0, st, a);
+  }
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// apply (push)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float norm_grad(float raw, const int32_t* slice_rows, int s) {
+  return slice_rows ? (float)((double)raw / (double)slice_rows[s]) : raw;
+}
+
+// LR-FTRL, one slice, 16-byte slots: read (n,z) as one dwordx2, write it back.
+__global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
+  int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const FtrlParams fp = a.opt.ftrl;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u32 slot = a.slots[i];
+    u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+    float raw = a.grads[row];
+    if (a.zero_after) a.grads[row] = 0.0f;
+    if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
+    if (slot == kNoSlot) continue;
+    float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
+    float2 nz = *st;
+    float w = ftrl_weight(nz.y, nz.x, fp);
+    float g = norm_grad(raw, a.slice_rows, 0);
+    ftrl_push(nz.x, nz.y, w, g, fp);
+    *st = nz;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_apply_generic(ApplyArgs a) {
+  int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const TableView& t = a.table;
+  const TableLayout& L = t.L;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int S = a.S, ps = a.pstride, P = a.P;
+  const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u32 slot = a.slots[i];
+    u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+    float* g = a.grads + (size_t)row * S * ps;
+    u32 m = a.masks ? a.masks[row] : all;
+    if (slot != kNoSlot) {
+      u32* sp = t.words + (u64)slot * L.stride;
+      u64 key = *reinterpret_cast<u64*>(sp);
+      if (a.sum_slices) {
+        for (int p = 0; p < P; ++p) {
+          float acc = 0.0f;
+          for (int s = 0; s < S; ++s)
+            if (m & (1u << s)) acc += norm_grad(g[s * ps + p], a.slice_rows, s);
+          slot_push(sp, key, p, acc, L, a.opt);
+        }
+        if (L.has_flag) sp[L.flag_word] = 1u;
+      } else {
+        for (int s = 0; s < S; ++s) {
+          if (!(m & (1u << s))) continue;
+          for (int p = 0; p < P; ++p)
+            slot_push(sp, key, p, norm_grad(g[s * ps + p], a.slice_rows, s), L, a.opt);
+          if (L.has_flag) sp[L.flag_word] = 1u;
+        }
+      }
+    }
+    if (a.zero_after) {
+      for (int j = 0; j < S * ps; ++j) g[j] = 0.0f;
+      if (a.masks_rw) a.masks_rw[row] = 0u;
+    }
+    if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
+  }
+}
+
+void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
+  if (a.n_max <= 0) return;
+  const TableLayout& L = a.table.L;
+  int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
+  if (L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag && a.S == 1 && !a.masks &&
+      a.pstride == 1) {
+    hipLaunchKernelGGL(k_apply_lr16, dim3(grid), dim3(kBlock), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_apply_generic, dim3(grid), dim3(kBlock), 0, st, a);
+  }
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// worker-side gradient gather (multi-rank path): pos-indexed raw sums ->
+// owner-grouped send buffer, normalised per slice, source rows cleared.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_gather_grads(GatherGradArgs a) {
+  int64_t n = dev_count(a.n_dev, a.n_max, a.n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int S = a.S, ps = a.pstride, W = S * ps;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    u32 row = a.map[i];
+    float* src = a.grad_rw + (size_t)row * W;
+    float* dst = a.out + (size_t)i * W;
+    for (int s = 0; s < S; ++s)
+      for (int p = 0; p < ps; ++p) {
+        dst[s * ps + p] = norm_grad(src[s * ps + p], a.slice_rows, s);
+        src[s * ps + p] = 0.0f;
+      }
+    if (a.tmask_rw) {
+      a.out_mask[i] = a.tmask_rw[row];
+      a.tmask_rw[row] = 0u;
+    }
+  }
+}
+
+void launch_gather_grads(const GatherGradArgs& a, hipStream_t st) {
+  if (a.n_max <= 0) return;
+  hipLaunchKernelGGL(k_gather_grads, dim3(grid_for(a.n_max)), dim3(kBlock), 0, st, a);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// owner bucketing: counts per rank, then a block-aggregated scatter that
+// reserves each (block, owner) range with one global atomic.
+// ---------------------------------------------------------------------------
+constexpr int kBucketItems = 16;                 // items per thread
+constexpr int kBucketChunk = kBlock * kBucketItems;
+constexpr int kMaxWorld = 256;
+
+__global__ void __launch_bounds__(kBlock) k_bucket_count(const u64* __restrict__ keys,
+                                                         const int64_t* n_dev, int64_t n_max,
+                                                         int world,
+                                                         unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int hist[kMaxWorld];
+  for (int o = threadIdx.x; o < world; o += blockDim.x) hist[o] = 0;
+  __syncthreads();
+  int64_t n = dev_count(n_dev, n_max, n_max);
+  int64_t base = (int64_t)blockIdx.x * kBucketChunk;
+  for (int j = 0; j < kBucketItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+    if (i < n) atomicAdd(&hist[owner_of(keys[i], (u32)world)], 1u);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < world; o += blockDim.x)
+    if (hist[o]) atomicAdd(&counts[o], (unsigned long long)hist[o]);
+}
+
+__global__ void __launch_bounds__(kBlock) k_bucket_scatter(
+    const u64* __restrict__ keys, const u32* __restrict__ upos, const int64_t* n_dev,
+    int64_t n_max, int world, const unsigned long long* __restrict__ counts,
+    unsigned long long* __restrict__ cursor, u64* __restrict__ send_keys,
+    u32* __restrict__ send_pos) {
+  __shared__ unsigned int hist[kMaxWorld];
+  __shared__ unsigned long long base_of[kMaxWorld];
+  for (int o = threadIdx.x; o < world; o += blockDim.x) hist[o] = 0;
+  __syncthreads();
+  int64_t n = dev_count(n_dev, n_max, n_max);
+  int64_t base = (int64_t)blockIdx.x * kBucketChunk;
+  u32 own[kBucketItems];
+#pragma unroll
+  for (int j = 0; j < kBucketItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+    own[j] = (i < n) ? owner_of(keys[i], (u32)world) : 0xFFFFFFFFu;
+    if (own[j] != 0xFFFFFFFFu) atomicAdd(&hist[own[j]], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long off = 0;
+    for (int o = 0; o < world; ++o) {
+      unsigned long long c = counts[o];
+      base_of[o] = off + (hist[o] ? atomicAdd(&cursor[o], (unsigned long long)hist[o]) : 0ull);
+      off += c;
+    }
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < world; o += blockDim.x) hist[o] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kBucketItems; ++j) {
+    if (own[j] == 0xFFFFFFFFu) continue;
+    int64_t i = base + (int64_t)j * kBlock + threadIdx.x;
+    unsigned int r = atomicAdd(&hist[own[j]], 1u);
+    unsigned long long dst = base_of[own[j]] + r;
+    send_keys[dst] = keys[i];
+    send_pos[dst] = upos[i];
+  }
+}
+
+void launch_bucket(const BucketArgs& a, hipStream_t st) {
+  if (a.world > kMaxWorld) throw std::runtime_error("bucket: world size > 256 unsupported");
+  XF_HIP_CHECK(hipMemsetAsync(a.counts, 0, sizeof(int64_t) * a.world, st));
+  XF_HIP_CHECK(hipMemsetAsync(a.scratch, 0, sizeof(int64_t) * a.world, st));
+  if (a.n_max <= 0) return;
+  int grid = (int)((a.n_max + kBucketChunk - 1) / kBucketChunk);
+  hipLaunchKernelGGL(k_bucket_count, dim3(grid), dim3(kBlock), 0, st, a.uniq_keys, a.n_dev,
+                     a.n_max, a.world, reinterpret_cast<unsigned long long*>(a.counts));
+  hipLaunchKernelGGL(k_bucket_scatter, dim3(grid), dim3(kBlock), 0, st, a.uniq_keys, a.uniq_pos,
+                     a.n_dev, a.n_max, a.world,
+                     reinterpret_cast<const unsigned long long*>(a.counts),
+                     reinterpret_cast<unsigned long long*>(a.scratch), a.send_keys, a.send_pos);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// row gather / scatter helpers
+// ---------------------------------------------------------------------------
+__global__ void k_scatter_rows(const float* __restrict__ src, float* __restrict__ dst,
+                               const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
+                               int width) {
+  int64_t n = dev_count(n_dev, n_max, n_max) * width;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    int64_t i = e / width;
+    int c = (int)(e - i * width);
+    int64_t r = map ? (int64_t)map[i] : i;
+    dst[r * width + c] = src[e];
+  }
+}
+
+__global__ void k_gather_rows(const float* __restrict__ src, float* __restrict__ dst,
+                              const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
+                              int width, bool zero_src) {
+  int64_t n = dev_count(n_dev, n_max, n_max) * width;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    int64_t i = e / width;
+    int c = (int)(e - i * width);
+    int64_t r = (int64_t)map[i] * width + c;
+    dst[e] = src[r];
+    if (zero_src) const_cast<float*>(src)[r] = 0.0f;
+  }
+}
+
+__global__ void k_gather_u32(const u32* __restrict__ src, u32* __restrict__ dst,
+                             const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
+                             bool zero_src) {
+  int64_t n = dev_count(n_dev, n_max, n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    dst[i] = src[map[i]];
+    if (zero_src) const_cast<u32*>(src)[map[i]] = 0u;
+  }
+}
+
+__global__ void k_scatter_u32(const u32* __restrict__ src, u32* __restrict__ dst,
+                              const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max) {
+  int64_t n = dev_count(n_dev, n_max, n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[map[i]] = src[i];
+}
+
+void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                         int64_t n_max, int width, hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_scatter_rows, dim3(grid_for(n_max * width)), dim3(kBlock), 0, st, src, dst,
+                     map, n_dev, n_max, width);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+void launch_gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
+                        int64_t n_max, int width, bool zero_src, hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_gather_rows, dim3(grid_for(n_max * width)), dim3(kBlock), 0, st, src, dst,
+                     map, n_dev, n_max, width, zero_src);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+void launch_gather_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
+                       int64_t n_max, bool zero_src, hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_gather_u32, dim3(grid_for(n_max)), dim3(kBlock), 0, st, src, dst, map,
+                     n_dev, n_max, zero_src);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+void launch_scatter_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
+                        int64_t n_max, hipStream_t st) {
+  if (n_max <= 0) return;
+  hipLaunchKernelGGL(k_scatter_u32, dim3(grid_for(n_max)), dim3(kBlock), 0, st, src, dst, map,
+                     n_dev, n_max);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// checkpoint export / import
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_table_export(TableView t, u64* __restrict__ keys_out,
+                                                         u32* __restrict__ words_out,
+                                                         int64_t max_rows,
+                                                         unsigned long long* counter) {
+  const int W = t.L.stride - 2;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += stride) {
+    const u32* sp = t.words + s * (u64)t.L.stride;
+    u64 key = *reinterpret_cast<const u64*>(sp);
+    bool live = key != kEmptyKey;
+    unsigned long long idx = wave_append(counter, live);
+    if (live && (int64_t)idx < max_rows) {
+      keys_out[idx] = key;
+      for (int w = 0; w < W; ++w) words_out[idx * W + w] = sp[2 + w];
+    }
+  }
+}
+
+void launch_table_export(const TableView& t, u64* keys_out, u32* words_out, int64_t max_rows,
+                         unsigned long long* counter, hipStream_t st) {
+  XF_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(k_table_export, dim3(grid_for((int64_t)t.cap)), dim3(kBlock), 0, st, t,
+                     keys_out, words_out, max_rows, counter);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void __launch_bounds__(kBlock) k_table_import(TableView t, const u64* __restrict__ keys,
+                                                         const u32* __restrict__ words,
+                                                         int64_t n) {
+  const int W = t.L.stride - 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    bool claimed = false;
+    u32 slot = probe(t, sanitize_key(keys[i]), true, claimed);
+    wave_append(t.size, claimed);
+    if (slot == kNoSlot) continue;
+    u32* sp = t.words + (u64)slot * t.L.stride;
+    for (int w = 0; w < W; ++w) sp[2 + w] = words[i * W + w];
+  }
+}
+
+void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,
+                         hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_table_import, dim3(grid_for(n)), dim3(kBlock), 0, st, t, keys, words, n);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace xflow

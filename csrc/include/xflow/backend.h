@@ -1,0 +1,194 @@
+// xflow-amd: device backend interface.
+//
+// The engine (engine.cpp) is written once against this interface.  Two
+// implementations exist: HipBackend (gfx950 kernels, csrc/hip/*.hip) and
+// CpuBackend (csrc/cpu/cpu_backend.cpp) which runs the identical per-element
+// recipes from common.h/types.h on the host, single threaded and
+// deterministic.  The CPU backend exists for the reference "plumbing" config
+// (LR+SGD on bundled data without a GPU) and for multi-rank gloo tests; on a
+// GPU the HIP backend is the one that runs, and it fails loudly if missing.
+//
+// Every count argument that can be produced on the device is passed as a
+// pointer (`const int64_t* n_dev`) plus an upper bound (`n_max`), so a whole
+// single-GPU training step is launched without any host synchronisation.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+
+#include "xflow/types.h"
+
+namespace xflow {
+
+struct TableView {
+  u32* words = nullptr;      // slot array
+  u64 cap = 0;               // power of two
+  TableLayout L;
+  unsigned long long* size = nullptr;   // device counter: occupied slots
+  u32* overflow = nullptr;   // set when a probe wraps the whole table
+};
+
+struct ScratchView {           // per-step dedup table (keys only)
+  u64* keys = nullptr;         // [cap], kEmptyKey when free
+  u64 cap = 0;
+};
+
+struct DedupOut {
+  u32* pos = nullptr;          // [nnz] scratch slot of each occurrence
+  u64* uniq_keys = nullptr;    // [nnz_max]
+  u32* uniq_pos = nullptr;     // [nnz_max]
+  int64_t* n_uniq = nullptr;   // device counter
+  u32* overflow = nullptr;
+};
+
+struct FwdArgs {
+  BatchView batch;
+  const u32* pos = nullptr;        // [nnz]
+  const float* wpull = nullptr;    // [scratch_cap][pstride]
+  float* grad = nullptr;           // [scratch_cap][S][pstride] (null: forward only)
+  u32* tmask = nullptr;            // [scratch_cap] slice-touch bits (null unless S>1)
+  float* pctr = nullptr;           // [rows] optional
+  LossStats* stats = nullptr;      // accumulated (device)
+  ModelSpec model;
+  int S = 1;                       // slices in this batch
+};
+
+struct PullArgs {
+  TableView table;
+  OptSpec opt;
+  const u64* keys = nullptr;
+  const int64_t* n_dev = nullptr;  // count (device) or null => n_host
+  int64_t n_host = 0;
+  int64_t n_max = 0;
+  bool insert = true;
+  u32* out_slot = nullptr;         // [n] slot index (UINT32 max when absent)
+  float* out_vals = nullptr;       // rows of pstride floats
+  const u32* out_map = nullptr;    // row index for entry i (null => i)
+  int pstride = 1;
+};
+
+struct ApplyArgs {
+  TableView table;
+  OptSpec opt;
+  const u64* keys = nullptr;       // needed for latent init of un-pushed slots
+  const u32* slots = nullptr;
+  const int64_t* n_dev = nullptr;
+  int64_t n_host = 0;
+  int64_t n_max = 0;
+  float* grads = nullptr;          // rows of S*pstride floats
+  const u32* grad_map = nullptr;   // row index for entry i (null => i)
+  const u32* masks = nullptr;      // per-row slice bits (null => all S slices)
+  bool zero_after = false;         // clear consumed gradient rows (and masks)
+  u32* masks_rw = nullptr;         // masks buffer to clear when zero_after
+  int S = 1;
+  int pstride = 1;
+  int P = 1;
+  bool sum_slices = false;         // one push of Σ_s g_s instead of S ordered pushes
+  // Raw per-slice loss sums are divided by the slice's row count here, in
+  // double like lr_worker.cc:116-118 (null => rows already normalised).
+  const int32_t* slice_rows = nullptr;
+  // Optional fused reset of the worker dedup scratch (single-device path).
+  ScratchView scratch;
+  const u32* reset_pos = nullptr;
+};
+
+struct GatherGradArgs {           // worker: pos-indexed raw sums -> send order
+  const float* grad = nullptr;     // [scratch_cap][S][pstride], cleared after read
+  float* grad_rw = nullptr;        // same buffer (for clearing)
+  const u32* tmask = nullptr;      // optional slice bits, cleared after read
+  u32* tmask_rw = nullptr;
+  const u32* map = nullptr;        // send_pos
+  const int64_t* n_dev = nullptr;
+  int64_t n_max = 0;
+  int S = 1;
+  int pstride = 1;
+  const int32_t* slice_rows = nullptr;  // [S]
+  float* out = nullptr;            // [n][S*pstride] normalised gradients
+  u32* out_mask = nullptr;         // [n] (when tmask)
+};
+
+struct BucketArgs {                // group unique keys by owning rank
+  const u64* uniq_keys = nullptr;
+  const u32* uniq_pos = nullptr;
+  const int64_t* n_dev = nullptr;
+  int64_t n_max = 0;
+  int world = 1;
+  int64_t* counts = nullptr;       // [world] (device) out
+  u64* send_keys = nullptr;        // [n_max] out, grouped by owner
+  u32* send_pos = nullptr;         // [n_max] out
+  int64_t* scratch = nullptr;      // [2*world] workspace
+};
+
+struct SynthArgs {                 // synthetic Criteo-shaped batch generator
+  u64* keys = nullptr;
+  float* labels = nullptr;
+  int32_t* fgid = nullptr;         // optional
+  int64_t rows = 0;
+  int fields = 39;
+  const uint64_t* vocab = nullptr;    // [fields] cardinalities (host or device per backend)
+  const float* zipf_s = nullptr;      // [fields] exponents
+  uint64_t hash_space = 1000000000ull;
+  uint64_t seed = 0;
+  uint64_t step = 0;
+  float planted_scale = 0.3f;
+  float planted_bias = -1.2f;
+};
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual bool is_gpu() const = 0;
+  virtual std::string name() const = 0;
+
+  // memory
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void free(void* p) = 0;
+  virtual void memset(void* p, int v, size_t bytes) = 0;
+  virtual void fill_u64(u64* p, u64 v, size_t n) = 0;
+  virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;
+  virtual void copy_d2h(void* dst, const void* src, size_t bytes) = 0;  // synchronising
+  virtual void copy_d2d(void* dst, const void* src, size_t bytes) = 0;
+  virtual void synchronize() = 0;
+  virtual void set_stream(void* stream) = 0;
+  virtual void* stream() const = 0;
+
+  // kernels
+  // Mark every slot free (key words = kEmptyKey) with zero optimizer state.
+  virtual void table_clear(const TableView& t) = 0;
+  virtual void dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o) = 0;
+  virtual void scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev,
+                             int64_t n_max) = 0;
+  virtual void table_pull(const PullArgs& a) = 0;
+  virtual void table_apply(const ApplyArgs& a) = 0;
+  virtual void forward_backward(const FwdArgs& a) = 0;
+  virtual void slice_masks(const BatchView& b, const u32* pos, u32* tmask) = 0;
+  virtual void bucket(const BucketArgs& a) = 0;
+  virtual void gather_grads(const GatherGradArgs& a) = 0;
+  // rows of `width` floats: dst[map? map[i] : i] = src[i]   (scatter)
+  virtual void scatter_rows(const float* src, float* dst, const u32* map,
+                            const int64_t* n_dev, int64_t n_max, int width) = 0;
+  // dst[i] = src[map[i]]; optionally zero the source row   (gather)
+  virtual void gather_rows(const float* src, float* dst, const u32* map,
+                           const int64_t* n_dev, int64_t n_max, int width,
+                           bool zero_src) = 0;
+  virtual void gather_u32(const u32* src, u32* dst, const u32* map,
+                          const int64_t* n_dev, int64_t n_max, bool zero_src) = 0;
+  virtual void scatter_u32(const u32* src, u32* dst, const u32* map,
+                           const int64_t* n_dev, int64_t n_max) = 0;
+  virtual void synth_batch(const SynthArgs& a) = 0;
+  // count occupied slots / dump table rows (checkpointing); returns rows written
+  virtual int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
+                               int64_t max_rows) = 0;
+  virtual void table_import(const TableView& t, const u64* keys, const u32* words,
+                            int64_t n) = 0;
+};
+
+std::unique_ptr<Backend> make_cpu_backend();
+// Defined in csrc/hip/hip_backend.hip; ordinal = HIP device index.
+std::unique_ptr<Backend> make_hip_backend(int device);
+bool hip_backend_available();
+
+}  // namespace xflow

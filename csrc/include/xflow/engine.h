@@ -1,0 +1,148 @@
+// xflow-amd: Engine — one rank's sparse CTR trainer state and step pipeline.
+//
+// A rank plays both ps-lite roles of the reference at once:
+//   worker  (lr_worker.cc / fm_worker.cc / mvm_worker.cc): dedups a batch's
+//           keys, forward/backward over its rows, produces per-(key, slice)
+//           gradient sums;
+//   server  (ftrl.h / sgd.h via server.h): owns a shard of the HBM hash table
+//           and answers pulls / applies pushes for the keys it owns.
+// Single-rank training fuses both (train_step); multi-rank training drives the
+// phase methods from the distributed layer with sparse all-to-alls between
+// them (xflow_amd/parallel/sparse_a2a.py).
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "xflow/backend.h"
+
+namespace xflow {
+
+struct EngineConfig {
+  ModelSpec model;
+  OptSpec opt;
+  int table_log2_cap = 20;     // slots = 2^table_log2_cap (<= 2^31)
+  int64_t max_rows = 1 << 16;  // per step
+  int64_t max_nnz = 1 << 22;   // per step
+  int max_slices = 1;          // slices per step (<= 32)
+  bool sum_slices = false;     // apply Σ_s g_s once instead of ordered per-slice pushes
+  double scratch_factor = 1.25;  // dedup scratch capacity = pow2 >= factor * max_nnz
+  int device = -1;             // -1 => CPU backend, else HIP device ordinal
+};
+
+class Engine {
+ public:
+  explicit Engine(const EngineConfig& cfg);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  const EngineConfig& config() const { return cfg_; }
+  Backend& backend() { return *be_; }
+  bool is_gpu() const { return be_->is_gpu(); }
+  void set_stream(void* s) { be_->set_stream(s); }
+  void synchronize() { be_->synchronize(); }
+
+  // ---- single-rank fused step -------------------------------------------
+  // Batch pointers are backend memory (device pointers on the HIP backend).
+  void train_step(const BatchView& b);
+  // Forward only; pctr (backend memory, may be null) receives predictions.
+  // Keys are looked up without insertion.
+  void eval_step(const BatchView& b, float* pctr);
+
+  // Push explicit gradients (host arrays) to keys, like the reference's
+  // initialisation pushes (lr_worker.cc:180-182, fm_worker.cc:248-252).
+  void push_host(const std::vector<u64>& keys, const std::vector<float>& grads);
+  // Pull current values (host) of keys without inserting them.
+  std::vector<float> pull_host(const std::vector<u64>& keys);
+
+  // ---- multi-rank phases --------------------------------------------------
+  // worker: dedup the batch and group its unique keys by owner rank.
+  // counts_out: backend int64[world]; send_keys_out: backend u64[>= n_unique].
+  void w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out);
+  // server: probe/insert n received keys, write pulled rows (pstride floats)
+  // into out_vals (backend memory), remember slots for s_apply.
+  void s_pull(const u64* recv_keys, int64_t n, float* out_vals);
+  // worker: place pulled rows (in send order) into the pos-indexed buffer,
+  // run forward/backward, then emit normalised gradients in send order.
+  // grads_out: [n_send][S*pstride]; masks_out: [n_send] (used when S>1).
+  void w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
+                          float* grads_out, u32* masks_out);
+  // server: apply received gradients source by source (deterministic order).
+  // src_offsets has world+1 entries delimiting each source's rows.
+  void s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
+               const std::vector<int64_t>& src_offsets, int S);
+  // worker: release the per-step dedup scratch.
+  void w_finish();
+
+  // ---- stats / introspection -------------------------------------------
+  // which = 0: training forward passes, 1: eval_step passes.
+  LossStats read_stats(bool reset, int which = 0);
+  int64_t n_unique();            // unique keys of the last prepared batch (syncs)
+  int64_t table_size();          // occupied slots (syncs)
+  uint64_t table_capacity() const { return table_.cap; }
+  size_t table_bytes() const { return table_bytes_; }
+  bool overflowed();
+  int pstride() const { return cfg_.model.pstride(); }
+  int slices_of(const BatchView& b) const;
+
+  // ---- checkpoint ------------------------------------------------------
+  // Host copies of every live slot: keys + (stride-2) state words each.
+  void export_table(std::vector<u64>& keys, std::vector<u32>& words);
+  void import_table(const std::vector<u64>& keys, const std::vector<u32>& words);
+  int state_words() const { return table_.L.stride - 2; }
+  // Binary shard file: header + keys + state words.
+  void save(const std::string& path);
+  void load(const std::string& path);
+
+  // Synthetic Criteo-shaped batch into engine-owned staging buffers.
+  BatchView synth_batch(const SynthArgs& a, int64_t slice_rows);
+  // Copy a host CSR batch into engine-owned staging buffers.
+  BatchView stage_host_batch(const BatchView& host);
+
+ private:
+  void ensure_server_capacity(int64_t n);
+  const int32_t* slice_rows_dev(const BatchView& b, int S);
+  void dedup_(const BatchView& b);
+
+  EngineConfig cfg_;
+  std::unique_ptr<Backend> be_;
+  TableView table_;
+  size_t table_bytes_ = 0;
+  ScratchView scratch_;
+
+  // worker buffers (backend memory)
+  u32* pos_ = nullptr;          // [max_nnz]
+  u64* uniq_keys_ = nullptr;    // [max_nnz]
+  u32* uniq_pos_ = nullptr;     // [max_nnz]
+  u32* uniq_slot_ = nullptr;    // [max_nnz]
+  int64_t* n_uniq_ = nullptr;   // [1]
+  u32* overflow_ = nullptr;     // [2]: scratch, table
+  float* wpull_ = nullptr;      // [scratch_cap * pstride]
+  float* grad_ = nullptr;       // [scratch_cap * max_slices * pstride]
+  u32* tmask_ = nullptr;        // [scratch_cap]
+  LossStats* stats_ = nullptr;  // [1]
+  u32* send_pos_ = nullptr;     // [max_nnz]
+  int64_t* bucket_ws_ = nullptr;  // [2*256]
+  int32_t* slice_rows_ = nullptr;  // [32]
+  int64_t cached_rows_ = -1, cached_slice_rows_ = -1;
+  int64_t last_nsend_ = 0;
+
+  // staging batch buffers (backend memory)
+  u64* st_keys_ = nullptr;
+  int32_t* st_rowptr_ = nullptr;
+  int32_t* st_fgid_ = nullptr;
+  float* st_labels_ = nullptr;
+
+  // server buffers
+  u32* srv_slots_ = nullptr;
+  int64_t srv_cap_ = 0;
+  int64_t srv_n_ = 0;
+
+  u64* host_keys_dev_ = nullptr;   // push_host / pull_host staging
+  float* host_vals_dev_ = nullptr;
+  int64_t host_cap_ = 0;
+};
+
+}  // namespace xflow

@@ -1,0 +1,134 @@
+// xflow-amd: model / table / batch descriptors shared by both backends.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "xflow/common.h"
+
+namespace xflow {
+
+// Model families of the reference (src/model/{lr,fm,mvm}).
+enum ModelKind : int { kLR = 0, kFM = 1, kMVM = 2 };
+enum OptKind : int { kFTRL = 0, kSGD = 1 };
+
+// FM interaction math.  kFmReference reproduces fm_worker.cc:159-202 /
+// :126-157 (y = wx + (Σ_k Σ_f v)^2 - Σ_k Σ_f v^2, w-grad accumulated D times);
+// kFmStandard is Rendle's ½Σ_k[(Σ_f v_fk)^2 - Σ_f v_fk^2].
+enum FmMath : int { kFmReference = 0, kFmStandard = 1 };
+
+// MVM field-product range.  kMvmCompat multiplies fields [0, max_fgid) like
+// mvm_worker.cc:198-203 (the max field's sum is written out of bounds there
+// and never multiplied); kMvmFixed multiplies [0, max_fgid].
+enum MvmMath : int { kMvmCompat = 0, kMvmFixed = 1 };
+
+// Parameters per hashed key.  LR: [w]; FM: [w, v_0..v_{D-1}]; MVM: [v_0..].
+// Params with index >= p_w are latent ("v") params: lazily random-initialised
+// (FTRL, ftrl.h:114-120) or constant-initialised (SGD, sgd.h:69) until their
+// first push, tracked by one per-slot "pushed" flag.
+struct ModelSpec {
+  int kind = kLR;
+  int v_dim = 10;   // fm_worker.h:92 / mvm_worker.h:92
+  int fm_math = kFmReference;
+  int mvm_math = kMvmCompat;
+  int max_fields = 64;  // MVM per-row field buckets (device LDS budget)
+
+  XF_HD int P() const { return kind == kLR ? 1 : (kind == kFM ? 1 + v_dim : v_dim); }
+  XF_HD int p_w() const { return kind == kMVM ? 0 : 1; }
+  // Stride (floats) of one key's row in the pulled-weights / gradient buffers:
+  // 1 for LR, otherwise padded to 16 bytes so kernels use dwordx4 accesses.
+  XF_HD int pstride() const { int p = P(); return p == 1 ? 1 : ((p + 3) & ~3); }
+};
+
+struct OptSpec {
+  int kind = kFTRL;
+  FtrlParams ftrl;
+  SgdParams sgd;
+  float v_init_scale = 1e-2f;  // ftrl.h:117
+  uint64_t seed = 0x5eed;
+};
+
+// Slot layout of the HBM-resident open-addressing table, in 32-bit words:
+//   [0,1]  u64 key (kEmptyKey when free)
+//   [2, 2+sp*P)  optimizer state: FTRL (n,z) pairs, SGD w
+//   [2+sp*P]     pushed flag (only when the model has latent params)
+// padded to a multiple of 4 words (16 B).  LR-FTRL is exactly 16 B/slot.
+struct TableLayout {
+  int P = 1;
+  int p_w = 1;
+  int opt = kFTRL;
+  int sp = 2;          // state words per param
+  int has_flag = 0;
+  int flag_word = 0;
+  int stride = 4;      // words per slot
+
+  static TableLayout make(const ModelSpec& m, const OptSpec& o) {
+    TableLayout t;
+    t.P = m.P();
+    t.p_w = m.p_w();
+    t.opt = o.kind;
+    t.sp = (o.kind == kFTRL) ? 2 : 1;
+    t.has_flag = (t.P > t.p_w) ? 1 : 0;
+    t.flag_word = 2 + t.sp * t.P;
+    int words = 2 + t.sp * t.P + t.has_flag;
+    t.stride = (words + 3) & ~3;
+    return t;
+  }
+};
+
+// Current weight of param p stored in `slot` (reference pull semantics).
+XF_HD float slot_weight(const u32* slot, u64 key, int p, const TableLayout& L,
+                        const OptSpec& o) {
+  const float* st = reinterpret_cast<const float*>(slot + 2);
+  bool latent = p >= L.p_w;
+  if (latent && L.has_flag && slot[L.flag_word] == 0u) {
+    return L.opt == kFTRL ? normal_init(key, (u32)(p - L.p_w), o.seed) * o.v_init_scale
+                          : o.sgd.v_init;
+  }
+  if (L.opt == kFTRL) return ftrl_weight(st[2 * p + 1], st[2 * p], o.ftrl);
+  return st[p];
+}
+
+// Weight of a key that is not in the table (lookup-only pulls at eval time).
+XF_HD float absent_weight(u64 key, int p, const TableLayout& L, const OptSpec& o) {
+  if (p >= L.p_w) {
+    return L.opt == kFTRL ? normal_init(key, (u32)(p - L.p_w), o.seed) * o.v_init_scale
+                          : o.sgd.v_init;
+  }
+  return 0.0f;
+}
+
+// Apply one push of gradient g to param p of `slot` (slot lock-free: callers
+// guarantee a single writer per slot per launch).
+XF_HD void slot_push(u32* slot, u64 key, int p, float g, const TableLayout& L,
+                     const OptSpec& o) {
+  float w = slot_weight(slot, key, p, L, o);
+  float* st = reinterpret_cast<float*>(slot + 2);
+  if (L.opt == kFTRL) {
+    ftrl_push(st[2 * p], st[2 * p + 1], w, g, o.ftrl);
+  } else {
+    st[p] = w - o.sgd.lr * g;
+  }
+}
+
+// A batch in CSR form (device or host pointers, depending on the backend).
+struct BatchView {
+  const u64* keys = nullptr;      // [nnz]
+  const int32_t* row_ptr = nullptr;  // [rows+1]; null => fixed nnz_per_row
+  const int32_t* fgid = nullptr;  // [nnz], MVM only
+  const float* labels = nullptr;  // [rows], 0/1
+  int64_t rows = 0;
+  int64_t nnz = 0;
+  int nnz_per_row = 0;            // used when row_ptr == null
+  int64_t slice_rows = 0;         // rows per slice (gradient normaliser); 0 => rows
+};
+
+// Loss statistics accumulated by forward passes (device or host memory).
+struct LossStats {
+  double ln_loss;      // Σ -[y ln p + (1-y) ln(1-p)], p clipped to [1e-7, 1-1e-7]
+  double log2_lik;     // Σ  [y log2 p + (1-y) log2(1-p)] (reference print, base.h:97-101)
+  double rows;
+  double positives;
+};
+
+}  // namespace xflow

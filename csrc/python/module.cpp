@@ -1,0 +1,343 @@
+// xflow-amd: Python bindings (pybind11) of the native core.
+//
+// Device buffers cross the boundary as integer addresses (torch's
+// tensor.data_ptr()) so the module has no libtorch dependency; the Python
+// layer (xflow_amd/engine.py) owns shape/dtype/device checks.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "xflow/engine.h"
+#include "xflow/reader.h"
+#include "xflow/trainer.h"
+
+namespace py = pybind11;
+using namespace xflow;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t a) {
+  return reinterpret_cast<T*>(a);
+}
+
+template <typename T>
+py::array_t<T> to_np(const std::vector<T>& v) {
+  py::array_t<T> a((py::ssize_t)v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), sizeof(T) * v.size());
+  return a;
+}
+
+py::dict block_to_dict(const CsrBlock& b) {
+  py::dict d;
+  d["row_ptr"] = to_np(b.row_ptr);
+  d["keys"] = to_np(b.keys);
+  d["fgid"] = to_np(b.fgid);
+  d["labels"] = to_np(b.labels);
+  d["max_fgid"] = b.max_fgid;
+  return d;
+}
+
+py::dict stats_dict(const LossStats& s) {
+  py::dict d;
+  d["ln_loss"] = s.ln_loss;
+  d["log2_lik"] = s.log2_lik;
+  d["rows"] = s.rows;
+  d["positives"] = s.positives;
+  return d;
+}
+
+ModelSpec model_from(py::dict d) {
+  ModelSpec m;
+  if (d.contains("kind")) m.kind = d["kind"].cast<int>();
+  if (d.contains("v_dim")) m.v_dim = d["v_dim"].cast<int>();
+  if (d.contains("fm_math")) m.fm_math = d["fm_math"].cast<int>();
+  if (d.contains("mvm_math")) m.mvm_math = d["mvm_math"].cast<int>();
+  return m;
+}
+
+OptSpec opt_from(py::dict d) {
+  OptSpec o;
+  if (d.contains("kind")) o.kind = d["kind"].cast<int>();
+  if (d.contains("alpha")) o.ftrl.alpha = d["alpha"].cast<float>();
+  if (d.contains("beta")) o.ftrl.beta = d["beta"].cast<float>();
+  if (d.contains("lambda1")) o.ftrl.lambda1 = d["lambda1"].cast<float>();
+  if (d.contains("lambda2")) o.ftrl.lambda2 = d["lambda2"].cast<float>();
+  if (d.contains("lr")) o.sgd.lr = d["lr"].cast<float>();
+  if (d.contains("sgd_v_init")) o.sgd.v_init = d["sgd_v_init"].cast<float>();
+  if (d.contains("v_init_scale")) o.v_init_scale = d["v_init_scale"].cast<float>();
+  if (d.contains("seed")) o.seed = d["seed"].cast<uint64_t>();
+  return o;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_xflow_native, m) {
+  m.doc() = "xflow-amd native core: HBM hash-table engine, gfx950 kernels, libffm reader";
+
+  m.def("hip_available", &hip_backend_available);
+  m.def("feature_hash", [](py::bytes b) {
+    std::string s = b;
+    return feature_hash(s.data(), s.size());
+  });
+  m.def("parse_libffm", [](py::bytes b) {
+    std::string s = b;
+    CsrBlock blk;
+    parse_libffm(s.data(), s.size(), blk);
+    return block_to_dict(blk);
+  });
+  m.def("reference_auc", [](py::array_t<int32_t> labels, py::array_t<float> pctr) {
+    auto l = labels.unchecked<1>();
+    auto p = pctr.unchecked<1>();
+    std::vector<std::pair<int, float>> v;
+    for (py::ssize_t i = 0; i < l.shape(0); ++i) v.emplace_back(l(i), p(i));
+    EvalResult r = reference_auc(v);
+    py::dict d;
+    d["logloss_printed"] = r.logloss_printed;
+    d["ln_logloss"] = r.ln_logloss;
+    d["auc"] = r.auc;
+    d["tp"] = r.tp;
+    d["n"] = r.n;
+    d["line"] = r.line;
+    return d;
+  });
+
+  py::class_<BatchView>(m, "BatchView")
+      .def(py::init<>())
+      .def_property("keys", [](const BatchView& b) { return (uintptr_t)b.keys; },
+                    [](BatchView& b, uintptr_t v) { b.keys = P<const u64>(v); })
+      .def_property("row_ptr", [](const BatchView& b) { return (uintptr_t)b.row_ptr; },
+                    [](BatchView& b, uintptr_t v) { b.row_ptr = P<const int32_t>(v); })
+      .def_property("fgid", [](const BatchView& b) { return (uintptr_t)b.fgid; },
+                    [](BatchView& b, uintptr_t v) { b.fgid = P<const int32_t>(v); })
+      .def_property("labels", [](const BatchView& b) { return (uintptr_t)b.labels; },
+                    [](BatchView& b, uintptr_t v) { b.labels = P<const float>(v); })
+      .def_readwrite("rows", &BatchView::rows)
+      .def_readwrite("nnz", &BatchView::nnz)
+      .def_readwrite("nnz_per_row", &BatchView::nnz_per_row)
+      .def_readwrite("slice_rows", &BatchView::slice_rows);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,
+                       int64_t max_nnz, int max_slices, bool sum_slices, double scratch_factor,
+                       int device) {
+             EngineConfig c;
+             c.model = model_from(model);
+             c.opt = opt_from(opt);
+             c.table_log2_cap = table_log2_cap;
+             c.max_rows = max_rows;
+             c.max_nnz = max_nnz;
+             c.max_slices = max_slices;
+             c.sum_slices = sum_slices;
+             c.scratch_factor = scratch_factor;
+             c.device = device;
+             return new Engine(c);
+           }),
+           py::arg("model"), py::arg("opt"), py::arg("table_log2_cap") = 20,
+           py::arg("max_rows") = 1 << 16, py::arg("max_nnz") = 1 << 22,
+           py::arg("max_slices") = 1, py::arg("sum_slices") = false,
+           py::arg("scratch_factor") = 1.25, py::arg("device") = -1)
+      .def_property_readonly("is_gpu", &Engine::is_gpu)
+      .def_property_readonly("backend_name", [](Engine& e) { return e.backend().name(); })
+      .def_property_readonly("pstride", &Engine::pstride)
+      .def_property_readonly("P", [](Engine& e) { return e.config().model.P(); })
+      .def_property_readonly("state_words", &Engine::state_words)
+      .def_property_readonly("table_capacity", &Engine::table_capacity)
+      .def_property_readonly("table_bytes", &Engine::table_bytes)
+      .def("set_stream", [](Engine& e, uintptr_t s) { e.set_stream(reinterpret_cast<void*>(s)); })
+      .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("train_step", &Engine::train_step, py::call_guard<py::gil_scoped_release>())
+      .def("eval_step",
+           [](Engine& e, const BatchView& b, uintptr_t pctr) { e.eval_step(b, P<float>(pctr)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("slices_of", &Engine::slices_of)
+      .def("push_host",
+           [](Engine& e, py::array_t<uint64_t> keys, py::array_t<float> grads) {
+             std::vector<u64> k(keys.data(), keys.data() + keys.size());
+             std::vector<float> g(grads.data(), grads.data() + grads.size());
+             e.push_host(k, g);
+           })
+      .def("pull_host",
+           [](Engine& e, py::array_t<uint64_t> keys) {
+             std::vector<u64> k(keys.data(), keys.data() + keys.size());
+             return to_np(e.pull_host(k));
+           })
+      .def("w_prepare",
+           [](Engine& e, const BatchView& b, int world, uintptr_t counts, uintptr_t send_keys) {
+             e.w_prepare(b, world, P<int64_t>(counts), P<u64>(send_keys));
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("s_pull",
+           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out) {
+             e.s_pull(P<const u64>(keys), n, P<float>(out));
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("w_forward_backward",
+           [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t grads,
+              uintptr_t masks) {
+             e.w_forward_backward(b, P<const float>(pulled), n_send, P<float>(grads),
+                                  P<u32>(masks));
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("s_apply",
+           [](Engine& e, uintptr_t keys, uintptr_t grads, uintptr_t masks,
+              std::vector<int64_t> offsets, int S) {
+             e.s_apply(P<const u64>(keys), P<const float>(grads), P<const u32>(masks), offsets, S);
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def("w_finish", &Engine::w_finish)
+      .def("read_stats",
+           [](Engine& e, bool reset, int which) { return stats_dict(e.read_stats(reset, which)); },
+           py::arg("reset") = false, py::arg("which") = 0)
+      .def("n_unique", &Engine::n_unique)
+      .def("table_size", &Engine::table_size)
+      .def("overflowed", &Engine::overflowed)
+      .def("export_table",
+           [](Engine& e) {
+             std::vector<u64> k;
+             std::vector<u32> w;
+             e.export_table(k, w);
+             return py::make_tuple(to_np(k), to_np(w));
+           })
+      .def("import_table",
+           [](Engine& e, py::array_t<uint64_t> keys, py::array_t<uint32_t> words) {
+             std::vector<u64> k(keys.data(), keys.data() + keys.size());
+             std::vector<u32> w(words.data(), words.data() + words.size());
+             e.import_table(k, w);
+           })
+      .def("save", &Engine::save)
+      .def("load", &Engine::load)
+      .def("synth_batch",
+           [](Engine& e, int64_t rows, std::vector<uint64_t> vocab, std::vector<float> zipf,
+              uint64_t hash_space, uint64_t seed, uint64_t step, float scale, float bias,
+              int64_t slice_rows, uintptr_t keys, uintptr_t labels, uintptr_t fgid) {
+             SynthArgs a;
+             a.keys = P<u64>(keys);
+             a.labels = P<float>(labels);
+             a.fgid = P<int32_t>(fgid);
+             a.rows = rows;
+             a.fields = (int)vocab.size();
+             a.vocab = vocab.data();
+             a.zipf_s = zipf.data();
+             a.hash_space = hash_space;
+             a.seed = seed;
+             a.step = step;
+             a.planted_scale = scale;
+             a.planted_bias = bias;
+             return e.synth_batch(a, slice_rows);
+           },
+           py::arg("rows"), py::arg("vocab"), py::arg("zipf"), py::arg("hash_space"),
+           py::arg("seed"), py::arg("step"), py::arg("scale"), py::arg("bias"),
+           py::arg("slice_rows"), py::arg("keys") = 0, py::arg("labels") = 0,
+           py::arg("fgid") = 0)
+      .def("stage_host_batch",
+           [](Engine& e, py::array_t<uint64_t> keys, py::object row_ptr, py::object fgid,
+              py::array_t<float> labels, int nnz_per_row, int64_t slice_rows) {
+             BatchView h;
+             h.keys = keys.data();
+             h.nnz = keys.size();
+             h.labels = labels.data();
+             h.rows = labels.size();
+             std::vector<int32_t> rp, fg;
+             if (!row_ptr.is_none()) {
+               auto a = row_ptr.cast<py::array_t<int32_t>>();
+               rp.assign(a.data(), a.data() + a.size());
+               h.row_ptr = rp.data();
+             }
+             if (!fgid.is_none()) {
+               auto a = fgid.cast<py::array_t<int32_t>>();
+               fg.assign(a.data(), a.data() + a.size());
+               h.fgid = fg.data();
+             }
+             h.nnz_per_row = nnz_per_row;
+             h.slice_rows = slice_rows;
+             return e.stage_host_batch(h);
+           });
+
+  py::class_<BlockReader>(m, "BlockReader")
+      .def(py::init<const std::string&, size_t>())
+      .def("next",
+           [](BlockReader& r) -> py::object {
+             CsrBlock b;
+             if (!r.next(b)) return py::none();
+             return block_to_dict(b);
+           })
+      .def("rewind", &BlockReader::rewind);
+
+  py::class_<PrefetchReader>(m, "PrefetchReader")
+      .def(py::init<const std::string&, size_t>())
+      .def("next", [](PrefetchReader& r) -> py::object {
+        CsrBlock b;
+        bool ok;
+        {
+          py::gil_scoped_release rel;
+          ok = r.next(b);
+        }
+        if (!ok) return py::none();
+        return block_to_dict(b);
+      });
+
+  py::class_<LoadData>(m, "LoadData")
+      .def(py::init([](const std::string& p, size_t bs) { return new LoadData(p.c_str(), bs); }))
+      .def("load_minibatch_hash_data_fread", &LoadData::load_minibatch_hash_data_fread)
+      .def_property_readonly("label", [](LoadData& l) { return l.m_data.label; })
+      .def_property_readonly("fea_matrix", [](LoadData& l) {
+        py::list rows;
+        for (auto& r : l.m_data.fea_matrix) {
+          py::list row;
+          for (auto& f : r) row.append(py::make_tuple(f.fgid, (uint64_t)f.fid));
+          rows.append(row);
+        }
+        return rows;
+      });
+
+  py::class_<Trainer>(m, "Trainer")
+      .def(py::init([](py::dict d) {
+        TrainerConfig c;
+        c.train_prefix = d["train_prefix"].cast<std::string>();
+        c.test_prefix = d["test_prefix"].cast<std::string>();
+        if (d.contains("model")) c.model = d["model"].cast<int>();
+        if (d.contains("epochs")) c.epochs = d["epochs"].cast<int>();
+        if (d.contains("threads")) c.threads = d["threads"].cast<int>();
+        if (d.contains("train_block_bytes")) c.train_block_bytes = d["train_block_bytes"].cast<int64_t>();
+        if (d.contains("test_block_bytes")) c.test_block_bytes = d["test_block_bytes"].cast<int64_t>();
+        if (d.contains("serial_slices")) c.serial_slices = d["serial_slices"].cast<bool>();
+        if (d.contains("keep_remainder")) c.keep_remainder = d["keep_remainder"].cast<bool>();
+        if (d.contains("mvm_predict_compat")) c.mvm_predict_compat = d["mvm_predict_compat"].cast<bool>();
+        if (d.contains("init_push")) c.init_push = d["init_push"].cast<bool>();
+        if (d.contains("rank")) c.rank = d["rank"].cast<int>();
+        if (d.contains("pred_dir")) c.pred_dir = d["pred_dir"].cast<std::string>();
+        if (d.contains("device")) c.device = d["device"].cast<int>();
+        if (d.contains("table_log2_cap")) c.table_log2_cap = d["table_log2_cap"].cast<int>();
+        if (d.contains("sum_slices")) c.sum_slices = d["sum_slices"].cast<bool>();
+        if (d.contains("verbose")) c.verbose = d["verbose"].cast<bool>();
+        if (d.contains("model_spec")) c.model_spec = model_from(d["model_spec"].cast<py::dict>());
+        if (d.contains("opt")) c.opt = opt_from(d["opt"].cast<py::dict>());
+        return new Trainer(c);
+      }))
+      .def("train", &Trainer::train, py::call_guard<py::gil_scoped_release>())
+      .def("train_epochs", &Trainer::train_epochs, py::call_guard<py::gil_scoped_release>())
+      .def("predict",
+           [](Trainer& t, int block) {
+             EvalResult r;
+             {
+               py::gil_scoped_release rel;
+               r = t.predict(block);
+             }
+             py::dict d;
+             d["logloss_printed"] = r.logloss_printed;
+             d["ln_logloss"] = r.ln_logloss;
+             d["auc"] = r.auc;
+             d["tp"] = r.tp;
+             d["n"] = r.n;
+             d["line"] = r.line;
+             return d;
+           },
+           py::arg("block") = 0)
+      .def_property_readonly("threads", &Trainer::threads)
+      .def_property_readonly("engine", &Trainer::engine, py::return_value_policy::reference_internal);
+}

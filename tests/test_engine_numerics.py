@@ -1,0 +1,75 @@
+"""Engine (native C++ CPU backend and gfx950 HIP backend) vs the plain PyTorch
+fp32 reference step (xflow_amd/testing/torch_ref.py), for every model family,
+both optimizers, single- and multi-slice batches."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import random_csr, to_batch
+from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+from xflow_amd.engine import Engine
+from xflow_amd.testing import torch_ref
+from xflow_amd.testing.hashing import normal_init
+
+CASES = [
+    ("lr", "ftrl", "reference", "compat", 1),
+    ("lr", "ftrl", "reference", "compat", 4),
+    ("lr", "sgd", "reference", "compat", 1),
+    ("fm", "ftrl", "reference", "compat", 1),
+    ("fm", "ftrl", "standard", "compat", 3),
+    ("fm", "sgd", "standard", "compat", 1),
+    ("mvm", "ftrl", "reference", "compat", 1),
+    ("mvm", "ftrl", "reference", "fixed", 2),
+]
+
+
+def _run(device, kind, opt, fm_math, mvm_math, slices, steps=3, rows=96, v_dim=4):
+    m = ModelConfig(kind=kind, v_dim=v_dim, fm_math=fm_math, mvm_math=mvm_math)
+    o = OptimConfig(kind=opt)
+    eng = Engine(m, o, EngineConfig(table_log2_cap=14, max_rows=rows, max_nnz=rows * 16,
+                                    max_slices=slices), device=device)
+    P = m.params_per_key
+    ref = torch_ref.RefTable(P, 0 if kind == "mvm" else 1, opt,
+                             init_fn=lambda k, d: normal_init(k, d) * np.float32(1e-2))
+    slice_rows = rows // slices
+    for step in range(steps):
+        keys, rp, fg, lab = random_csr(rows, fields=6, vocab=60, seed=100 + step)
+        b = to_batch(keys, rp, fg, lab, device, slice_rows=slice_rows)
+        eng.train_step(b)
+        torch_ref.train_step(ref, kind, keys, lab, rp, slice_rows, fg, fm_math, mvm_math)
+    # all keys seen
+    allk = np.unique(np.concatenate([random_csr(rows, 6, 60, 100 + s)[0] for s in range(steps)]))
+    got = eng.pull(allk)
+    want = ref.weights(allk, insert=False).numpy()
+    assert eng.table_size() == len(allk)
+    return got, want, eng
+
+
+@pytest.mark.parametrize("kind,opt,fm_math,mvm_math,slices", CASES)
+def test_engine_matches_torch_reference_cpu(kind, opt, fm_math, mvm_math, slices):
+    got, want, _ = _run(torch.device("cpu"), kind, opt, fm_math, mvm_math, slices)
+    np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,opt,fm_math,mvm_math,slices", CASES)
+def test_engine_matches_torch_reference_gpu(gpu_device, kind, opt, fm_math, mvm_math, slices):
+    got, want, eng = _run(gpu_device, kind, opt, fm_math, mvm_math, slices)
+    assert eng.is_gpu and eng.backend_name.startswith("hip:gfx950")
+    np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_matches_cpu_backend_eval(gpu_device):
+    """Predictions of the HIP engine equal the CPU engine's after training."""
+    outs = []
+    for dev in (torch.device("cpu"), gpu_device):
+        eng = Engine(ModelConfig(kind="fm", v_dim=8), OptimConfig(),
+                     EngineConfig(table_log2_cap=14, max_rows=256, max_nnz=4096, max_slices=1),
+                     device=dev)
+        for s in range(4):
+            k, rp, fg, lab = random_csr(256, 8, 200, seed=s)
+            eng.train_step(to_batch(k, rp, fg, lab, dev))
+        k, rp, fg, lab = random_csr(256, 8, 200, seed=99)
+        outs.append(eng.eval_step(to_batch(k, rp, fg, lab, dev)).cpu().numpy())
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-4, atol=1e-6)

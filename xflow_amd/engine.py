@@ -1,0 +1,246 @@
+"""Python face of the native Engine: torch-tensor batches, streams, checks.
+
+The native engine (csrc/engine/engine.cpp) owns the HBM hash table and all
+per-step buffers; this wrapper only validates tensors and hands device
+addresses over.  On a GPU it always runs the gfx950 HIP backend on torch's
+current stream (so engine kernels, torch ops and RCCL collectives are ordered
+on one queue); on CPU it runs the native C++ backend.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from xflow_amd import native
+from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+
+
+@dataclass
+class Batch:
+    """A CSR batch of torch tensors on the engine's device."""
+
+    keys: torch.Tensor                  # int64 [nnz] (u64 bit patterns)
+    labels: torch.Tensor                # float32 [rows]
+    row_ptr: Optional[torch.Tensor] = None   # int32 [rows+1]; None => fixed nnz/row
+    fgid: Optional[torch.Tensor] = None      # int32 [nnz]
+    nnz_per_row: int = 0
+    slice_rows: int = 0                 # rows per slice (gradient normaliser); 0 => all rows
+
+    @property
+    def rows(self) -> int:
+        return int(self.labels.numel())
+
+    @property
+    def nnz(self) -> int:
+        return int(self.keys.numel())
+
+    def view(self):
+        n = native.load()
+        v = n.BatchView()
+        v.keys = self.keys.data_ptr()
+        v.labels = self.labels.data_ptr()
+        v.row_ptr = self.row_ptr.data_ptr() if self.row_ptr is not None else 0
+        v.fgid = self.fgid.data_ptr() if self.fgid is not None else 0
+        v.rows = self.rows
+        v.nnz = self.nnz
+        v.nnz_per_row = self.nnz_per_row
+        v.slice_rows = self.slice_rows
+        return v
+
+    def check(self, device: torch.device) -> None:
+        for name, t, dt in (("keys", self.keys, torch.int64), ("labels", self.labels, torch.float32),
+                            ("row_ptr", self.row_ptr, torch.int32), ("fgid", self.fgid, torch.int32)):
+            if t is None:
+                continue
+            if t.dtype != dt:
+                raise TypeError(f"batch.{name} must be {dt}, got {t.dtype}")
+            if t.device != device:
+                raise ValueError(f"batch.{name} on {t.device}, engine on {device}")
+            if not t.is_contiguous():
+                raise ValueError(f"batch.{name} must be contiguous")
+        if self.row_ptr is None:
+            if self.nnz_per_row <= 0 or self.nnz != self.rows * self.nnz_per_row:
+                raise ValueError("fixed-width batch needs nnz == rows * nnz_per_row")
+        elif self.row_ptr.numel() != self.rows + 1:
+            raise ValueError("row_ptr must have rows+1 entries")
+
+
+def _device_index(device: torch.device) -> int:
+    if device.type == "cpu":
+        return -1
+    if device.type != "cuda":
+        raise ValueError(f"unsupported device {device}")
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+class Engine:
+    """One rank's sparse trainer state (hash-table shard + worker buffers)."""
+
+    def __init__(self, model: ModelConfig | None = None, optim: OptimConfig | None = None,
+                 engine: EngineConfig | None = None, device: str | torch.device = "cpu"):
+        self.model = model or ModelConfig()
+        self.optim = optim or OptimConfig()
+        self.cfg = engine or EngineConfig()
+        self.device = torch.device(device)
+        if self.device.type == "cuda":
+            native.require_hip()
+            if self.device.index is None:
+                self.device = torch.device("cuda", torch.cuda.current_device())
+        n = native.load()
+        self._e = n.Engine(self.model.native(), self.optim.native(),
+                           table_log2_cap=self.cfg.table_log2_cap, max_rows=self.cfg.max_rows,
+                           max_nnz=self.cfg.max_nnz, max_slices=self.cfg.max_slices,
+                           sum_slices=self.cfg.sum_slices, scratch_factor=self.cfg.scratch_factor,
+                           device=_device_index(self.device))
+        if self.is_gpu != (self.device.type == "cuda"):
+            raise RuntimeError("native engine backend does not match the requested device")
+
+    # ---- properties -------------------------------------------------------
+    @property
+    def native(self):
+        return self._e
+
+    @property
+    def is_gpu(self) -> bool:
+        return bool(self._e.is_gpu)
+
+    @property
+    def backend_name(self) -> str:
+        return self._e.backend_name
+
+    @property
+    def pstride(self) -> int:
+        return int(self._e.pstride)
+
+    @property
+    def params_per_key(self) -> int:
+        return int(self._e.P)
+
+    def _sync_stream(self) -> None:
+        if self.is_gpu:
+            self._e.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ---- single rank --------------------------------------------------------
+    def train_step(self, batch: Batch) -> None:
+        batch.check(self.device)
+        self._sync_stream()
+        self._e.train_step(batch.view())
+
+    def eval_step(self, batch: Batch, pctr: torch.Tensor | None = None) -> torch.Tensor:
+        batch.check(self.device)
+        if pctr is None:
+            pctr = torch.empty(batch.rows, dtype=torch.float32, device=self.device)
+        self._sync_stream()
+        self._e.eval_step(batch.view(), pctr.data_ptr())
+        return pctr
+
+    def train_view(self, view) -> None:
+        """Train on a native BatchView (e.g. engine-staged synthetic batch)."""
+        self._sync_stream()
+        self._e.train_step(view)
+
+    def synth_batch(self, rows: int, vocab, zipf_s, hash_space: int, seed: int, step: int,
+                    planted_scale: float = 0.3, planted_bias: float = -1.2, slice_rows: int = 0,
+                    out: Batch | None = None):
+        """Generate a synthetic batch on the engine's device.
+
+        Without ``out`` the batch lives in engine-owned staging memory and a
+        native BatchView is returned; with ``out`` (a Batch of preallocated
+        tensors) the generator writes into those tensors and ``out`` is returned.
+        """
+        self._sync_stream()
+        kw = {}
+        if out is not None:
+            kw = dict(keys=out.keys.data_ptr(), labels=out.labels.data_ptr(),
+                      fgid=out.fgid.data_ptr() if out.fgid is not None else 0)
+        v = self._e.synth_batch(int(rows), [int(x) for x in vocab], [float(s) for s in zipf_s],
+                                int(hash_space), int(seed), int(step), float(planted_scale),
+                                float(planted_bias), int(slice_rows), **kw)
+        if out is None:
+            return v
+        out.nnz_per_row = len(vocab)
+        out.slice_rows = int(slice_rows)
+        return out
+
+    def push(self, keys, grads) -> None:
+        self._e.push_host(np.asarray(keys, dtype=np.uint64),
+                          np.asarray(grads, dtype=np.float32).reshape(-1))
+
+    def pull(self, keys) -> np.ndarray:
+        k = np.asarray(keys, dtype=np.uint64)
+        return self._e.pull_host(k).reshape(len(k), self.params_per_key)
+
+    # ---- multi-rank phases (driven by parallel.sparse_a2a) ----------------------
+    def w_prepare(self, batch: Batch, world: int, counts: torch.Tensor, send_keys: torch.Tensor):
+        batch.check(self.device)
+        self._sync_stream()
+        self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr())
+
+    def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor) -> None:
+        self._sync_stream()
+        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr())
+
+    def w_forward_backward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
+                           grads_out: torch.Tensor, masks_out: torch.Tensor | None) -> None:
+        self._sync_stream()
+        self._e.w_forward_backward(batch.view(), pulled.data_ptr(), int(n_send),
+                                   grads_out.data_ptr(),
+                                   masks_out.data_ptr() if masks_out is not None else 0)
+
+    def s_apply(self, recv_keys: torch.Tensor, recv_grads: torch.Tensor,
+                recv_masks: torch.Tensor | None, offsets, S: int) -> None:
+        self._sync_stream()
+        self._e.s_apply(recv_keys.data_ptr(), recv_grads.data_ptr(),
+                        recv_masks.data_ptr() if recv_masks is not None else 0,
+                        [int(o) for o in offsets], int(S))
+
+    def w_finish(self) -> None:
+        self._sync_stream()
+        self._e.w_finish()
+
+    # ---- stats / checkpoint -------------------------------------------------
+    def slices_of(self, batch: Batch) -> int:
+        return int(self._e.slices_of(batch.view()))
+
+    def read_stats(self, reset: bool = False, which: int = 0) -> dict:
+        self._sync_stream()
+        return self._e.read_stats(reset, which)
+
+    def table_size(self) -> int:
+        self._sync_stream()
+        return int(self._e.table_size())
+
+    def n_unique(self) -> int:
+        self._sync_stream()
+        return int(self._e.n_unique())
+
+    def overflowed(self) -> bool:
+        self._sync_stream()
+        return bool(self._e.overflowed())
+
+    def export_table(self):
+        self._sync_stream()
+        return self._e.export_table()
+
+    def import_table(self, keys: np.ndarray, words: np.ndarray) -> None:
+        self._sync_stream()
+        self._e.import_table(np.ascontiguousarray(keys, dtype=np.uint64),
+                             np.ascontiguousarray(words, dtype=np.uint32))
+
+    @property
+    def state_words(self) -> int:
+        return int(self._e.state_words)
+
+    def save(self, path: str) -> None:
+        self._sync_stream()
+        self._e.save(path)
+
+    def load(self, path: str) -> None:
+        self._sync_stream()
+        self._e.load(path)
+
+    def synchronize(self) -> None:
+        self._e.synchronize()
