@@ -101,8 +101,14 @@ class CpuBackend final : public Backend {
       for (int w = 2; w < t.L.stride; ++w) sp[w] = 0u;
     }
   }
+  // Same persistent, epoch-stamped scratch protocol as the HIP kernels
+  // (k_scratch_maybe_clear / k_dedup_insert / k_dedup_compact).
   void dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o) override {
     const u64 mask = s.cap - 1;
+    if (*s.claims > s.rebuild_at) {
+      for (u64 i = 0; i < s.cap; ++i) s.keys[i] = kEmptyKey;
+      *s.claims = 0;
+    }
     for (int64_t i = 0; i < nnz; ++i) {
       u64 k = sanitize_key(keys[i]);
       u64 p = fmix64(k) & mask;
@@ -111,16 +117,23 @@ class CpuBackend final : public Backend {
         if (s.keys[p] == k) break;
         if (s.keys[p] == kEmptyKey) {
           s.keys[p] = k;
-          int64_t idx = (*o.n_uniq)++;
-          o.uniq_keys[idx] = k;
-          o.uniq_pos[idx] = (u32)p;
+          ++*s.claims;
           break;
         }
         p = (p + 1) & mask;
       }
       if (n == s.cap) { *o.overflow = 1u; p = 0; }
       o.pos[i] = (u32)p;
+      s.stamps[p] = s.epoch;
     }
+    int64_t u = 0;
+    for (u64 p = 0; p < s.cap; ++p) {
+      if (s.stamps[p] != s.epoch) continue;
+      o.uniq_keys[u] = s.keys[p];
+      o.uniq_pos[u] = (u32)p;
+      ++u;
+    }
+    *o.n_uniq = u;
   }
 
   void scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max) override {

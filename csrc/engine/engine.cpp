@@ -53,6 +53,14 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (scratch_.cap > (1ull << 31)) throw std::invalid_argument("max_nnz too large");
   scratch_.keys = balloc<u64>(be, scratch_.cap);
   be.fill_u64(scratch_.keys, kEmptyKey, scratch_.cap);
+  scratch_.stamps = balloc<u32>(be, scratch_.cap);
+  be.memset(scratch_.stamps, 0, sizeof(u32) * scratch_.cap);
+  scratch_.claims = balloc<unsigned long long>(be, 1);
+  be.memset(scratch_.claims, 0, sizeof(unsigned long long));
+  // Rebuild once half full: one more step adds at most max_nnz <= cap/factor
+  // keys, so the load factor stays below 0.5 + 1/factor.
+  scratch_.rebuild_at = scratch_.cap / 2;
+  scratch_.epoch = 0;
 
   const int ps = cfg_.model.pstride();
   pos_ = balloc<u32>(be, nnz);
@@ -82,7 +90,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 Engine::~Engine() {
   Backend& be = *be_;
   be.synchronize();
-  void* ptrs[] = {table_.words, table_.size, overflow_, scratch_.keys, pos_, uniq_keys_,
+  void* ptrs[] = {table_.words, table_.size, overflow_, scratch_.keys, scratch_.stamps,
+                  scratch_.claims, pos_, uniq_keys_,
                   uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_, host_keys_dev_, host_vals_dev_};
@@ -112,6 +121,7 @@ void Engine::dedup_(const BatchView& b) {
   if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
   be_->memset(n_uniq_, 0, sizeof(int64_t));
+  if (++scratch_.epoch == 0) scratch_.epoch = 1;  // 0 marks never-stamped slots
   DedupOut o;
   o.pos = pos_;
   o.uniq_keys = uniq_keys_;
@@ -152,6 +162,7 @@ void Engine::train_step(const BatchView& b) {
   fa.stats = stats_;
   fa.model = cfg_.model;
   fa.S = S;
+  fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   be_->forward_backward(fa);
 
   ApplyArgs aa;
@@ -171,8 +182,6 @@ void Engine::train_step(const BatchView& b) {
   aa.P = cfg_.model.P();
   aa.sum_slices = cfg_.sum_slices;
   aa.slice_rows = srows;
-  aa.scratch = scratch_;
-  aa.reset_pos = uniq_pos_;
   be_->table_apply(aa);
 }
 
@@ -201,7 +210,6 @@ void Engine::eval_step(const BatchView& b, float* pctr) {
   fa.model = cfg_.model;
   fa.S = 1;
   be_->forward_backward(fa);
-  be_->scratch_reset(scratch_, uniq_pos_, n_uniq_, b.nnz);
 }
 
 void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& grads) {
@@ -339,6 +347,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.stats = stats_;
   fa.model = cfg_.model;
   fa.S = S;
+  fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   be_->forward_backward(fa);
   GatherGradArgs ga;
   ga.grad = grad_;
@@ -383,7 +392,8 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
   }
 }
 
-void Engine::w_finish() { be_->scratch_reset(scratch_, uniq_pos_, n_uniq_, cfg_.max_nnz); }
+// The dedup scratch is epoch-stamped and persistent: nothing to release.
+void Engine::w_finish() {}
 
 // ---------------------------------------------------------------------------
 LossStats Engine::read_stats(bool reset, int which) {

@@ -27,48 +27,150 @@ constexpr u32 kNoSlot = 0xFFFFFFFFu;
 // ---------------------------------------------------------------------------
 // dedup
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) k_dedup(const u64* __restrict__ keys, int64_t nnz,
-                                                  u64* __restrict__ skeys, u64 cap,
-                                                  u32* __restrict__ pos, u64* __restrict__ uk,
-                                                  u32* __restrict__ up,
-                                                  unsigned long long* __restrict__ n_uniq,
-                                                  u32* __restrict__ overflow) {
-  const u64 mask = cap - 1;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += stride) {
-    u64 k = sanitize_key(keys[i]);
-    u64 s = fmix64(k) & mask;
-    bool claimed = false;
+// The worker dedup table is persistent across steps (see ScratchView): hot
+// keys keep their slot, so after warm-up almost every occurrence is a plain
+// hit.  CTR keys are extremely skewed (top-1000 keys ~60% of occurrences); a
+// table cleared every step made each hot key a same-address CAS storm.
+//
+// Step 0 -- device-side rebuild: when `claims` exceeds rebuild_at, every slot
+// is freed (grid-stride fill) before the step; otherwise the launch exits.
+__global__ void k_scratch_maybe_clear(u64* __restrict__ skeys, u64 cap,
+                                      const unsigned long long* __restrict__ claims,
+                                      u64 rebuild_at) {
+  if (*claims <= rebuild_at) return;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += stride)
+    skeys[s] = kEmptyKey;
+}
+
+__global__ void k_scratch_claims_reset(unsigned long long* claims, u64 rebuild_at) {
+  if (*claims > rebuild_at) *claims = 0ull;
+}
+
+// Step 1 -- insert / stamp.  Each lane owns kDedupItems occurrences spaced one
+// block apart (coalesced key loads) and issues all of their first-probe loads
+// before resolving any, so a wave keeps 8 independent random reads in flight.
+// A hit writes the epoch stamp with a plain (idempotent, no-return) store; only
+// keys new to the table CAS.
+constexpr int kDedupItems = 8;
+constexpr int kDedupChunk = kBlock * kDedupItems;
+
+__global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__ keys, int64_t nnz,
+                                                         ScratchView sv, u32* __restrict__ pos,
+                                                         u32* __restrict__ overflow) {
+  u64* __restrict__ skeys = sv.keys;
+  const u64 cap = sv.cap, mask = cap - 1;
+  const int64_t base = (int64_t)blockIdx.x * kDedupChunk + threadIdx.x;
+  u64 k[kDedupItems], s[kDedupItems], cur[kDedupItems];
+#pragma unroll
+  for (int j = 0; j < kDedupItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    k[j] = i < nnz ? sanitize_key(keys[i]) : 0ull;
+    s[j] = fmix64(k[j]) & mask;
+  }
+#pragma unroll
+  for (int j = 0; j < kDedupItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    cur[j] = i < nnz ? skeys[s[j]] : k[j];
+  }
+  unsigned int claimed = 0;
+#pragma unroll
+  for (int j = 0; j < kDedupItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    if (i >= nnz) continue;
+    u64 sj = s[j], c = cur[j];
     u64 n = 0;
-    for (; n < cap; ++n) {
-      u64 cur = skeys[s];
-      if (cur == k) break;
-      if (cur == kEmptyKey) {
-        u64 prev = atomicCAS((unsigned long long*)&skeys[s], (unsigned long long)kEmptyKey,
-                             (unsigned long long)k);
-        if (prev == kEmptyKey) { claimed = true; break; }
-        if (prev == k) break;
+    while (c != k[j]) {
+      if (c == kEmptyKey) {
+        u64 prev = atomicCAS((unsigned long long*)&skeys[sj], (unsigned long long)kEmptyKey,
+                             (unsigned long long)k[j]);
+        if (prev == kEmptyKey) {
+          ++claimed;
+          break;
+        }
+        if (prev == k[j]) break;
       }
-      s = (s + 1) & mask;
+      if (++n >= cap) {
+        *overflow = 1u;
+        break;
+      }
+      sj = (sj + 1) & mask;
+      c = skeys[sj];
     }
-    if (n == cap) { *overflow = 1u; s = 0; }
-    pos[i] = (u32)s;
-    unsigned long long idx = wave_append(n_uniq, claimed);
-    if (claimed) {
-      uk[idx] = k;
-      up[idx] = (u32)s;
-    }
+    pos[i] = (u32)sj;
+    sv.stamps[sj] = sv.epoch;
+  }
+  // one atomic per wave for the rebuild counter
+  unsigned int tot = claimed;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  if (lane_id() == 0 && tot) atomicAdd(sv.claims, (unsigned long long)tot);
+}
+
+// Step 2 -- compaction: scan the stamps (coalesced, cap*4 bytes) and emit
+// (key, slot) of every slot stamped with this epoch.  One global atomic per
+// workgroup.
+constexpr int kCompactItems = 16;
+constexpr int kCompactChunk = kBlock * kCompactItems;
+
+__global__ void __launch_bounds__(kBlock) k_dedup_compact(ScratchView sv, u64* __restrict__ uk,
+                                                          u32* __restrict__ up,
+                                                          unsigned long long* __restrict__ n_uniq) {
+  __shared__ unsigned int wave_tot[kBlock / kWave];
+  __shared__ unsigned long long block_base;
+  const u64 base = (u64)blockIdx.x * kCompactChunk + threadIdx.x;
+  unsigned int hit = 0, cnt = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) {
+    u64 s = base + (u64)j * kBlock;
+    bool h = s < sv.cap && sv.stamps[s] == sv.epoch;
+    hit |= (unsigned int)h << j;
+    cnt += h;
+  }
+  // block exclusive scan of per-lane counts
+  const int lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
+  unsigned int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    unsigned int v = __shfl_up(incl, o);
+    if (lane >= o) incl += v;
+  }
+  if (lane == kWave - 1) wave_tot[w] = incl;
+  __syncthreads();
+  unsigned int wave_off = 0, total = 0;
+  for (int i = 0; i < kBlock / kWave; ++i) {
+    if (i < w) wave_off += wave_tot[i];
+    total += wave_tot[i];
+  }
+  if (threadIdx.x == 0) block_base = total ? atomicAdd(n_uniq, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  unsigned long long dst = block_base + wave_off + (incl - cnt);
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) {
+    if (!(hit & (1u << j))) continue;
+    u64 s = base + (u64)j * kBlock;
+    uk[dst] = sv.keys[s];
+    up[dst] = (u32)s;
+    ++dst;
   }
 }
 
 void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st) {
   if (nnz <= 0) return;
-  hipLaunchKernelGGL(k_dedup, dim3(grid_for(nnz)), dim3(kBlock), 0, st, keys, nnz, s.keys,
-                     s.cap, o.pos, o.uniq_keys, o.uniq_pos,
-                     reinterpret_cast<unsigned long long*>(o.n_uniq), o.overflow);
+  hipLaunchKernelGGL(k_scratch_maybe_clear, dim3(grid_for((int64_t)s.cap)), dim3(kBlock), 0, st,
+                     s.keys, s.cap, s.claims, s.rebuild_at);
+  hipLaunchKernelGGL(k_scratch_claims_reset, dim3(1), dim3(1), 0, st, s.claims, s.rebuild_at);
+  int g1 = (int)((nnz + kDedupChunk - 1) / kDedupChunk);
+  hipLaunchKernelGGL(k_dedup_insert, dim3(g1), dim3(kBlock), 0, st, keys, nnz, s, o.pos,
+                     o.overflow);
+  int g2 = (int)((s.cap + kCompactChunk - 1) / kCompactChunk);
+  hipLaunchKernelGGL(k_dedup_compact, dim3(g2), dim3(kBlock), 0, st, s, o.uniq_keys, o.uniq_pos,
+                     reinterpret_cast<unsigned long long*>(o.n_uniq));
   XF_HIP_CHECK(hipGetLastError());
 }
 
+// The persistent scratch needs no per-step reset (stamps expire with the
+// epoch); kept as an explicit full clear for callers that want a cold table.
 __global__ void k_scratch_reset(u64* __restrict__ skeys, const u32* __restrict__ pos,
                                 const int64_t* n_dev, int64_t n_max) {
   int64_t n = dev_count(n_dev, n_max, n_max);

@@ -31,9 +31,19 @@ struct TableView {
   u32* overflow = nullptr;   // set when a probe wraps the whole table
 };
 
-struct ScratchView {           // per-step dedup table (keys only)
+// Worker dedup table.  Persistent across steps: a key keeps its slot, so hot
+// keys are never re-inserted (no CAS storms on the skewed head of the key
+// distribution).  A slot is "in the current batch" when its stamp equals the
+// step's epoch (set by idempotent plain stores); the unique list is recovered
+// by scanning stamps.  The table is cleared on the device once `claims` (keys
+// inserted since the last clear) exceeds `rebuild_at`.
+struct ScratchView {
   u64* keys = nullptr;         // [cap], kEmptyKey when free
+  u32* stamps = nullptr;       // [cap], epoch of the last batch touching the slot
   u64 cap = 0;
+  u32 epoch = 1;               // current step (never 0)
+  unsigned long long* claims = nullptr;  // device counter of inserted keys
+  u64 rebuild_at = 0;          // clear the table before a step once claims > rebuild_at
 };
 
 struct DedupOut {
@@ -54,6 +64,7 @@ struct FwdArgs {
   LossStats* stats = nullptr;      // accumulated (device)
   ModelSpec model;
   int S = 1;                       // slices in this batch
+  bool agg_ok = false;             // grad indices (pos*S+s)*pstride fit in a u32 (LDS aggregation)
 };
 
 struct PullArgs {

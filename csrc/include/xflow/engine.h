@@ -27,7 +27,7 @@ struct EngineConfig {
   int64_t max_nnz = 1 << 22;   // per step
   int max_slices = 1;          // slices per step (<= 32)
   bool sum_slices = false;     // apply Σ_s g_s once instead of ordered per-slice pushes
-  double scratch_factor = 1.25;  // dedup scratch capacity = pow2 >= factor * max_nnz
+  double scratch_factor = 2.5;  // dedup scratch capacity = pow2 >= factor * max_nnz
   int device = -1;             // -1 => CPU backend, else HIP device ordinal
 };
 

@@ -140,7 +140,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("model"), py::arg("opt"), py::arg("table_log2_cap") = 20,
            py::arg("max_rows") = 1 << 16, py::arg("max_nnz") = 1 << 22,
            py::arg("max_slices") = 1, py::arg("sum_slices") = false,
-           py::arg("scratch_factor") = 1.25, py::arg("device") = -1)
+           py::arg("scratch_factor") = 2.5, py::arg("device") = -1)
       .def_property_readonly("is_gpu", &Engine::is_gpu)
       .def_property_readonly("backend_name", [](Engine& e) { return e.backend().name(); })
       .def_property_readonly("pstride", &Engine::pstride)

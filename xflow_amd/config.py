@@ -83,7 +83,7 @@ class EngineConfig:
     max_nnz: int = 1 << 22
     max_slices: int = 1
     sum_slices: bool = False      # one push of Σ_s g_s instead of ordered per-slice pushes
-    scratch_factor: float = 1.25
+    scratch_factor: float = 2.5
 
 
 @dataclass
