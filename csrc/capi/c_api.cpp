@@ -25,9 +25,9 @@ struct XFlow {
 };
 
 int default_device() {
+  if (!xflow::hip_backend_available()) return -1;
   const char* e = std::getenv("XFLOW_DEVICE");
-  if (e) return std::atoi(e);
-  return xflow::hip_backend_available() ? 0 : -1;
+  return e ? std::atoi(e) : 0;
 }
 
 template <typename F>

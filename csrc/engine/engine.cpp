@@ -104,14 +104,18 @@ int Engine::slices_of(const BatchView& b) const {
 }
 
 const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
-  if (b.rows == cached_rows_ && b.slice_rows == cached_slice_rows_) return slice_rows_;
+  if (b.rows == cached_rows_ && b.slice_rows == cached_slice_rows_ && S == cached_S_)
+    return slice_rows_;
   int32_t h[32];
   for (int s = 0; s < S; ++s) {
     int64_t sr = b.slice_rows > 0 ? b.slice_rows : b.rows;
     int64_t rem = b.rows - (int64_t)s * sr;
-    h[s] = (int32_t)(rem < sr ? rem : sr);
+    rem = rem < 0 ? 0 : rem;
+    // an empty slice has no gradient rows; 1 keeps 0/rows finite
+    h[s] = (int32_t)(rem < sr ? (rem > 0 ? rem : 1) : sr);
   }
   be_->copy_h2d(slice_rows_, h, sizeof(int32_t) * S);
+  cached_S_ = S;
   cached_rows_ = b.rows;
   cached_slice_rows_ = b.slice_rows;
   return slice_rows_;
@@ -304,7 +308,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
   ba.send_pos = send_pos_;
   ba.scratch = bucket_ws_;
   be_->bucket(ba);
-  if (S > 1 && !cfg_.sum_slices) be_->slice_masks(b, pos_, tmask_);
+  (void)S;  // slice masks are built in w_forward_backward with the step's global S
 }
 
 void Engine::ensure_server_capacity(int64_t n) {
@@ -315,7 +319,21 @@ void Engine::ensure_server_capacity(int64_t n) {
   srv_slots_ = balloc<u32>(*be_, srv_cap_);
 }
 
-void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals) {
+void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr) {
+  be_->scatter_rows(pulled, wpull_, send_pos_, nullptr, n_send, pstride());
+  FwdArgs fa;
+  fa.batch = b;
+  fa.pos = pos_;
+  fa.wpull = wpull_;
+  fa.grad = nullptr;
+  fa.pctr = pctr;
+  fa.stats = stats_ + 1;
+  fa.model = cfg_.model;
+  fa.S = 1;
+  be_->forward_backward(fa);
+}
+
+void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert) {
   ensure_server_capacity(n);
   srv_n_ = n;
   if (n == 0) return;
@@ -325,7 +343,7 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals) {
   pa.keys = recv_keys;
   pa.n_host = n;
   pa.n_max = n;
-  pa.insert = true;
+  pa.insert = insert;
   pa.out_slot = srv_slots_;
   pa.out_vals = out_vals;
   pa.pstride = pstride();
@@ -333,12 +351,18 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals) {
 }
 
 void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
-                                float* grads_out, u32* masks_out) {
-  const int S = slices_of(b);
+                                float* grads_out, u32* masks_out, int S_global) {
+  // All ranks of a step must agree on the gradient row width (S*pstride):
+  // S_global (>= this batch's slices) lets a rank with a short or empty batch
+  // emit the same layout; its extra slices carry no rows and no mask bits.
+  const int S = S_global > 0 ? S_global : slices_of(b);
+  if (S < slices_of(b) || S > cfg_.max_slices)
+    throw std::invalid_argument("w_forward_backward: S_global out of range");
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
   be_->scatter_rows(pulled, wpull_, send_pos_, nullptr, n_send, ps);
+  if (masks) be_->slice_masks(b, pos_, tmask_);
   FwdArgs fa;
   fa.batch = b;
   fa.pos = pos_;

@@ -63,12 +63,14 @@ class Engine {
   void w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out);
   // server: probe/insert n received keys, write pulled rows (pstride floats)
   // into out_vals (backend memory), remember slots for s_apply.
-  void s_pull(const u64* recv_keys, int64_t n, float* out_vals);
+  void s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert = true);
+  // worker: forward only from pulled rows (sharded evaluation); pctr may be null.
+  void w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr);
   // worker: place pulled rows (in send order) into the pos-indexed buffer,
   // run forward/backward, then emit normalised gradients in send order.
   // grads_out: [n_send][S*pstride]; masks_out: [n_send] (used when S>1).
   void w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
-                          float* grads_out, u32* masks_out);
+                          float* grads_out, u32* masks_out, int S_global = 0);
   // server: apply received gradients source by source (deterministic order).
   // src_offsets has world+1 entries delimiting each source's rows.
   void s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
@@ -127,6 +129,7 @@ class Engine {
   int64_t* bucket_ws_ = nullptr;  // [2*256]
   int32_t* slice_rows_ = nullptr;  // [32]
   int64_t cached_rows_ = -1, cached_slice_rows_ = -1;
+  int cached_S_ = -1;
   int64_t last_nsend_ = 0;
 
   // staging batch buffers (backend memory)

@@ -107,15 +107,45 @@ class PrefetchReader {
   bool full_ = false, eof_ = false, stop_ = false;
 };
 
+// ---- reference-compatible IO base (io.h:24-59) ----
+// Opening a missing file throws std::runtime_error (the reference exit(1)s).
+class IO {
+ public:
+  explicit IO(const char* file_path);
+  virtual ~IO();
+  void Init();
+  virtual void load_all_data() = 0;
+  virtual void load_minibatch_data(int num) = 0;
+  const char* file_path;
+
+ protected:
+  bool next_line(std::string& line);  // false at EOF
+  FILE* fp_ = nullptr;
+};
+
 // ---- reference-compatible loader (load_data_from_disk.h:19-34) ----
-class LoadData {
+// load_minibatch_hash_data_fread is the reference's live loader (block read,
+// libffm, hashed fid).  The other four are the reference's unused loaders,
+// implemented with their intended semantics:
+//   load_all_data / load_minibatch_data(num): numeric `fgid:fid:val` triples
+//     (fid used as the key verbatim, val kept), whole file / next num lines;
+//   load_all_hash_data / load_mibibatch_hash_data(num) [sic]: every
+//     whitespace token hashed whole (sscanf("%s") + std::hash in the
+//     reference), fgid = 0.
+class LoadData : public IO {
  public:
   LoadData(const char* file_path, size_t block_size);
-  ~LoadData();
+  ~LoadData() override;
+  void load_all_data() override;
+  void load_minibatch_data(int num) override;
+  void load_all_hash_data();
+  void load_mibibatch_hash_data(int num);
   void load_minibatch_hash_data_fread();
   Data m_data;
 
  private:
+  void parse_numeric_line(const std::string& line);
+  void parse_hashed_line(const std::string& line);
   std::unique_ptr<BlockReader> reader_;
   CsrBlock block_;
 };

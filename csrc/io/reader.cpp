@@ -158,10 +158,100 @@ bool PrefetchReader::next(CsrBlock& out) {
   return true;
 }
 
+IO::IO(const char* path) : file_path(path) { Init(); }
+
+IO::~IO() {
+  if (fp_) std::fclose(fp_);
+}
+
+void IO::Init() {
+  if (fp_) return;
+  fp_ = std::fopen(file_path, "rb");
+  if (!fp_) throw std::runtime_error(std::string("open file ") + file_path + " error! ");
+}
+
+bool IO::next_line(std::string& line) {
+  line.clear();
+  int c;
+  bool any = false;
+  while ((c = std::fgetc(fp_)) != EOF) {
+    any = true;
+    if (c == '\n') break;
+    line.push_back((char)c);
+  }
+  return any;
+}
+
 LoadData::LoadData(const char* file_path, size_t block_size)
-    : reader_(new BlockReader(file_path, block_size)) {}
+    : IO(file_path), reader_(new BlockReader(file_path, block_size)) {}
 
 LoadData::~LoadData() = default;
+
+void LoadData::parse_numeric_line(const std::string& line) {
+  const char* p = line.c_str();
+  float y = 0;
+  int nchar = 0;
+  std::vector<kv> sample;
+  if (std::sscanf(p, "%f%n", &y, &nchar) >= 1) {
+    p += nchar;
+    m_data.label.push_back((int)y);
+    int fg = 0, val = 0;
+    long fid = 0;
+    while (std::sscanf(p, "%d:%ld:%d%n", &fg, &fid, &val, &nchar) >= 3) {
+      p += nchar;
+      sample.push_back(kv{fg, (size_t)fid, val});
+    }
+    m_data.fea_matrix.push_back(std::move(sample));
+  }
+}
+
+void LoadData::parse_hashed_line(const std::string& line) {
+  const char* p = line.c_str();
+  float y = 0;
+  int nchar = 0;
+  std::vector<kv> sample;
+  if (std::sscanf(p, "%f%n", &y, &nchar) >= 1) {
+    p += nchar;
+    m_data.label.push_back((int)y);
+    const char* e = p + std::strlen(p);
+    while (p < e) {
+      while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) ++p;
+      const char* q = p;
+      while (q < e && *q != ' ' && *q != '\t' && *q != '\r') ++q;
+      if (q > p) sample.push_back(kv{0, (size_t)feature_hash(p, (size_t)(q - p)), 0});
+      p = q;
+    }
+    m_data.fea_matrix.push_back(std::move(sample));
+  }
+}
+
+void LoadData::load_all_data() {
+  m_data.fea_matrix.clear();
+  m_data.label.clear();
+  std::string line;
+  while (next_line(line)) parse_numeric_line(line);
+}
+
+void LoadData::load_minibatch_data(int num) {
+  m_data.fea_matrix.clear();
+  m_data.label.clear();
+  std::string line;
+  for (int i = 0; i < num && next_line(line); ++i) parse_numeric_line(line);
+}
+
+void LoadData::load_all_hash_data() {
+  m_data.fea_matrix.clear();
+  m_data.label.clear();
+  std::string line;
+  while (next_line(line)) parse_hashed_line(line);
+}
+
+void LoadData::load_mibibatch_hash_data(int num) {
+  m_data.fea_matrix.clear();
+  m_data.label.clear();
+  std::string line;
+  for (int i = 0; i < num && next_line(line); ++i) parse_hashed_line(line);
+}
 
 void LoadData::load_minibatch_hash_data_fread() {
   m_data.fea_matrix.clear();

@@ -172,16 +172,24 @@ PYBIND11_MODULE(_xflow_native, m) {
            },
            py::call_guard<py::gil_scoped_release>())
       .def("s_pull",
-           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out) {
-             e.s_pull(P<const u64>(keys), n, P<float>(out));
+           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert) {
+             e.s_pull(P<const u64>(keys), n, P<float>(out), insert);
+           },
+           py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("insert") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def("w_forward",
+           [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t pctr) {
+             e.w_forward(b, P<const float>(pulled), n_send, P<float>(pctr));
            },
            py::call_guard<py::gil_scoped_release>())
       .def("w_forward_backward",
            [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t grads,
-              uintptr_t masks) {
+              uintptr_t masks, int S) {
              e.w_forward_backward(b, P<const float>(pulled), n_send, P<float>(grads),
-                                  P<u32>(masks));
+                                  P<u32>(masks), S);
            },
+           py::arg("batch"), py::arg("pulled"), py::arg("n_send"), py::arg("grads"),
+           py::arg("masks"), py::arg("S") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("s_apply",
            [](Engine& e, uintptr_t keys, uintptr_t grads, uintptr_t masks,
@@ -284,6 +292,10 @@ PYBIND11_MODULE(_xflow_native, m) {
   py::class_<LoadData>(m, "LoadData")
       .def(py::init([](const std::string& p, size_t bs) { return new LoadData(p.c_str(), bs); }))
       .def("load_minibatch_hash_data_fread", &LoadData::load_minibatch_hash_data_fread)
+      .def("load_all_data", &LoadData::load_all_data)
+      .def("load_minibatch_data", &LoadData::load_minibatch_data)
+      .def("load_all_hash_data", &LoadData::load_all_hash_data)
+      .def("load_mibibatch_hash_data", &LoadData::load_mibibatch_hash_data)
       .def_property_readonly("label", [](LoadData& l) { return l.m_data.label; })
       .def_property_readonly("fea_matrix", [](LoadData& l) {
         py::list rows;

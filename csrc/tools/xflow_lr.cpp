@@ -38,7 +38,8 @@ int main(int argc, char* argv[]) {
   cfg.epochs = std::atoi(argv[4]);
   std::string save, load;
   const char* dev = std::getenv("XFLOW_DEVICE");
-  cfg.device = dev ? std::atoi(dev) : (xflow::hip_backend_available() ? 0 : -1);
+  const bool gpu = xflow::hip_backend_available();
+  cfg.device = gpu ? (dev ? std::atoi(dev) : 0) : -1;
   for (int i = 5; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> const char* {

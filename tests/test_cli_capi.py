@@ -1,0 +1,107 @@
+"""Entry points: the native xflow_lr binary, the Python CLI, the compat
+launch scripts and the C API (libxflow_api.so: XFCreate / XFStartTrain)."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import DATA, ROOT
+
+TRAIN = os.path.join(DATA, "small_train")
+TEST = os.path.join(DATA, "small_test")
+ENV = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="", XFLOW_DEVICE="-1")
+
+
+def _run(cmd, cwd, timeout=300, env=ENV):
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def _lines(out):
+    return [l for l in out.splitlines() if l.strip()]
+
+
+def test_native_binary_matches_reference_output(tmp_path):
+    out = _run([os.path.join(ROOT, "build", "bin", "xflow_lr"), TRAIN, TEST, "0", "30",
+                "--threads", "8"], tmp_path)
+    ls = _lines(out)
+    assert ls[0].strip() == "start LR"
+    assert ls[1] == "my rank is = 0"
+    assert "epoch : 29" in ls
+    i = ls.index("LR AUC: ")
+    assert ls[i + 1].startswith("logloss: -0.") and "\tauc = 0.5" in ls[i + 1]
+    assert ls[-1] == "train end......"
+    assert len(open(tmp_path / "pred_0_0.txt").read().splitlines()) == 200
+
+
+def test_native_binary_usage_and_roles(tmp_path):
+    r = subprocess.run([os.path.join(ROOT, "build", "bin", "xflow_lr")], capture_output=True,
+                       text=True, env=ENV)
+    assert r.returncode == 1 and "run_ps_local.sh" in r.stdout
+    env = dict(ENV, DMLC_ROLE="server")
+    out = _run([os.path.join(ROOT, "build", "bin", "xflow_lr"), TRAIN, TEST, "0", "1"],
+               tmp_path, env=env)
+    assert "init server success" in out
+
+
+def test_python_cli_equals_native(tmp_path):
+    a = _run([os.path.join(ROOT, "build", "bin", "xflow_lr"), TRAIN, TEST, "1", "5",
+              "--threads", "8"], tmp_path / ".." if False else tmp_path)
+    os.rename(tmp_path / "pred_0_0.txt", tmp_path / "native.txt")
+    b = _run([sys.executable, "-m", "xflow_amd.cli", TRAIN, TEST, "1", "5", "--threads", "8",
+              "--cpu"], tmp_path)
+    la = [l for l in _lines(a) if l.startswith("logloss")]
+    lb = [l for l in _lines(b) if l.startswith("logloss")]
+    assert la == lb
+    assert open(tmp_path / "native.txt").read() == open(tmp_path / "pred_0_0.txt").read()
+
+
+def test_run_ps_local_script_three_workers(tmp_path):
+    env = dict(ENV, XFLOW_FLAGS="--threads 8")
+    out = _run(["bash", os.path.join(ROOT, "run_ps_local.sh"), "0", "5", "3"], tmp_path,
+               env=env)
+    assert out.count("train end......") == 3
+    assert out.count("init server success") == 1
+    assert sum(1 for l in _lines(out) if l.startswith("logloss: ")) == 1
+
+
+def test_cli_checkpoint_save_and_resume(tmp_path):
+    ck = str(tmp_path / "ck")
+    _run([sys.executable, "-m", "xflow_amd.cli", TRAIN, TEST, "0", "3", "--threads", "8",
+          "--cpu", "--save", ck, "--metrics", str(tmp_path / "m.jsonl")], tmp_path)
+    assert os.path.exists(os.path.join(ck, "meta.json"))
+    assert os.path.exists(os.path.join(ck, "shard-00000-of-00001.xftb"))
+    out = _run([sys.executable, "-m", "xflow_amd.cli", TRAIN, TEST, "0", "0", "--threads", "8",
+                "--cpu", "--load", ck], tmp_path)
+    first = [l for l in open(tmp_path / "pred_0_0.txt")]
+    assert len(first) == 200 and "logloss: " in out
+    recs = [l for l in open(tmp_path / "m.jsonl")]
+    assert any('"event": "epoch"' in r for r in recs) and any('"event": "eval"' in r for r in recs)
+
+
+def test_c_api(tmp_path):
+    lib = ctypes.CDLL(os.path.join(ROOT, "build", "lib", "libxflow_api.so"))
+    lib.XFCreateEx.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_char_p,
+                               ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.XFGetLastError.restype = ctypes.c_char_p
+    h = ctypes.c_void_p()
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        assert lib.XFCreateEx(ctypes.byref(h), TRAIN.encode(), TEST.encode(), 0, 10, 8, -1) == 0
+        assert lib.XFStartTrain(ctypes.byref(h)) == 0, lib.XFGetLastError()
+        ll, auc = ctypes.c_double(), ctypes.c_double()
+        assert lib.XFPredict(ctypes.byref(h), ctypes.byref(ll), ctypes.byref(auc)) == 0
+        assert -1.0 < ll.value < -0.5 and 0.5 < auc.value < 0.7
+        assert lib.XFSave(ctypes.byref(h), str(tmp_path / "t.xftb").encode()) == 0
+        assert lib.XFFree(ctypes.byref(h)) == 0 and not h.value
+        bad = ctypes.c_void_p()
+        assert lib.XFCreate(ctypes.byref(bad), b"/nonexistent/x", TEST.encode()) == 0
+        assert lib.XFStartTrain(ctypes.byref(bad)) == -1
+        assert b"error" in lib.XFGetLastError()
+        lib.XFFree(ctypes.byref(bad))
+    finally:
+        os.chdir(cwd)

@@ -1,0 +1,127 @@
+"""Dedup scratch (persistence, epoch stamps, device-side rebuild), synthetic
+data generator, FTRL / sigmoid scalar recipes, on the CPU backend and (gpu
+marker) on the gfx950 HIP backend."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import random_csr, to_batch
+from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+from xflow_amd.data.synth import SynthConfig, SyntheticCriteo, criteo_vocab
+from xflow_amd.engine import Engine
+from xflow_amd.testing import torch_ref
+
+DEVICES = [pytest.param("cpu", id="cpu"), pytest.param("cuda", id="gpu", marks=pytest.mark.gpu)]
+
+
+def _dev(name):
+    return torch.device("cuda", 0) if name == "cuda" else torch.device("cpu")
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+def test_dedup_unique_count_over_many_steps_with_rebuild(devname):
+    dev = _dev(devname)
+    # tiny scratch (factor 2.5 of 512 nnz -> 2048 slots, rebuild at 1024 claims)
+    eng = Engine(ModelConfig(), OptimConfig(),
+                 EngineConfig(table_log2_cap=16, max_rows=64, max_nnz=512), device=dev)
+    seen = set()
+    for step in range(40):
+        k, rp, fg, lab = random_csr(64, 6, vocab=400 + 50 * step, seed=step)
+        b = to_batch(k, rp, fg, lab, dev)
+        eng.train_step(b)
+        assert eng.n_unique() == len(np.unique(k)), step
+        seen.update(k.tolist())
+    assert eng.table_size() == len(seen)
+    assert not eng.overflowed()
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+def test_eval_does_not_insert(devname):
+    dev = _dev(devname)
+    eng = Engine(ModelConfig(kind="fm", v_dim=4), OptimConfig(),
+                 EngineConfig(table_log2_cap=12, max_rows=64, max_nnz=1024), device=dev)
+    k, rp, fg, lab = random_csr(64, 6, seed=3)
+    p = eng.eval_step(to_batch(k, rp, fg, lab, dev))
+    assert eng.table_size() == 0
+    assert torch.isfinite(p).all() and p.shape == (64,)
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+def test_synthetic_criteo_shape(devname):
+    dev = _dev(devname)
+    rows = 4096
+    cfg = SynthConfig()
+    eng = Engine(ModelConfig(kind="mvm", v_dim=4), OptimConfig(),
+                 EngineConfig(table_log2_cap=16, max_rows=rows, max_nnz=rows * cfg.fields),
+                 device=dev)
+    gen = SyntheticCriteo(eng, rows, cfg)
+    b = gen.alloc_batch()
+    gen.next(out=b)
+    k = b.keys.cpu().numpy().reshape(rows, cfg.fields)
+    assert (k >= 0).all() and (k < cfg.hash_space).all()
+    assert (b.fgid.cpu().numpy().reshape(rows, -1) == np.arange(cfg.fields)).all()
+    y = b.labels.cpu().numpy()
+    assert set(np.unique(y)) <= {0.0, 1.0} and 0.1 < y.mean() < 0.45
+    # power-law: the 3-valued field has very few distinct keys, big fields many
+    small = cfg.vocab.index(3)
+    assert len(np.unique(k[:, small])) <= 3
+    assert len(np.unique(k[:, 13])) > 500
+    # counter based: same (seed, step) -> same batch, next step differs
+    b2 = gen.alloc_batch()
+    gen.step = 0
+    gen.next(out=b2)
+    assert torch.equal(b.keys, b2.keys)
+    gen.next(out=b2)
+    assert not torch.equal(b.keys, b2.keys)
+    assert sum(criteo_vocab()) >= 999_000_000
+
+
+@pytest.mark.gpu
+def test_synthetic_gpu_equals_cpu():
+    rows = 2048
+    cfg = SynthConfig()
+    out = []
+    for dev in (torch.device("cpu"), torch.device("cuda", 0)):
+        eng = Engine(ModelConfig(), OptimConfig(),
+                     EngineConfig(table_log2_cap=12, max_rows=rows, max_nnz=rows * 39), device=dev)
+        gen = SyntheticCriteo(eng, rows, cfg)
+        b = gen.alloc_batch()
+        gen.next(out=b)
+        out.append((b.keys.cpu().numpy(), b.labels.cpu().numpy()))
+    assert (out[0][0] == out[1][0]).mean() > 0.9999   # double pow may differ in the last ulp
+    assert (out[0][1] == out[1][1]).mean() > 0.999
+
+
+def test_sigmoid_reference_clamps(native):
+    eng = Engine(ModelConfig(), OptimConfig(), EngineConfig(table_log2_cap=8, max_rows=8,
+                                                            max_nnz=64))
+    x = torch.tensor([-40.0, -30.5, -30.0, -1.0, 0.0, 0.7, 30.0, 30.5, 50.0])
+    p = torch_ref.sigmoid_ref(x)
+    assert p[0] == pytest.approx(1e-6) and p[1] == pytest.approx(1e-6)
+    assert p[-1] == 1.0 and p[-2] == 1.0
+    ex = math.pow(2.718281828, 0.7)
+    assert p[5].item() == pytest.approx(ex / (1 + ex), rel=1e-7)
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+def test_ftrl_single_key_closed_form(devname):
+    """One key, explicit gradients: table state follows ftrl.h:58-74 exactly."""
+    dev = _dev(devname)
+    eng = Engine(ModelConfig(), OptimConfig(), EngineConfig(table_log2_cap=8, max_rows=8,
+                                                            max_nnz=64), device=dev)
+    a, b, l1, l2 = np.float32(0.05), np.float32(1.0), np.float32(5e-5), np.float32(10.0)
+    w = n = z = np.float32(0)
+    for g in [0.3, -0.2, 1e-5, 0.7, -0.9]:
+        g = np.float32(g)
+        eng.push([12345], [g])
+        nn = np.float32(n + g * g)
+        z = np.float32(z + np.float32(g - np.float32(np.float32(np.sqrt(nn) - np.sqrt(n)) / a) * w))
+        n = nn
+        if abs(z) <= l1:
+            w = np.float32(0)
+        else:
+            tmpr = np.float32(z - l1) if z > 0 else np.float32(z + l1)
+            w = np.float32(tmpr / np.float32(-1.0 * np.float32(np.float32(b + np.sqrt(n)) / a + l2)))
+        assert eng.pull([12345])[0, 0] == w

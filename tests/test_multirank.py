@@ -1,0 +1,144 @@
+"""Multi-rank (gloo, CPU) tests of the sharded table + sparse all-to-all path.
+
+Equivalence: one lock-step step on W ranks with S slices each equals one
+single-rank step whose batch concatenates the ranks' batches as W*S ordered
+slices (every slice reads the same weights; owners apply pushes in (source,
+slice) order; gradients normalised per slice)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_world
+from helpers import random_csr, to_batch
+from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+from xflow_amd.engine import Engine
+from xflow_amd.testing.hashing import owner_of
+
+ROWS, FIELDS, VOCAB, STEPS = 64, 6, 80, 3
+
+
+def _batches(rank, step):
+    return random_csr(ROWS, FIELDS, VOCAB, seed=1000 * step + rank)
+
+
+def _make_engine(kind, slices):
+    return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
+                  EngineConfig(table_log2_cap=14, max_rows=4 * ROWS, max_nnz=4 * ROWS * 16,
+                               max_slices=4 * slices))
+
+
+def _sharded_worker(rank, world, kind, slices, out_dir):
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    eng = _make_engine(kind, slices)
+    sh = ShardedEngine(eng)
+    for step in range(STEPS):
+        k, rp, fg, lab = _batches(rank, step)
+        sh.train_step(to_batch(k, rp, fg, lab, torch.device("cpu"), slice_rows=ROWS // slices),
+                      S=slices)
+    keys, words = eng.export_table()
+    np.save(os.path.join(out_dir, f"keys{rank}.npy"), keys)
+    vals = eng.pull(keys) if len(keys) else np.zeros((0, eng.params_per_key), np.float32)
+    np.save(os.path.join(out_dir, f"vals{rank}.npy"), vals)
+    st = eng.read_stats()
+    np.save(os.path.join(out_dir, f"stats{rank}.npy"), np.array([st["rows"], st["ln_loss"]]))
+
+
+@pytest.mark.parametrize("kind,slices", [("lr", 1), ("lr", 2), ("fm", 2), ("mvm", 1)])
+def test_sharded_equals_single_rank(tmp_path, kind, slices):
+    world = 2
+    run_world(_sharded_worker, world, kind, slices, str(tmp_path))
+    # single-rank replay: concatenated batches, world*slices ordered slices
+    ref = _make_engine(kind, slices)
+    for step in range(STEPS):
+        parts = [_batches(r, step) for r in range(world)]
+        keys = np.concatenate([p[0] for p in parts])
+        fg = np.concatenate([p[2] for p in parts])
+        lab = np.concatenate([p[3] for p in parts])
+        rp = np.concatenate([parts[0][1]] + [p[1][1:] + len(parts[0][0]) for p in parts[1:]])
+        ref.train_step(to_batch(keys, rp.astype(np.int32), fg, lab, torch.device("cpu"),
+                                slice_rows=ROWS // slices))
+    allk, allv = [], []
+    for r in range(world):
+        k = np.load(tmp_path / f"keys{r}.npy")
+        assert (owner_of(k, world) == r).all(), "a rank holds keys it does not own"
+        allk.append(k)
+        allv.append(np.load(tmp_path / f"vals{r}.npy"))
+    k = np.concatenate(allk)
+    v = np.concatenate(allv)
+    assert len(np.unique(k)) == len(k)
+    want = ref.pull(k)
+    assert ref.table_size() == len(k)
+    np.testing.assert_allclose(v, want, rtol=1e-4, atol=1e-6)
+    rows = sum(np.load(tmp_path / f"stats{r}.npy")[0] for r in range(world))
+    assert rows == world * ROWS * STEPS
+
+
+def _ckpt_worker(rank, world, ckpt_dir, out_dir):
+    from xflow_amd import checkpoint
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    eng = _make_engine("fm", 1)
+    sh = ShardedEngine(eng)
+    for step in range(2):
+        k, rp, fg, lab = _batches(rank, step)
+        sh.train_step(to_batch(k, rp, fg, lab, torch.device("cpu")))
+    checkpoint.save(eng, ckpt_dir, rank, world, meta={"epoch": 1})
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"k{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"v{rank}.npy"), eng.pull(keys))
+
+
+def _reload_worker(rank, world, ckpt_dir, out_dir):
+    from xflow_amd import checkpoint
+
+    eng = _make_engine("fm", 1)
+    meta = checkpoint.load(eng, ckpt_dir, rank, world)
+    assert meta["epoch"] == 1 and meta["world"] == 2
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"rk{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"rv{rank}.npy"), eng.pull(keys))
+
+
+def test_checkpoint_reshard_2_to_1_and_3(tmp_path):
+    ck = str(tmp_path / "ckpt")
+    run_world(_ckpt_worker, 2, ck, str(tmp_path))
+    k = np.concatenate([np.load(tmp_path / f"k{r}.npy") for r in range(2)])
+    v = np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(2)])
+    order = np.argsort(k)
+    # world 1: one engine loads every shard
+    from xflow_amd import checkpoint
+
+    one = _make_engine("fm", 1)
+    checkpoint.load(one, ck, 0, 1)
+    np.testing.assert_array_equal(one.pull(k[order]), v[order])
+    # world 3: keys re-sharded by the new owner function
+    run_world(_reload_worker, 3, ck, str(tmp_path))
+    k3 = np.concatenate([np.load(tmp_path / f"rk{r}.npy") for r in range(3)])
+    v3 = np.concatenate([np.load(tmp_path / f"rv{r}.npy") for r in range(3)])
+    o3 = np.argsort(k3)
+    np.testing.assert_array_equal(k3[o3], k[order])
+    np.testing.assert_array_equal(v3[o3], v[order])
+
+
+def _trainer_worker(rank, world, data_dir, pred_dir):
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
+                      test_prefix=os.path.join(data_dir, "small_test"), epochs=3, threads=4,
+                      pred_dir=pred_dir, engine=EngineConfig(table_log2_cap=14))
+    t = Trainer(cfg, device=torch.device("cpu"))
+    res = t.train()
+    if rank == 0:
+        assert res["n"] == 200 and 0.0 < res["auc"] < 1.0
+
+
+def test_trainer_two_workers_bundled_data(tmp_path):
+    from conftest import DATA
+
+    run_world(_trainer_worker, 2, DATA, str(tmp_path))
+    pred = np.loadtxt(tmp_path / "pred_0_0.txt")
+    assert pred.shape == (200, 3)

@@ -1,0 +1,105 @@
+"""``xflow_lr``-compatible command line (multi-rank capable).
+
+    python -m xflow_amd.cli <train_prefix> <test_prefix> <model 0|1|2> <epochs> [flags]
+
+Positional arguments are the reference binary's (src/model/main.cc:15-48).
+Process roles follow the reference launch scripts' DMLC_ROLE: scheduler and
+server processes exit (the workers' GPUs hold the table shards); workers
+train.  World size / rank come from torchrun env (RANK, WORLD_SIZE, ...) or
+DMLC_NUM_WORKER / DMLC_WORKER_ID (scripts/local.sh sets both).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import torch
+
+from xflow_amd.config import (EngineConfig, ModelConfig, OptimConfig, TrainConfig,
+                              MODEL_NAMES, model_kind)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="xflow_lr", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("train_prefix")
+    ap.add_argument("test_prefix")
+    ap.add_argument("model", help="0 = LR, 1 = FM, 2 = MVM (or lr/fm/mvm)")
+    ap.add_argument("epochs", type=int)
+    ap.add_argument("--threads", type=int, default=0,
+                    help="slices per block (default: os.cpu_count(), like hardware_concurrency)")
+    ap.add_argument("--serial-slices", action="store_true",
+                    help="one step per slice instead of all slices in one step")
+    ap.add_argument("--keep-remainder", action="store_true",
+                    help="train rows %% threads too (the reference drops them)")
+    ap.add_argument("--optimizer", choices=["ftrl", "sgd"], default="ftrl")
+    ap.add_argument("--alpha", type=float, default=5e-2)
+    ap.add_argument("--beta", type=float, default=1.0)
+    ap.add_argument("--lambda1", type=float, default=5e-5)
+    ap.add_argument("--lambda2", type=float, default=10.0)
+    ap.add_argument("--lr", type=float, default=1e-3, help="SGD learning rate")
+    ap.add_argument("--v-dim", type=int, default=10)
+    ap.add_argument("--fm-math", choices=["reference", "standard"], default="reference")
+    ap.add_argument("--mvm-math", choices=["compat", "fixed"], default="compat")
+    ap.add_argument("--mvm-predict-compat", action="store_true")
+    ap.add_argument("--sum-slices", action="store_true",
+                    help="one FTRL push of the summed slice gradients per step")
+    ap.add_argument("--no-init-push", action="store_true")
+    ap.add_argument("--log2-cap", type=int, default=22, help="table slots per rank = 2^N")
+    ap.add_argument("--train-block-bytes", type=int, default=2 << 20)
+    ap.add_argument("--test-block-bytes", type=int, default=0)
+    ap.add_argument("--cpu", action="store_true", help="use the native CPU backend")
+    ap.add_argument("--pred-dir", default=".")
+    ap.add_argument("--save", default="", help="checkpoint directory to write after training")
+    ap.add_argument("--load", default="", help="checkpoint directory to resume from")
+    ap.add_argument("--metrics", default="", help="JSON-lines metrics file (rank 0)")
+    ap.add_argument("--trace-dir", default="", help="torch.profiler chrome trace directory")
+    return ap
+
+
+def config_from_args(a) -> TrainConfig:
+    kind = MODEL_NAMES[model_kind(a.model)]
+    return TrainConfig(
+        train_prefix=a.train_prefix, test_prefix=a.test_prefix, epochs=a.epochs,
+        threads=a.threads, train_block_bytes=a.train_block_bytes,
+        test_block_bytes=a.test_block_bytes, serial_slices=a.serial_slices,
+        keep_remainder=a.keep_remainder, mvm_predict_compat=a.mvm_predict_compat,
+        init_push=not a.no_init_push, pred_dir=a.pred_dir, checkpoint_dir=a.save,
+        metrics_file=a.metrics,
+        model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math),
+        optim=OptimConfig(kind=a.optimizer, alpha=a.alpha, beta=a.beta, lambda1=a.lambda1,
+                          lambda2=a.lambda2, lr=a.lr),
+        engine=EngineConfig(table_log2_cap=a.log2_cap, sum_slices=a.sum_slices))
+
+
+def main(argv=None) -> int:
+    from xflow_amd.parallel import dist as xdist
+
+    if xdist.is_scheduler():
+        return 0
+    if xdist.is_server():
+        print("init server success ", flush=True)
+        return 0
+    a = build_parser().parse_args(argv)
+    cfg = config_from_args(a)
+    print({0: "start LR ", 1: "start FM ", 2: "start MVM "}[model_kind(a.model)], flush=True)
+    device = torch.device("cpu") if a.cpu else xdist.device_for_rank()
+    from xflow_amd.trainer import Trainer
+    from xflow_amd.utils.trace import torch_profile
+
+    t = Trainer(cfg, device=device)
+    try:
+        if a.load:
+            t.load(a.load)
+        with torch_profile(a.trace_dir):
+            t.train()
+        if a.save:
+            t.save(a.save)
+    finally:
+        t.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

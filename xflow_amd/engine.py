@@ -179,16 +179,24 @@ class Engine:
         self._sync_stream()
         self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr())
 
-    def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor) -> None:
+    def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor,
+               insert: bool = True) -> None:
         self._sync_stream()
-        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr())
+        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr(), insert)
+
+    def w_forward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
+                  pctr: torch.Tensor | None) -> None:
+        self._sync_stream()
+        self._e.w_forward(batch.view(), pulled.data_ptr(), int(n_send),
+                          pctr.data_ptr() if pctr is not None else 0)
 
     def w_forward_backward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
-                           grads_out: torch.Tensor, masks_out: torch.Tensor | None) -> None:
+                           grads_out: torch.Tensor, masks_out: torch.Tensor | None,
+                           S: int = 0) -> None:
         self._sync_stream()
         self._e.w_forward_backward(batch.view(), pulled.data_ptr(), int(n_send),
                                    grads_out.data_ptr(),
-                                   masks_out.data_ptr() if masks_out is not None else 0)
+                                   masks_out.data_ptr() if masks_out is not None else 0, int(S))
 
     def s_apply(self, recv_keys: torch.Tensor, recv_grads: torch.Tensor,
                 recv_masks: torch.Tensor | None, offsets, S: int) -> None:

@@ -15,12 +15,18 @@ fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
   7. a2a grads    (+ slice masks when slices are applied in order)
   8. s_apply      owner applies contributions source by source (fixed order:
                   deterministic, the analogue of ps-lite's serialized handler)
-  9. w_finish     release the dedup scratch
 
 Collectives go through torch.distributed: backend "nccl" is RCCL on ROCm
 (xGMI peer links between the node's GPUs), "gloo" runs the same code on CPU for
 tests.  Each all-to-all moves only the touched keys (8 B) and their P floats,
-so a step's traffic is ~K*(8+8P) bytes per rank, spread over all 7 xGMI links.
+so a step's traffic is ~K*(8+8P) bytes per rank, spread over all 7 xGMI links
+instead of a dense all-reduce of the table.
+
+Consistency: steps are lock-step across ranks (every rank joins every
+exchange; a rank without data passes an empty batch).  The reference's workers
+are asynchronous; here all slices of all ranks in a step read the same table
+state, and each owner applies the (source, slice) pushes one by one in source
+order -- a deterministic serialisation of the reference's arrival-order pushes.
 """
 from __future__ import annotations
 
@@ -57,7 +63,7 @@ class ShardedEngine:
         dev = engine.device
         self.counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
         self.recv_counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
-        self.send_keys = torch.empty(engine.cfg.max_nnz, dtype=torch.int64, device=dev)
+        self.send_keys = torch.empty(max(engine.cfg.max_nnz, 1), dtype=torch.int64, device=dev)
         self._recv_keys = _Buf(torch.int64, dev)
         self._vals_out = _Buf(torch.float32, dev)
         self._pulled = _Buf(torch.float32, dev)
@@ -72,30 +78,45 @@ class ShardedEngine:
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def train_step(self, batch: Batch) -> None:
+    def _exchange_keys(self, batch: Batch):
+        """Dedup + bucket + key all-to-all.  Returns (send, recv splits, recv keys)."""
         e = self.engine
-        S = e.slices_of(batch)
-        ps = e.pstride
-        ordered_masks = S > 1 and not e.cfg.sum_slices
         e.w_prepare(batch, self.world, self.counts, self.send_keys)
         self._a2a(self.recv_counts, self.counts, None, None)
         both = torch.cat([self.counts, self.recv_counts]).cpu().tolist()
         send_splits, recv_splits = both[: self.world], both[self.world:]
         n_send, n_recv = int(sum(send_splits)), int(sum(recv_splits))
         self.last_send, self.last_recv = n_send, n_recv
-
         recv_keys = self._recv_keys.get(n_recv)
         self._a2a(recv_keys, self.send_keys[:n_send], recv_splits, send_splits)
+        return send_splits, recv_splits, recv_keys
 
+    def _pull(self, recv_keys, send_splits, recv_splits, insert: bool) -> torch.Tensor:
+        e = self.engine
+        ps = e.pstride
+        n_send, n_recv = sum(send_splits), sum(recv_splits)
         vals = self._vals_out.get(n_recv * ps).view(n_recv, ps)
-        e.s_pull(recv_keys, n_recv, vals)
+        e.s_pull(recv_keys, n_recv, vals, insert=insert)
         pulled = self._pulled.get(n_send * ps).view(n_send, ps)
         self._a2a(pulled, vals, send_splits, recv_splits)
+        return pulled
+
+    def train_step(self, batch: Batch, S: Optional[int] = None) -> None:
+        """One lock-step training step.  S = slices per step, identical on every
+        rank (defaults to this batch's slice count, fine when all ranks use the
+        same batch shape)."""
+        e = self.engine
+        S = int(S) if S else e.slices_of(batch)
+        ps = e.pstride
+        ordered_masks = S > 1 and not e.cfg.sum_slices
+        send_splits, recv_splits, recv_keys = self._exchange_keys(batch)
+        n_send, n_recv = self.last_send, self.last_recv
+        pulled = self._pull(recv_keys, send_splits, recv_splits, insert=True)
 
         W = S * ps
         grads_out = self._grads_out.get(n_send * W).view(n_send, W)
         masks_out = self._masks_out.get(n_send) if ordered_masks else None
-        e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out)
+        e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S)
         grads_in = self._grads_in.get(n_recv * W).view(n_recv, W)
         self._a2a(grads_in, grads_out, recv_splits, send_splits)
         masks_in = None
@@ -107,9 +128,15 @@ class ShardedEngine:
             offsets.append(offsets[-1] + int(c))
         e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
         e.w_finish()
-        self.bytes_moved += (n_send + n_recv) * 8 + (n_send + n_recv) * ps * 4 + \
-            (n_send + n_recv) * W * 4
+        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)
 
-    def eval_pull_step(self, batch: Batch, pctr: torch.Tensor) -> torch.Tensor:
-        """Forward-only step for sharded evaluation (keys are not inserted)."""
-        raise NotImplementedError  # implemented in xflow_amd.trainer via local pull
+    def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Forward-only sharded step (keys looked up, never inserted).  Every
+        rank must call it (a rank without test data passes an empty batch)."""
+        e = self.engine
+        if pctr is None:
+            pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
+        send_splits, recv_splits, recv_keys = self._exchange_keys(batch)
+        pulled = self._pull(recv_keys, send_splits, recv_splits, insert=False)
+        e.w_forward(batch, pulled, self.last_send, pctr if batch.rows else None)
+        return pctr

@@ -1,0 +1,268 @@
+"""Multi-rank training loop over libffm shards (Python orchestration of the
+native engine).
+
+Reference: the workers' batch_training / predict / train
+(/root/reference/src/model/lr/lr_worker.cc:73-217, fm_worker.cc:98-287,
+mvm_worker.cc:109-314).  Same data contract: rank r trains on
+``<train_prefix>-%05d`` (r) block by block (2 MB blocks, rows split into
+``threads`` slices of rows//threads, remainder dropped), then rank 0 predicts
+``<test_prefix>-00000``, writes ``pred_0_0.txt`` and prints the reference's
+``logloss: .. auc = ..`` line.
+
+Differences by design (MI355X-first):
+* the parameter server is the ranks' own HBM table shards; Pull/Push are the
+  sparse all-to-alls of parallel/sparse_a2a.py (world > 1) or the fused
+  single-rank step;
+* the reference's Hogwild threads become the S slices of one step (all read
+  the same weights, pushes applied in slice order), or one step per slice
+  (serial_slices);
+* ranks advance in lock-step; a rank that ran out of blocks joins each
+  exchange with an empty batch until every rank is done with the epoch.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from xflow_amd import checkpoint
+from xflow_amd import native as _native
+from xflow_amd.config import TrainConfig, model_kind
+from xflow_amd.engine import Batch, Engine
+from xflow_amd.metrics import MetricsLogger, reference_auc
+from xflow_amd.parallel import dist as xdist
+from xflow_amd.testing.hashing import owner_of
+from xflow_amd.utils.trace import PhaseTimer
+
+
+def shard_path(prefix: str, rank: int) -> str:
+    return "%s-%05d" % (prefix, rank)
+
+
+def _say(msg: str) -> None:
+    print(msg, flush=True)
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig, device: Optional[torch.device] = None):
+        self.cfg = cfg
+        self.world = xdist.start(device)
+        self.rank = xdist.my_rank()
+        self.device = device or xdist.device_for_rank()
+        self.threads = cfg.resolved_threads()
+        self.concurrent = not cfg.serial_slices
+        if self.concurrent and self.threads > 32:
+            raise ValueError("concurrent slices: at most 32 per block; use serial_slices")
+        self.S = self.threads if self.concurrent else 1
+        max_block = max(cfg.train_block_bytes, cfg.resolved_test_block())
+        ecfg = cfg.engine
+        ecfg.max_rows = max(ecfg.max_rows, max_block // 2 + 16)
+        ecfg.max_nnz = max(ecfg.max_nnz, max_block // 2 + 16)
+        ecfg.max_slices = max(ecfg.max_slices, self.S)
+        self.engine = Engine(cfg.model, cfg.optim, ecfg, device=self.device)
+        self.sharded = None
+        if self.world > 1:
+            from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+            self.sharded = ShardedEngine(self.engine)
+        self.metrics = MetricsLogger(cfg.metrics_file, self.rank)
+        self.timer = PhaseTimer(self.device, enabled=bool(os.environ.get("XFLOW_TRACE")))
+        self.epoch = 0
+        self.steps = 0
+        self.samples = 0
+        self._with_fgid = model_kind(cfg.model.kind) == 2
+
+    # ------------------------------------------------------------------ data
+    def _to_batch(self, blk: Optional[dict], used: int, slice_rows: int) -> Batch:
+        dev = self.device
+        if blk is None or used <= 0:
+            return Batch(keys=torch.empty(0, dtype=torch.int64, device=dev),
+                         labels=torch.empty(0, dtype=torch.float32, device=dev),
+                         row_ptr=torch.zeros(1, dtype=torch.int32, device=dev),
+                         fgid=torch.empty(0, dtype=torch.int32, device=dev),
+                         slice_rows=max(slice_rows, 1))
+        rp = blk["row_ptr"][: used + 1]
+        nnz = int(rp[-1])
+        pin = dev.type == "cuda"
+
+        def up(a):
+            t = torch.from_numpy(np.ascontiguousarray(a))
+            if pin:
+                t = t.pin_memory()
+            return t.to(dev, non_blocking=True)
+
+        return Batch(keys=up(blk["keys"][:nnz].view(np.int64)), labels=up(blk["labels"][:used]),
+                     row_ptr=up(rp), fgid=up(blk["fgid"][:nnz]) if self._with_fgid else None,
+                     slice_rows=slice_rows)
+
+    def _split(self, rows: int):
+        """(used rows, slice rows) under the reference's slicing rule."""
+        ts = rows // self.threads
+        if self.cfg.keep_remainder:
+            return rows, max(1, -(-rows // self.threads))
+        return ts * self.threads, ts
+
+    def _step(self, batch: Batch) -> None:
+        if self.sharded is not None:
+            self.sharded.train_step(batch, S=self.S)
+        elif batch.rows > 0:
+            self.engine.train_step(batch)
+
+    def _slices_of(self, blk: Optional[dict]):
+        """Batches of one block: one concurrent step, or one step per slice."""
+        rows = 0 if blk is None else len(blk["labels"])
+        used, sr = self._split(rows)
+        if self.concurrent or blk is None or used <= 0:
+            yield self._to_batch(blk, used, sr)
+            return
+        rp = blk["row_ptr"]
+        for s0 in range(0, used, sr):
+            n = min(sr, used - s0)
+            sub = {"row_ptr": rp[s0: s0 + n + 1] - rp[s0],
+                   "keys": blk["keys"][rp[s0]: rp[s0 + n]],
+                   "fgid": blk["fgid"][rp[s0]: rp[s0 + n]],
+                   "labels": blk["labels"][s0: s0 + n]}
+            yield self._to_batch(sub, n, n)
+
+    # ----------------------------------------------------------------- train
+    def init_push(self) -> None:
+        """Reference initialisation pushes: key 0 (LR, FM: w and v) / key 1 (MVM)
+        with zero gradients (lr_worker.cc:180-182, fm_worker.cc:248-252,
+        mvm_worker.cc:276-278), applied once by the key's owner."""
+        key = 1 if model_kind(self.cfg.model.kind) == 2 else 0
+        if int(owner_of(np.array([key], dtype=np.uint64), self.world)[0]) == self.rank:
+            self.engine.push([key], np.zeros(self.engine.params_per_key, dtype=np.float32))
+        xdist.barrier()
+
+    def train_epochs(self, epochs: int) -> None:
+        cfg = self.cfg
+        path = shard_path(cfg.train_prefix, self.rank)
+        nat = _native.load()
+        log_every = int(os.environ.get("XFLOW_LOG_EVERY", "0"))
+        for _ in range(epochs):
+            reader = nat.PrefetchReader(path, cfg.train_block_bytes)
+            t0 = time.perf_counter()
+            ep_samples = 0
+            while True:
+                blk = reader.next()
+                if not xdist.all_any(blk is not None, self.device):
+                    break
+                for b in self._slices_of(blk):
+                    with self.timer.phase("step"):
+                        self._step(b)
+                    self.steps += 1
+                    ep_samples += b.rows
+                    if log_every and self.steps % log_every == 0:
+                        self._log_progress(ep_samples, t0)
+            self.samples += ep_samples
+            self.epoch += 1
+            if self.epoch % 30 == 0:
+                _say("epoch : %d" % (self.epoch - 1))
+            st = self.engine.read_stats(reset=True)
+            tot = xdist.all_sum([st["ln_loss"], st["rows"], ep_samples], self.device)
+            self.metrics.log(event="epoch", epoch=self.epoch, steps=self.steps,
+                             train_logloss=tot[0] / max(tot[1], 1.0),
+                             samples_per_s=tot[2] / max(time.perf_counter() - t0, 1e-9),
+                             table_keys=self.engine.table_size())
+            if cfg.checkpoint_dir and os.environ.get("XFLOW_CKPT_EVERY_EPOCH"):
+                self.save(cfg.checkpoint_dir)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def _log_progress(self, ep_samples: int, t0: float) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        rate = ep_samples / max(time.perf_counter() - t0, 1e-9)
+        rec = dict(event="progress", epoch=self.epoch, step=self.steps, samples_per_s=rate,
+                   unique_keys=self.engine.n_unique())
+        if self.sharded is not None:
+            rec["a2a_bytes"] = self.sharded.bytes_moved
+        self.metrics.log(**rec)
+
+    # --------------------------------------------------------------- predict
+    def predict(self, block: int = 0) -> Optional[dict]:
+        """Rank 0 predicts its test shard; other ranks serve their table shards."""
+        cfg = self.cfg
+        nat = _native.load()
+        labels, preds = [], []
+        reader = None
+        if self.rank == 0:
+            reader = nat.BlockReader(shard_path(cfg.test_prefix, 0), cfg.resolved_test_block())
+        compat_mvm = model_kind(cfg.model.kind) == 2 and cfg.mvm_predict_compat
+        while True:
+            blk = reader.next() if reader is not None else None
+            if not xdist.all_any(blk is not None, self.device):
+                break
+            rows = 0 if blk is None else len(blk["labels"])
+            used, sr = self._split(rows)
+            b = self._to_batch(blk, used, sr)
+            if self.sharded is not None:
+                pctr = self.sharded.eval_step(b)
+            elif b.rows > 0:
+                pctr = self.engine.eval_step(b)
+            else:
+                continue
+            if b.rows == 0:
+                continue
+            p = pctr.cpu().numpy()
+            lab = blk["labels"][:used].astype(np.int32)
+            if compat_mvm and sr > 0:
+                keep = (np.arange(used) % sr) < min(self.engine.model.v_dim, sr)
+                p, lab = p[keep], lab[keep]
+            preds.append(p)
+            labels.append(lab)
+        if self.rank != 0:
+            return None
+        p = np.concatenate(preds) if preds else np.zeros(0, np.float32)
+        y = np.concatenate(labels) if labels else np.zeros(0, np.int32)
+        os.makedirs(cfg.pred_dir or ".", exist_ok=True)
+        with open(os.path.join(cfg.pred_dir or ".", "pred_%d_%d.txt" % (self.rank, block)), "w") as f:
+            for pi, yi in zip(p.tolist(), y.tolist()):
+                f.write("%s\t%d\t%d\n" % (_fmt_float(pi), 1 - yi, yi))
+        res = reference_auc(y, p)
+        _say(res["line"])
+        self.metrics.log(event="eval", auc=res["auc"], ln_logloss=res["ln_logloss"],
+                         logloss_printed=res["logloss_printed"], n=res["n"])
+        return res
+
+    def train(self) -> Optional[dict]:
+        """The reference's Worker::train(): log rank, train, rank-0 predict."""
+        _say("my rank is = %d" % self.rank)
+        if self.cfg.init_push:
+            self.init_push()
+        self.train_epochs(self.cfg.epochs)
+        res = None
+        if self.rank == 0:
+            _say("LR AUC: " if model_kind(self.cfg.model.kind) == 0 else "FM AUC: ")
+        res = self.predict(0)
+        _say("train end......")
+        return res
+
+    # ------------------------------------------------------------ checkpoint
+    def save(self, ckpt_dir: str) -> None:
+        checkpoint.save(self.engine, ckpt_dir, self.rank, self.world,
+                        meta={"epoch": self.epoch, "steps": self.steps})
+        xdist.barrier()
+
+    def load(self, ckpt_dir: str) -> dict:
+        meta = checkpoint.load(self.engine, ckpt_dir, self.rank, self.world)
+        self.epoch = int(meta.get("epoch", 0))
+        self.steps = int(meta.get("steps", 0))
+        xdist.barrier()
+        return meta
+
+    def close(self) -> None:
+        xdist.finalize()
+
+
+def _fmt_float(x: float) -> str:
+    """C++ ostream default float formatting (%g, 6 significant digits)."""
+    return "%g" % x
+
+
+if __name__ == "__main__":  # pragma: no cover
+    sys.exit("use python -m xflow_amd.cli")
