@@ -354,12 +354,13 @@ class CpuBackend final : public Backend {
 
   void synth_batch(const SynthArgs& a) override {
     if (a.fields > kSynthMaxFields) throw std::runtime_error("synth: at most 64 fields");
+    std::vector<SynthField> F(a.fields);
+    for (int f = 0; f < a.fields; ++f) F[f] = synth_field(a.vocab[f], (double)a.zipf_s[f]);
     for (int64_t r = 0; r < a.rows; ++r) {
       const u64 rs = synth_row_seed(a.seed, a.step, r);
       float logit = a.planted_bias;
       for (int f = 0; f < a.fields; ++f) {
-        u64 v = a.vocab[f] ? a.vocab[f] : 1;
-        u64 key = synth_key(rs, f, v, (double)a.zipf_s[f], a.hash_space);
+        u64 key = synth_key(rs, f, F[f], a.hash_space);
         a.keys[r * a.fields + f] = key;
         if (a.fgid) a.fgid[r * a.fields + f] = f;
         logit += synth_planted_weight(key, a.planted_scale);

@@ -61,6 +61,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // keys, so the load factor stays below 0.5 + 1/factor.
   scratch_.rebuild_at = scratch_.cap / 2;
   scratch_.epoch = 0;
+  block_counts_ = balloc<u32>(be, scratch_.cap / 4096 + 1);
 
   const int ps = cfg_.model.pstride();
   pos_ = balloc<u32>(be, nnz);
@@ -91,7 +92,7 @@ Engine::~Engine() {
   Backend& be = *be_;
   be.synchronize();
   void* ptrs[] = {table_.words, table_.size, overflow_, scratch_.keys, scratch_.stamps,
-                  scratch_.claims, pos_, uniq_keys_,
+                  scratch_.claims, block_counts_, pos_, uniq_keys_,
                   uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_, host_keys_dev_, host_vals_dev_};
@@ -132,6 +133,7 @@ void Engine::dedup_(const BatchView& b) {
   o.uniq_pos = uniq_pos_;
   o.n_uniq = n_uniq_;
   o.overflow = overflow_;
+  o.block_counts = block_counts_;
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 

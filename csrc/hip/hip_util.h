@@ -63,6 +63,24 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Workgroup-wide sum of a per-lane count, then ONE no-return atomic by lane 0
+// of wave 0.  Bookkeeping counters (table size, dedup claims) are single
+// addresses: per-wave atomics on them serialise at one L2 channel.
+template <int BLOCK>
+__device__ __forceinline__ void block_count_add(unsigned long long* counter, unsigned int v) {
+  __shared__ unsigned int part[BLOCK / kWave];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (threadIdx.x % kWave == 0) part[threadIdx.x / kWave] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int t = 0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / kWave; ++i) t += part[i];
+    if (t) atomicAdd(counter, (unsigned long long)t);
+  }
+}
+
 // Read a device-side element count, clamped to the launch's upper bound.
 __device__ __forceinline__ int64_t dev_count(const int64_t* n_dev, int64_t n_host,
                                              int64_t n_max) {

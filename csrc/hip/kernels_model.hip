@@ -86,16 +86,17 @@ __device__ void flush_stats(StatAcc a, LossStats* out) {
 // atomic per distinct key.  Two tables alternate so one barrier per column
 // suffices: column j inserts into table j&1 while the flush of table (j-1)&1
 // by other waves completes before the next barrier.
-constexpr int kColSlots = 2 * kBlock;
 constexpr u32 kColEmpty = 0xFFFFFFFFu;
 
-template <int PS>
+// LOG2 = log2(table slots) = log2(2 * workgroup size)
+template <int PS, int LOG2>
 struct ColumnAgg {
-  u32 (*tag)[kColSlots];
-  float (*acc)[kColSlots * PS];
+  static constexpr int kSlots = 1 << LOG2;
+  u32 (*tag)[kSlots];
+  float (*acc)[kSlots * PS];
 
   __device__ __forceinline__ void init() {
-    for (int i = threadIdx.x; i < kColSlots; i += blockDim.x) {
+    for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         tag[t][i] = kColEmpty;
@@ -104,9 +105,10 @@ struct ColumnAgg {
       }
     }
   }
-  // slot of `dest` in table t (claimed on first use)
+  // slot of `dest` in table t (claimed on first use); a column inserts at most
+  // kSlots/2 keys, so the probe always terminates
   __device__ __forceinline__ int insert(int t, u32 dest) {
-    u32 h = (dest * 0x9E3779B1u) >> (32 - 9);  // kColSlots == 512
+    u32 h = (dest * 0x9E3779B1u) >> (32 - LOG2);
     while (true) {
       u32 cur = tag[t][h];
       if (cur == dest) return (int)h;
@@ -114,7 +116,7 @@ struct ColumnAgg {
         u32 old = atomicCAS(&tag[t][h], kColEmpty, dest);
         if (old == kColEmpty || old == dest) return (int)h;
       }
-      h = (h + 1) & (kColSlots - 1);
+      h = (h + 1) & (kSlots - 1);
     }
   }
   __device__ __forceinline__ void add(int t, int h, int c, float g) {
@@ -122,7 +124,7 @@ struct ColumnAgg {
   }
   // one global atomic per (distinct key, component); resets the table
   __device__ __forceinline__ void flush(int t, float* __restrict__ grad) {
-    for (int i = threadIdx.x; i < kColSlots; i += blockDim.x) {
+    for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
       u32 d = tag[t][i];
       if (d == kColEmpty) continue;
 #pragma unroll
@@ -136,17 +138,23 @@ struct ColumnAgg {
   }
 };
 
+constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
+
 // LR: the row gather keeps 4 independent pos->wpull chains in flight per lane;
 // the sum order is the row's feature order (bitwise equal to the CPU backend).
-template <bool kGrad, bool kAgg>
-__global__ void __launch_bounds__(kBlock) k_lr(FwdArgs a) {
-  __shared__ u32 s_tag[kAgg ? 2 : 1][kColSlots];
-  __shared__ float s_acc[kAgg ? 2 : 1][kColSlots];
+// BLOCK rows per workgroup: larger workgroups aggregate mid-frequency keys
+// better (Criteo-shaped batch: 4.29 M global atomics at 256 rows, 2.95 M at
+// 1024 rows, for 10.2 M occurrences).
+template <bool kGrad, bool kAgg, int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
+  constexpr int LOG2 = ilog2c(2 * BLOCK);
+  __shared__ u32 s_tag[kAgg ? 2 : 1][1 << LOG2];
+  __shared__ float s_acc[kAgg ? 2 : 1][1 << LOG2];
   __shared__ int s_maxlen;
   const BatchView& b = a.batch;
   const u32* __restrict__ pos = a.pos;
   const float* __restrict__ wp = a.wpull;
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool active = r < b.rows;
   RowRange rr{0, 0};
   StatAcc st;
@@ -176,7 +184,7 @@ __global__ void __launch_bounds__(kBlock) k_lr(FwdArgs a) {
     if (!kAgg) {
       for (int64_t q = rr.beg; q < rr.end; ++q) atomicAdd(&a.grad[pos[q] * S + s], loss);
     } else {
-      ColumnAgg<1> agg{s_tag, s_acc};
+      ColumnAgg<1, LOG2> agg{s_tag, s_acc};
       if (threadIdx.x == 0) s_maxlen = 0;
       agg.init();
       __syncthreads();
@@ -195,7 +203,7 @@ __global__ void __launch_bounds__(kBlock) k_lr(FwdArgs a) {
       }
     }
   }
-  flush_stats<kBlock>(st, a.stats);
+  flush_stats<BLOCK>(st, a.stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -352,12 +360,18 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
   const bool grad = a.grad != nullptr;
   int grid = (int)((a.batch.rows + kBlock - 1) / kBlock);
   switch (a.model.kind) {
-    case kLR:
+    case kLR: {
       // LDS aggregation needs every destination index to fit a u32 tag
-      if (grad && a.agg_ok) hipLaunchKernelGGL((k_lr<true, true>), dim3(grid), dim3(kBlock), 0, st, a);
-      else if (grad) hipLaunchKernelGGL((k_lr<true, false>), dim3(grid), dim3(kBlock), 0, st, a);
-      else hipLaunchKernelGGL((k_lr<false, false>), dim3(grid), dim3(kBlock), 0, st, a);
+      constexpr int kLrBlock = 1024;
+      int g = (int)((a.batch.rows + kLrBlock - 1) / kLrBlock);
+      if (grad && a.agg_ok)
+        hipLaunchKernelGGL((k_lr<true, true, kLrBlock>), dim3(g), dim3(kLrBlock), 0, st, a);
+      else if (grad)
+        hipLaunchKernelGGL((k_lr<true, false, kBlock>), dim3(grid), dim3(kBlock), 0, st, a);
+      else
+        hipLaunchKernelGGL((k_lr<false, false, kBlock>), dim3(grid), dim3(kBlock), 0, st, a);
       break;
+    }
     case kFM:
       if (grad) dispatch_fm<true>(a, grid, st);
       else dispatch_fm<false>(a, grid, st);

@@ -9,34 +9,45 @@ namespace xflow {
 namespace hip {
 
 struct SynthConsts {
-  u64 vocab[kSynthMaxFields];
-  float s[kSynthMaxFields];
+  SynthField f[kSynthMaxFields];
 };
 
+// A workgroup owns kSynthRows rows.  Lanes walk the tile's (row, field)
+// elements in memory order, so key/fgid stores are coalesced; each element's
+// planted weight is parked in LDS and one lane per row sums them in field
+// order (deterministic, the same order as the CPU backend).
+constexpr int kSynthRows = 64;
+
 __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= a.rows) return;
-  const u64 rs = synth_row_seed(a.seed, a.step, r);
-  float logit = a.planted_bias;
-  for (int f = 0; f < a.fields; ++f) {
-    u64 key = synth_key(rs, f, c.vocab[f], (double)c.s[f], a.hash_space);
-    a.keys[r * a.fields + f] = key;
-    if (a.fgid) a.fgid[r * a.fields + f] = f;
-    logit += synth_planted_weight(key, a.planted_scale);
+  __shared__ float pw[kSynthRows * kSynthMaxFields];
+  const int F = a.fields;
+  const int64_t r0 = (int64_t)blockIdx.x * kSynthRows;
+  const int rows = (int)min((int64_t)kSynthRows, a.rows - r0);
+  const int n = rows * F;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int rl = e / F, f = e - rl * F;
+    const int64_t r = r0 + rl;
+    const u64 key = synth_key(synth_row_seed(a.seed, a.step, r), f, c.f[f], a.hash_space);
+    a.keys[r0 * F + e] = key;
+    if (a.fgid) a.fgid[r0 * F + e] = f;
+    pw[e] = synth_planted_weight(key, a.planted_scale);
   }
-  a.labels[r] = synth_label(rs, logit);
+  __syncthreads();
+  if ((int)threadIdx.x < rows) {
+    const int64_t r = r0 + threadIdx.x;
+    float logit = a.planted_bias;
+    for (int f = 0; f < F; ++f) logit += pw[threadIdx.x * F + f];
+    a.labels[r] = synth_label(synth_row_seed(a.seed, a.step, r), logit);
+  }
 }
 
 void launch_synth(const SynthArgs& a, hipStream_t st) {
   if (a.rows <= 0) return;
   if (a.fields > kSynthMaxFields) throw std::runtime_error("synth: at most 64 fields");
   SynthConsts c;
-  for (int f = 0; f < a.fields; ++f) {
-    c.vocab[f] = a.vocab[f] ? a.vocab[f] : 1;
-    c.s[f] = a.zipf_s[f];
-  }
-  hipLaunchKernelGGL(k_synth, dim3((int)((a.rows + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, a,
-                     c);
+  for (int f = 0; f < a.fields; ++f) c.f[f] = synth_field(a.vocab[f], (double)a.zipf_s[f]);
+  hipLaunchKernelGGL(k_synth, dim3((int)((a.rows + kSynthRows - 1) / kSynthRows)), dim3(kBlock),
+                     0, st, a, c);
   XF_HIP_CHECK(hipGetLastError());
 }
 

@@ -100,55 +100,107 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
     pos[i] = (u32)sj;
     sv.stamps[sj] = sv.epoch;
   }
-  // one atomic per wave for the rebuild counter
-  unsigned int tot = claimed;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-  if (lane_id() == 0 && tot) atomicAdd(sv.claims, (unsigned long long)tot);
+  // one no-return atomic per workgroup for the rebuild counter
+  block_count_add<kBlock>(sv.claims, claimed);
 }
 
-// Step 2 -- compaction: scan the stamps (coalesced, cap*4 bytes) and emit
-// (key, slot) of every slot stamped with this epoch.  One global atomic per
-// workgroup.
+// Step 2 -- compaction of the slots stamped with this epoch into the unique
+// list, without a single global atomic: (a) each workgroup counts its 4096
+// slots (coalesced stamp reads), (b) one workgroup scans the counts, (c) each
+// workgroup re-reads its stamps (L3/L2 resident) and writes (key, slot) at
+// its offset.  Output order = slot order: deterministic.
 constexpr int kCompactItems = 16;
 constexpr int kCompactChunk = kBlock * kCompactItems;
+constexpr int kScanBlock = 1024;
 
-__global__ void __launch_bounds__(kBlock) k_dedup_compact(ScratchView sv, u64* __restrict__ uk,
-                                                          u32* __restrict__ up,
-                                                          unsigned long long* __restrict__ n_uniq) {
-  __shared__ unsigned int wave_tot[kBlock / kWave];
-  __shared__ unsigned long long block_base;
-  const u64 base = (u64)blockIdx.x * kCompactChunk + threadIdx.x;
-  unsigned int hit = 0, cnt = 0;
+// 16 consecutive stamps as four dwordx4 loads (cap is a power of two >= 16,
+// so a 16-slot group is either fully inside the table or fully outside).
+__device__ __forceinline__ unsigned int compact_hits(const ScratchView& sv, u64 base,
+                                                     unsigned int& cnt) {
+  unsigned int hit = 0;
+  cnt = 0;
+  if (base >= sv.cap) return 0;
+  const uint4* p = reinterpret_cast<const uint4*>(sv.stamps + base);
+  uint4 q[kCompactItems / 4];
 #pragma unroll
-  for (int j = 0; j < kCompactItems; ++j) {
-    u64 s = base + (u64)j * kBlock;
-    bool h = s < sv.cap && sv.stamps[s] == sv.epoch;
-    hit |= (unsigned int)h << j;
-    cnt += h;
+  for (int j = 0; j < kCompactItems / 4; ++j) q[j] = p[j];
+#pragma unroll
+  for (int j = 0; j < kCompactItems / 4; ++j) {
+    unsigned int h = (unsigned int)(q[j].x == sv.epoch) | ((unsigned int)(q[j].y == sv.epoch) << 1) |
+                     ((unsigned int)(q[j].z == sv.epoch) << 2) |
+                     ((unsigned int)(q[j].w == sv.epoch) << 3);
+    hit |= h << (4 * j);
   }
-  // block exclusive scan of per-lane counts
+  cnt = __popc(hit);
+  return hit;
+}
+
+// Block-wide exclusive scan of one value per lane; returns the exclusive
+// prefix and writes the block total to *total.
+template <int BLOCK>
+__device__ __forceinline__ unsigned int block_exclusive_scan(unsigned int v, unsigned int* total) {
+  __shared__ unsigned int wsum[BLOCK / kWave];
   const int lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
-  unsigned int incl = cnt;
+  unsigned int incl = v;
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
-    unsigned int v = __shfl_up(incl, o);
-    if (lane >= o) incl += v;
+    unsigned int t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
   }
-  if (lane == kWave - 1) wave_tot[w] = incl;
+  if (lane == kWave - 1) wsum[w] = incl;
   __syncthreads();
-  unsigned int wave_off = 0, total = 0;
-  for (int i = 0; i < kBlock / kWave; ++i) {
-    if (i < w) wave_off += wave_tot[i];
-    total += wave_tot[i];
+  unsigned int off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < BLOCK / kWave; ++i) {
+    off += (i < w) ? wsum[i] : 0u;
+    tot += wsum[i];
   }
-  if (threadIdx.x == 0) block_base = total ? atomicAdd(n_uniq, (unsigned long long)total) : 0ull;
   __syncthreads();
-  unsigned long long dst = block_base + wave_off + (incl - cnt);
+  *total = tot;
+  return off + incl - v;
+}
+
+// lane t owns the 16 consecutive slots [base + 16t, base + 16t + 16): the
+// stamp loads are dwordx4-able and the output stays in slot order
+__global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
+                                                          unsigned int* __restrict__ counts) {
+  const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
+  unsigned int cnt;
+  compact_hits(sv, base, cnt);
+  unsigned int tot;
+  block_exclusive_scan<kBlock>(cnt, &tot);
+  if (threadIdx.x == 0) counts[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kScanBlock) k_compact_scan(unsigned int* __restrict__ counts,
+                                                             int nb,
+                                                             unsigned long long* __restrict__ n_out) {
+  unsigned long long carry = 0;
+  for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
+    int i = c0 + (int)threadIdx.x;
+    unsigned int v = i < nb ? counts[i] : 0u;
+    unsigned int tot;
+    unsigned int ex = block_exclusive_scan<kScanBlock>(v, &tot);
+    if (i < nb) counts[i] = (unsigned int)(carry + ex);  // exclusive offsets (< 2^32 slots)
+    carry += tot;
+  }
+  if (threadIdx.x == 0) *n_out = carry;
+}
+
+__global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
+                                                          const unsigned int* __restrict__ offs,
+                                                          u64* __restrict__ uk,
+                                                          u32* __restrict__ up) {
+  const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
+  unsigned int cnt;
+  unsigned int hit = compact_hits(sv, base, cnt);
+  unsigned int tot;
+  unsigned int ex = block_exclusive_scan<kBlock>(cnt, &tot);
+  unsigned long long dst = (unsigned long long)offs[blockIdx.x] + ex;
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j) {
     if (!(hit & (1u << j))) continue;
-    u64 s = base + (u64)j * kBlock;
+    u64 s = base + (u64)j;
     uk[dst] = sv.keys[s];
     up[dst] = (u32)s;
     ++dst;
@@ -163,9 +215,13 @@ void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipSt
   int g1 = (int)((nnz + kDedupChunk - 1) / kDedupChunk);
   hipLaunchKernelGGL(k_dedup_insert, dim3(g1), dim3(kBlock), 0, st, keys, nnz, s, o.pos,
                      o.overflow);
+  if (!o.block_counts) throw std::runtime_error("dedup: block_counts workspace missing");
   int g2 = (int)((s.cap + kCompactChunk - 1) / kCompactChunk);
-  hipLaunchKernelGGL(k_dedup_compact, dim3(g2), dim3(kBlock), 0, st, s, o.uniq_keys, o.uniq_pos,
+  hipLaunchKernelGGL(k_compact_count, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts);
+  hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanBlock), 0, st, o.block_counts, g2,
                      reinterpret_cast<unsigned long long*>(o.n_uniq));
+  hipLaunchKernelGGL(k_compact_write, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts,
+                     o.uniq_keys, o.uniq_pos);
   XF_HIP_CHECK(hipGetLastError());
 }
 
@@ -239,7 +295,13 @@ __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, b
 }
 
 // LR-FTRL fast path: 16-byte slots {key, n, z}; one dwordx4 load yields the
-// key and the optimizer state together.
+// key and the optimizer state together.  Each lane owns kPullItems keys spaced
+// one block apart and issues all first-probe loads before resolving any (the
+// table is tens of GB: every probe is an HBM miss, so memory-level parallelism
+// is what matters).
+constexpr int kPullItems = 4;
+constexpr int kPullChunk = kBlock * kPullItems;
+
 __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp,
                                                       const u64* __restrict__ keys,
                                                       const int64_t* n_dev, int64_t n_host,
@@ -247,42 +309,58 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
                                                       u32* __restrict__ out_slot,
                                                       float* __restrict__ out_vals,
                                                       const u32* __restrict__ out_map) {
-  int64_t n = dev_count(n_dev, n_host, n_max);
+  const int64_t n = dev_count(n_dev, n_host, n_max);
   const u64 mask = t.cap - 1;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   uint4* slots = reinterpret_cast<uint4*>(t.words);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    u64 key = sanitize_key(keys[i]);
-    u64 s = fmix64(key) & mask;
-    bool claimed = false;
+  const int64_t base = (int64_t)blockIdx.x * kPullChunk + threadIdx.x;
+  u64 key[kPullItems], s[kPullItems];
+  uint4 v[kPullItems];
+#pragma unroll
+  for (int j = 0; j < kPullItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    key[j] = i < n ? sanitize_key(keys[i]) : 0ull;
+    s[j] = fmix64(key[j]) & mask;
+  }
+#pragma unroll
+  for (int j = 0; j < kPullItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    if (i < n) v[j] = slots[s[j]];
+  }
+  unsigned int claims = 0;
+#pragma unroll
+  for (int j = 0; j < kPullItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    if (i >= n) continue;
     u32 slot = kNoSlot;
     float w = 0.0f;
+    u64 sj = s[j];
+    uint4 vj = v[j];
     for (u64 c = 0; c < t.cap; ++c) {
-      uint4 v = slots[s];
-      u64 cur = (u64)v.x | ((u64)v.y << 32);
-      if (cur == key) {
-        slot = (u32)s;
-        w = ftrl_weight(__uint_as_float(v.w), __uint_as_float(v.z), fp);
+      u64 cur = (u64)vj.x | ((u64)vj.y << 32);
+      if (cur == key[j]) {
+        slot = (u32)sj;
+        w = ftrl_weight(__uint_as_float(vj.w), __uint_as_float(vj.z), fp);
         break;
       }
       if (cur == kEmptyKey) {
         if (!insert) break;
-        u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[s]),
-                             (unsigned long long)kEmptyKey, (unsigned long long)key);
-        if (prev == kEmptyKey) { claimed = true; slot = (u32)s; break; }  // fresh state: w = 0
-        if (prev == key) {
-          slot = (u32)s;
-          // claimed by another lane this launch: state is still zero -> w = 0
+        u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[sj]),
+                             (unsigned long long)kEmptyKey, (unsigned long long)key[j]);
+        // fresh slot, or claimed by another lane this launch: state is zero -> w = 0
+        if (prev == kEmptyKey || prev == key[j]) {
+          claims += prev == kEmptyKey;
+          slot = (u32)sj;
           break;
         }
       }
-      s = (s + 1) & mask;
+      sj = (sj + 1) & mask;
+      vj = slots[sj];
     }
     if (insert && slot == kNoSlot) *t.overflow = 1u;
-    wave_append(t.size, claimed);
     if (out_slot) out_slot[i] = slot;
     if (out_vals) out_vals[out_map ? out_map[i] : i] = w;
   }
+  block_count_add<kBlock>(t.size, claims);
 }
 
 __global__ void __launch_bounds__(kBlock) k_pull_generic(PullArgs a) {
@@ -290,11 +368,12 @@ __global__ void __launch_bounds__(kBlock) k_pull_generic(PullArgs a) {
   const TableView& t = a.table;
   const TableLayout& L = t.L;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned int claims = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     u64 key = sanitize_key(a.keys[i]);
     bool claimed = false;
     u32 slot = probe(t, key, a.insert, claimed);
-    wave_append(t.size, claimed);
+    claims += claimed;
     if (a.out_slot) a.out_slot[i] = slot;
     if (a.out_vals) {
       float* dst = a.out_vals + (size_t)(a.out_map ? a.out_map[i] : i) * a.pstride;
@@ -306,6 +385,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_generic(PullArgs a) {
       }
     }
   }
+  block_count_add<kBlock>(t.size, claims);
 }
 
 void launch_table_pull(const PullArgs& a, hipStream_t st) {
@@ -313,7 +393,9 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
   const TableLayout& L = a.table.L;
   int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
   if (L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag) {
-    hipLaunchKernelGGL(k_pull_lr16, dim3(grid), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
+    int64_t nm = a.n_dev ? a.n_max : a.n_host;
+    int g = (int)((nm + kPullChunk - 1) / kPullChunk);
+    hipLaunchKernelGGL(k_pull_lr16, dim3(g > 0 ? g : 1), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map);
   } else {
     hipLaunchKernelGGL(k_pull_generic, dim3(grid), dim3(kBlock), 0, st, a);
@@ -629,14 +711,16 @@ __global__ void __launch_bounds__(kBlock) k_table_import(TableView t, const u64*
                                                          int64_t n) {
   const int W = t.L.stride - 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned int claims = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     bool claimed = false;
     u32 slot = probe(t, sanitize_key(keys[i]), true, claimed);
-    wave_append(t.size, claimed);
+    claims += claimed;
     if (slot == kNoSlot) continue;
     u32* sp = t.words + (u64)slot * t.L.stride;
     for (int w = 0; w < W; ++w) sp[2 + w] = words[i * W + w];
   }
+  block_count_add<kBlock>(t.size, claims);
 }
 
 void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,

@@ -52,6 +52,7 @@ struct DedupOut {
   u32* uniq_pos = nullptr;     // [nnz_max]
   int64_t* n_uniq = nullptr;   // device counter
   u32* overflow = nullptr;
+  u32* block_counts = nullptr; // [cap/4096 + 1] compaction workspace (HIP backend)
 };
 
 struct FwdArgs {

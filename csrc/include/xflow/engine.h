@@ -120,6 +120,7 @@ class Engine {
   u32* uniq_pos_ = nullptr;     // [max_nnz]
   u32* uniq_slot_ = nullptr;    // [max_nnz]
   int64_t* n_uniq_ = nullptr;   // [1]
+  u32* block_counts_ = nullptr; // dedup compaction workspace
   u32* overflow_ = nullptr;     // [2]: scratch, table
   float* wpull_ = nullptr;      // [scratch_cap * pstride]
   float* grad_ = nullptr;       // [scratch_cap * max_slices * pstride]

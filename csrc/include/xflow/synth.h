@@ -13,6 +13,14 @@ namespace xflow {
 
 constexpr int kSynthMaxFields = 64;
 
+XF_HD u64 mulhi64(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (u64)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
 XF_HD double synth_unit(u64 h) {  // (0,1)
   return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
 }
@@ -27,21 +35,36 @@ XF_HD u64 synth_row_seed(u64 seed, u64 step, int64_t r) {
                 ((u64)r * 0xd1b54a32d192ed03ull));
 }
 
-XF_HD u64 synth_key(u64 rowseed, int f, u64 vocab, double s, u64 hash_space) {
+// Per-field constants of the truncated power law, computed once per batch.
+struct SynthField {
+  u64 vocab;
+  double A;      // (V+1)^(1-s) - 1
+  double inv_e;  // 1/(1-s)
+  double logv1;  // ln(V+1), for s == 1
+  int unit_s;
+};
+
+XF_HD SynthField synth_field(u64 vocab, double s) {
+  SynthField F;
+  F.vocab = vocab ? vocab : 1;
+  double V = (double)F.vocab;
+  F.unit_s = fabs(s - 1.0) < 1e-9;
+  F.logv1 = log(V + 1.0);
+  double e = 1.0 - s;
+  F.A = F.unit_s ? 0.0 : pow(V + 1.0, e) - 1.0;
+  F.inv_e = F.unit_s ? 0.0 : 1.0 / e;
+  return F;
+}
+
+XF_HD u64 synth_key(u64 rowseed, int f, const SynthField& F, u64 hash_space) {
   u64 h = fmix64(rowseed + (u64)(f + 1) * 0x94d049bb133111ebull);
   double u = synth_unit(h);
-  double V = (double)vocab;
-  double x;
-  if (fabs(s - 1.0) < 1e-9) {
-    x = exp(u * log(V + 1.0));
-  } else {
-    double e = 1.0 - s;
-    x = pow((pow(V + 1.0, e) - 1.0) * u + 1.0, 1.0 / e);
-  }
+  double x = F.unit_s ? exp(u * F.logv1) : pow(F.A * u + 1.0, F.inv_e);
   u64 rank = (u64)x;
   if (rank < 1) rank = 1;
-  if (rank > vocab) rank = vocab;
-  return fmix64(((u64)(f + 1) << 40) ^ (rank - 1) ^ 0x3c6ef372fe94f82bull) % hash_space;
+  if (rank > F.vocab) rank = F.vocab;
+  // hash into [0, hash_space) by multiply-high (no 64-bit division)
+  return mulhi64(fmix64(((u64)(f + 1) << 40) ^ (rank - 1) ^ 0x3c6ef372fe94f82bull), hash_space);
 }
 
 XF_HD float synth_label(u64 rowseed, float logit) {
