@@ -122,18 +122,31 @@ struct ColumnAgg {
   __device__ __forceinline__ void add(int t, int h, int c, float g) {
     atomicAdd(&acc[t][h * PS + c], g);
   }
-  // one global atomic per (distinct key, component); resets the table
+  // one global atomic per (distinct key, non-zero component); resets the
+  // table.  Consecutive lanes take consecutive components of a key's gradient
+  // row, so a wave's atomics land on a few contiguous PS*4-byte segments
+  // instead of 64 scattered rows.
   __device__ __forceinline__ void flush(int t, float* __restrict__ grad) {
-    for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
-      u32 d = tag[t][i];
-      if (d == kColEmpty) continue;
-#pragma unroll
-      for (int c = 0; c < PS; ++c) {
-        float v = acc[t][i * PS + c];
-        if (v != 0.0f) atomicAdd(&grad[(size_t)d * PS + c], v);
-        acc[t][i * PS + c] = 0.0f;
+    if constexpr (PS == 1) {
+      for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
+        u32 d = tag[t][i];
+        if (d == kColEmpty) continue;
+        float v = acc[t][i];
+        if (v != 0.0f) atomicAdd(&grad[d], v);
+        acc[t][i] = 0.0f;
+        tag[t][i] = kColEmpty;
       }
-      tag[t][i] = kColEmpty;
+    } else {
+      for (int e = threadIdx.x; e < kSlots * PS; e += blockDim.x) {
+        const int i = e / PS, c = e - i * PS;
+        u32 d = tag[t][i];
+        if (d == kColEmpty) continue;
+        float v = acc[t][e];
+        if (v != 0.0f) atomicAdd(&grad[(size_t)d * PS + c], v);
+        acc[t][e] = 0.0f;
+      }
+      __syncthreads();  // every lane has read the tags before they are reset
+      for (int i = threadIdx.x; i < kSlots; i += blockDim.x) tag[t][i] = kColEmpty;
     }
   }
 };
@@ -209,30 +222,56 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
 // ---------------------------------------------------------------------------
 // FM: pulled row = [w, v_0 .. v_{D-1}, pad] (pstride floats)
 // ---------------------------------------------------------------------------
-template <int D, bool kGrad>
-__global__ void __launch_bounds__(kBlock) k_fm(FwdArgs a) {
+constexpr int fm_ps(int D) { return ((1 + D) + 3) & ~3; }
+constexpr int fm_block(int D) { return fm_ps(D) <= 12 ? 256 : (fm_ps(D) <= 20 ? 128 : 64); }
+
+// FM: one lane per row; the pulled row [w, v_0..v_{D-1}, pad] is read as
+// PS/4 dwordx4 loads.  Backward: the P = 1+D gradient components of every
+// occurrence are summed per (key, slice) exactly in the per-column LDS tables
+// (vector accumulators), then flushed with one global atomic per non-zero
+// component -- hot keys cost one atomic per workgroup instead of one per row.
+template <int D, bool kGrad, bool kAgg>
+__global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
+  constexpr int PS = fm_ps(D);
+  constexpr int BLOCK = fm_block(D);
+  constexpr int LOG2 = ilog2c(2 * BLOCK);
+  __shared__ u32 s_tag[kAgg ? 2 : 1][kAgg ? (1 << LOG2) : 1];
+  __shared__ float s_acc[kAgg ? 2 : 1][kAgg ? (1 << LOG2) * PS : 1];
+  __shared__ int s_maxlen;
   const BatchView& b = a.batch;
-  const int ps = a.model.pstride();
   const bool standard = a.model.fm_math == kFmStandard;
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const u32* __restrict__ pos = a.pos;
+  const float4* __restrict__ wp4 = reinterpret_cast<const float4*>(a.wpull);
+  int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool active = r < b.rows;
+  RowRange rr{0, 0};
   StatAcc st;
-  if (r < b.rows) {
-    RowRange rr = row_range(b, r);
-    float wx = 0.0f, vp = 0.0f;
-    float vs[D];
+  float loss = 0.0f, vsum = 0.0f;
+  float vs[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+  for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+  if (active) {
+    rr = row_range(b, r);
+    float wx = 0.0f, vp = 0.0f;
     for (int64_t o = rr.beg; o < rr.end; ++o) {
-      const float* w = a.wpull + (size_t)a.pos[o] * ps;
+      float w[PS];
+      const float4* src = wp4 + (size_t)pos[o] * (PS / 4);
+#pragma unroll
+      for (int q = 0; q < PS / 4; ++q) {
+        float4 v4 = src[q];
+        w[4 * q] = v4.x;
+        w[4 * q + 1] = v4.y;
+        w[4 * q + 2] = v4.z;
+        w[4 * q + 3] = v4.w;
+      }
       wx += w[0];
 #pragma unroll
       for (int k = 0; k < D; ++k) {
-        float v = w[1 + k];
-        vs[k] += v;
-        vp += v * v;
+        vs[k] += w[1 + k];
+        vp += w[1 + k] * w[1 + k];
       }
     }
-    float vsum = 0.0f, y;
+    float y;
     if (standard) {
       float sq = 0.0f;
 #pragma unroll
@@ -245,25 +284,62 @@ __global__ void __launch_bounds__(kBlock) k_fm(FwdArgs a) {
     }
     float p = sigmoid_ref(y);
     float lab = b.labels[r];
-    float loss = p - lab;
+    loss = p - lab;
     if (a.pctr) a.pctr[r] = p;
     st.add(p, lab);
-    if (kGrad) {
-      const int s = slice_of(b, r, a.S);
-      const float gw = standard ? loss : loss * (float)D;
-      for (int64_t o = rr.beg; o < rr.end; ++o) {
-        const float* w = a.wpull + (size_t)a.pos[o] * ps;
-        float* g = a.grad + ((size_t)a.pos[o] * a.S + s) * ps;
-        atomicAdd(&g[0], gw);
+  }
+  if (kGrad) {
+    const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+    const u32 S = (u32)a.S;
+    const float gw = standard ? loss : loss * (float)D;
+    auto contrib = [&](u32 p, float* c) {
+      const float4* src = wp4 + (size_t)p * (PS / 4);
+      float w[PS];
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          float ref = standard ? vs[k] : vsum;
-          atomicAdd(&g[1 + k], loss * (ref - w[1 + k]));
+      for (int q = 0; q < PS / 4; ++q) {
+        float4 v4 = src[q];
+        w[4 * q] = v4.x;
+        w[4 * q + 1] = v4.y;
+        w[4 * q + 2] = v4.z;
+        w[4 * q + 3] = v4.w;
+      }
+      c[0] = gw;
+#pragma unroll
+      for (int k = 0; k < D; ++k) c[1 + k] = loss * ((standard ? vs[k] : vsum) - w[1 + k]);
+    };
+    if constexpr (!kAgg) {
+      for (int64_t q = rr.beg; q < rr.end; ++q) {
+        float c[1 + D];
+        contrib(pos[q], c);
+        float* g = a.grad + ((size_t)pos[q] * S + s) * PS;
+#pragma unroll
+        for (int k = 0; k < 1 + D; ++k) atomicAdd(&g[k], c[k]);
+      }
+    } else {
+      ColumnAgg<PS, LOG2> agg{s_tag, s_acc};
+      if (threadIdx.x == 0) s_maxlen = 0;
+      agg.init();
+      __syncthreads();
+      const int len = (int)(rr.end - rr.beg);
+      if (len > 0) atomicMax(&s_maxlen, len);
+      __syncthreads();
+      const int maxlen = s_maxlen;
+      for (int j = 0; j < maxlen; ++j) {
+        const int t = j & 1;
+        if (j < len) {
+          const u32 p = pos[rr.beg + j];
+          float c[1 + D];
+          contrib(p, c);
+          const int h = agg.insert(t, p * S + s);
+#pragma unroll
+          for (int k = 0; k < 1 + D; ++k) agg.add(t, h, k, c[k]);
         }
+        __syncthreads();
+        agg.flush(t, a.grad);
       }
     }
   }
-  flush_stats<kBlock>(st, a.stats);
+  flush_stats<BLOCK>(st, a.stats);
 }
 
 // ---------------------------------------------------------------------------
@@ -329,10 +405,17 @@ __global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
 }
 
 template <bool kGrad>
-static void dispatch_fm(const FwdArgs& a, int grid, hipStream_t st) {
+static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
+  const bool agg = kGrad && a.agg_ok;
   switch (a.model.v_dim) {
-#define XF_FM_CASE(DD) \
-  case DD: hipLaunchKernelGGL((k_fm<DD, kGrad>), dim3(grid), dim3(kBlock), 0, st, a); break;
+#define XF_FM_CASE(DD)                                                                   \
+  case DD: {                                                                             \
+    constexpr int B = fm_block(DD);                                                      \
+    int g = (int)((a.batch.rows + B - 1) / B);                                           \
+    if (agg) hipLaunchKernelGGL((k_fm<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);    \
+    else hipLaunchKernelGGL((k_fm<DD, kGrad, false>), dim3(g), dim3(B), 0, st, a);       \
+    break;                                                                               \
+  }
     XF_FM_CASE(1) XF_FM_CASE(2) XF_FM_CASE(4) XF_FM_CASE(8) XF_FM_CASE(10) XF_FM_CASE(16)
     XF_FM_CASE(32)
 #undef XF_FM_CASE
@@ -373,8 +456,8 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
       break;
     }
     case kFM:
-      if (grad) dispatch_fm<true>(a, grid, st);
-      else dispatch_fm<false>(a, grid, st);
+      if (grad) dispatch_fm<true>(a, st);
+      else dispatch_fm<false>(a, st);
       break;
     case kMVM:
       if (!a.batch.fgid) throw std::runtime_error("MVM needs field ids (fgid)");

@@ -4,17 +4,20 @@
 // (/root/reference/src/optimizer/ftrl.h:38-152, server.h:20-35) and the
 // worker-side sort/unique key preparation (lr_worker.cc:146-166):
 //
-//   dedup        per-step open-addressing scratch table: each occurrence finds
-//                or claims its key's slot; claimers append (key, slot) to the
-//                unique list with one atomic per wave.  No sort at all.
+//   dedup        persistent, epoch-stamped open-addressing scratch table: each
+//                occurrence finds (or CAS-claims, for keys new to the table)
+//                its key's slot and stamps it; the unique list is compacted
+//                from the stamps without global atomics.  No sort at all.
 //   table_pull   probe/insert of unique keys into the persistent table and
 //                evaluation of the reference pull value (FTRL weight closed form
 //                from (n,z), lazy N(0,1)*1e-2 latent init).
-//   table_apply  per-coordinate FTRL-Proximal / SGD push, one lane per key,
+//   table_apply  per-coordinate FTRL-Proximal / SGD push (one lane per key for
+//                LR, one lane group per key for multi-parameter models),
 //                contributions applied in (slice) order -> deterministic.
 //
-// All kernels are memory-latency bound (random 16-64 B accesses); they are
-// written as grid-stride loops over <= 2048 workgroups of 4 waves and read
+// All kernels are memory-latency bound (random 16-64 B accesses): they keep
+// several independent probes in flight per lane, count bookkeeping with one
+// atomic per workgroup (single-address atomics serialise), and read
 // device-side element counts so a whole step runs without host syncs.
 #include "kernels.h"
 #include "hip_util.h"
@@ -388,6 +391,62 @@ __global__ void __launch_bounds__(kBlock) k_pull_generic(PullArgs a) {
   block_count_add<kBlock>(t.size, claims);
 }
 
+// Multi-parameter layouts (FM / MVM / SGD): phase 1 probes one key per lane
+// (kPullItems keys in flight) and records the slot; phase 2 evaluates the
+// pull values with a group of G lanes per key (G = pow2 >= pstride), so the
+// slot's state words and the output row are read/written contiguously.
+__global__ void __launch_bounds__(kBlock) k_pull_probe(TableView t, const u64* __restrict__ keys,
+                                                       const int64_t* n_dev, int64_t n_host,
+                                                       int64_t n_max, bool insert,
+                                                       u32* __restrict__ out_slot) {
+  const int64_t n = dev_count(n_dev, n_host, n_max);
+  const int64_t base = (int64_t)blockIdx.x * kPullChunk + threadIdx.x;
+  unsigned int claims = 0;
+#pragma unroll
+  for (int j = 0; j < kPullItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    if (i >= n) continue;
+    bool claimed = false;
+    out_slot[i] = probe(t, sanitize_key(keys[i]), insert, claimed);
+    claims += claimed;
+  }
+  block_count_add<kBlock>(t.size, claims);
+}
+
+template <int G>
+__global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
+  const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const TableLayout& L = a.table.L;
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
+  const int p = threadIdx.x % G;
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; i < n; i += stride) {
+    const u32 slot = a.out_slot[i];
+    float* dst = a.out_vals + (size_t)(a.out_map ? a.out_map[i] : i) * a.pstride;
+    if (p >= a.pstride) continue;
+    float v = 0.0f;
+    if (p < L.P) {
+      if (slot == kNoSlot) {
+        v = absent_weight(sanitize_key(a.keys[i]), p, L, a.opt);
+      } else {
+        const u32* sp = a.table.words + (u64)slot * L.stride;
+        v = slot_weight(sp, *reinterpret_cast<const u64*>(sp), p, L, a.opt);
+      }
+    }
+    dst[p] = v;
+  }
+}
+
+template <int G>
+static void launch_pull_values(const PullArgs& a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(k_pull_values<G>, dim3(grid), dim3(kBlock), 0, st, a);
+}
+
+static int group_for(int width) {
+  int g = 1;
+  while (g < width) g <<= 1;
+  return g;
+}
+
 void launch_table_pull(const PullArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   const TableLayout& L = a.table.L;
@@ -397,6 +456,23 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
     int g = (int)((nm + kPullChunk - 1) / kPullChunk);
     hipLaunchKernelGGL(k_pull_lr16, dim3(g > 0 ? g : 1), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map);
+  } else if (a.out_slot && a.pstride >= 2 && a.pstride <= 64) {
+    int64_t nm = a.n_dev ? a.n_max : a.n_host;
+    int g1 = (int)((nm + kPullChunk - 1) / kPullChunk);
+    hipLaunchKernelGGL(k_pull_probe, dim3(g1 > 0 ? g1 : 1), dim3(kBlock), 0, st, a.table, a.keys,
+                       a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot);
+    if (a.out_vals) {
+      const int G = group_for(a.pstride);
+      const int g2 = grid_for(nm * G);
+      switch (G) {
+        case 2: launch_pull_values<2>(a, g2, st); break;
+        case 4: launch_pull_values<4>(a, g2, st); break;
+        case 8: launch_pull_values<8>(a, g2, st); break;
+        case 16: launch_pull_values<16>(a, g2, st); break;
+        case 32: launch_pull_values<32>(a, g2, st); break;
+        default: launch_pull_values<64>(a, g2, st); break;
+      }
+    }
   } else {
     hipLaunchKernelGGL(k_pull_generic, dim3(grid), dim3(kBlock), 0, st, a);
   }
@@ -471,6 +547,77 @@ __global__ void __launch_bounds__(kBlock) k_apply_generic(ApplyArgs a) {
   }
 }
 
+// Multi-parameter apply: a group of G lanes per key (G = pow2 >= pstride),
+// lane p owns parameter p's optimizer state, so a wave touches a few
+// contiguous slots instead of 64 scattered ones.  Every lane reads the
+// "pushed" flag before lane 0 of the group writes it (same wave, program
+// order); latent params use their lazy init value until the key's first push.
+template <int G>
+__global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
+  static_assert(G <= kWave, "a key's lanes must share a wave");
+  const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const TableLayout& L = a.table.L;
+  const int S = a.S, ps = a.pstride;
+  const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
+  const int p = threadIdx.x % G;
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; i < n; i += stride) {
+    const u32 slot = a.slots[i];
+    const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+    float* g = a.grads + (size_t)row * S * ps;
+    const u32 m = a.masks ? a.masks[row] : all;
+    if (slot != kNoSlot && p < L.P) {
+      u32* sp = a.table.words + (u64)slot * L.stride;
+      const u64 key = *reinterpret_cast<const u64*>(sp);
+      bool pushed = !L.has_flag || sp[L.flag_word] != 0u;
+      float* st = reinterpret_cast<float*>(sp + 2);
+      const bool latent = p >= L.p_w;
+      const bool ftrl = L.opt == kFTRL;
+      float n0 = 0.0f, z0 = 0.0f, w0 = 0.0f;
+      if (ftrl) {
+        float2 nz = *reinterpret_cast<float2*>(st + 2 * p);
+        n0 = nz.x;
+        z0 = nz.y;
+      } else {
+        w0 = st[p];
+      }
+      auto weight = [&]() -> float {
+        if (latent && !pushed)
+          return ftrl ? normal_init(key, (u32)(p - L.p_w), a.opt.seed) * a.opt.v_init_scale
+                      : a.opt.sgd.v_init;
+        return ftrl ? ftrl_weight(z0, n0, a.opt.ftrl) : w0;
+      };
+      auto push = [&](float gv) {
+        float w = weight();
+        if (ftrl) ftrl_push(n0, z0, w, gv, a.opt.ftrl);
+        else w0 = w - a.opt.sgd.lr * gv;
+        pushed = true;
+      };
+      if (a.sum_slices) {
+        float acc = 0.0f;
+        for (int s = 0; s < S; ++s)
+          if (m & (1u << s)) acc += norm_grad(g[s * ps + p], a.slice_rows, s);
+        if (m) push(acc);
+      } else {
+        for (int s = 0; s < S; ++s)
+          if (m & (1u << s)) push(norm_grad(g[s * ps + p], a.slice_rows, s));
+      }
+      if (ftrl) *reinterpret_cast<float2*>(st + 2 * p) = make_float2(n0, z0);
+      else st[p] = w0;
+      if (L.has_flag && p == 0 && m) sp[L.flag_word] = 1u;
+    }
+    if (a.zero_after && p < ps) {
+      for (int s = 0; s < S; ++s) g[s * ps + p] = 0.0f;
+      if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
+    }
+  }
+}
+
+template <int G>
+static void launch_apply_group(const ApplyArgs& a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(k_apply_group<G>, dim3(grid), dim3(kBlock), 0, st, a);
+}
+
 void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   const TableLayout& L = a.table.L;
@@ -478,6 +625,18 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag && a.S == 1 && !a.masks &&
       a.pstride == 1) {
     hipLaunchKernelGGL(k_apply_lr16, dim3(grid), dim3(kBlock), 0, st, a);
+  } else if (a.pstride >= 2 && a.pstride <= 64 && !a.reset_pos) {
+    int64_t nm = a.n_dev ? a.n_max : a.n_host;
+    const int G = group_for(a.pstride);
+    const int g2 = grid_for(nm * G);
+    switch (G) {
+      case 2: launch_apply_group<2>(a, g2, st); break;
+      case 4: launch_apply_group<4>(a, g2, st); break;
+      case 8: launch_apply_group<8>(a, g2, st); break;
+      case 16: launch_apply_group<16>(a, g2, st); break;
+      case 32: launch_apply_group<32>(a, g2, st); break;
+      default: launch_apply_group<64>(a, g2, st); break;
+    }
   } else {
     hipLaunchKernelGGL(k_apply_generic, dim3(grid), dim3(kBlock), 0, st, a);
   }
