@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--features", type=int, default=1_000_000_000)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (smoke only)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="force the multi-rank (all-to-all) step even at 1 GPU (overhead probe)")
     return ap.parse_args()
 
 
@@ -64,7 +66,10 @@ def main():
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1:
+    if world > 1 or a.sharded:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
                                 device_id=device if use_gpu else None)
 
@@ -81,7 +86,7 @@ def main():
                     device=device)
     gen = SyntheticCriteo(engine, a.batch, synth, rank=rank)
 
-    if world > 1:
+    if world > 1 or a.sharded:
         from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
         sharded = ShardedEngine(engine)
@@ -147,7 +152,7 @@ def main():
             "table_keys": int(table_keys),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
