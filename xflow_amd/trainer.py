@@ -36,6 +36,7 @@ from xflow_amd.engine import Batch, Engine
 from xflow_amd.metrics import MetricsLogger, reference_auc
 from xflow_amd.parallel import dist as xdist
 from xflow_amd.testing.hashing import owner_of
+from xflow_amd.utils.faults import injector_from_env, watchdog_from_env
 from xflow_amd.utils.trace import PhaseTimer
 
 
@@ -71,6 +72,8 @@ class Trainer:
             self.sharded = ShardedEngine(self.engine)
         self.metrics = MetricsLogger(cfg.metrics_file, self.rank)
         self.timer = PhaseTimer(self.device, enabled=bool(os.environ.get("XFLOW_TRACE")))
+        self.watchdog = watchdog_from_env(f"xflow-rank{self.rank}")
+        self.faults = injector_from_env(self.rank)
         self.epoch = 0
         self.steps = 0
         self.samples = 0
@@ -152,6 +155,11 @@ class Trainer:
                 if not xdist.all_any(blk is not None, self.device):
                     break
                 for b in self._slices_of(blk):
+                    if self.watchdog is not None:
+                        self.watchdog.beat()
+                    if not self.faults.before_step(self.steps):
+                        self.steps += 1
+                        continue
                     with self.timer.phase("step"):
                         self._step(b)
                     self.steps += 1
@@ -256,6 +264,8 @@ class Trainer:
         return meta
 
     def close(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()
         xdist.finalize()
 
 

@@ -1,0 +1,84 @@
+"""Failure detection and fault injection.
+
+* ``Watchdog``: a daemon thread per rank.  The trainer calls ``beat()`` every
+  step; if no beat arrives for ``timeout`` seconds the watchdog logs the stall
+  with every thread's stack and (policy "abort") terminates the process with
+  exit code 75, so a launcher sees a dead rank instead of a silent hang.  RCCL
+  / gloo collectives additionally carry the process-group timeout
+  (XFLOW_DIST_TIMEOUT) and async error handling (parallel/dist.py).
+* Fault injection for tests, from the environment (never set in production):
+    XFLOW_FAULT=kill:<rank>:<step>      rank exits abruptly before that step
+    XFLOW_FAULT=hang:<rank>:<step>      rank stops making progress (sleeps)
+    XFLOW_FAULT=drop_a2a:<rank>:<step>  rank skips the step's exchanges
+"""
+from __future__ import annotations
+
+import faulthandler
+import os
+import sys
+import threading
+import time
+from typing import Optional
+
+
+class Watchdog:
+    def __init__(self, timeout: float, policy: str = "abort", name: str = "xflow"):
+        self.timeout = float(timeout)
+        self.policy = policy
+        self.name = name
+        self._last = time.monotonic()
+        self._stop = threading.Event()
+        self.fired = False
+        self._th = threading.Thread(target=self._run, name=f"{name}-watchdog", daemon=True)
+
+    def start(self) -> "Watchdog":
+        self._th.start()
+        return self
+
+    def beat(self) -> None:
+        self._last = time.monotonic()
+
+    def stop(self) -> None:
+        self._stop.set()
+
+    def _run(self) -> None:
+        while not self._stop.wait(min(1.0, self.timeout / 4)):
+            if time.monotonic() - self._last > self.timeout:
+                self.fired = True
+                sys.stderr.write(f"[{self.name}] watchdog: no progress for {self.timeout:.0f}s\n")
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+                if self.policy == "abort":
+                    os._exit(75)
+                return
+
+
+def watchdog_from_env(name: str = "xflow") -> Optional[Watchdog]:
+    t = os.environ.get("XFLOW_WATCHDOG_SECS")
+    return Watchdog(float(t), os.environ.get("XFLOW_WATCHDOG_POLICY", "abort"), name).start() \
+        if t else None
+
+
+class FaultInjector:
+    def __init__(self, spec: Optional[str], rank: int):
+        self.kind = None
+        if spec:
+            kind, r, step = spec.split(":")
+            if int(r) == rank:
+                self.kind, self.step = kind, int(step)
+
+    def before_step(self, step: int) -> bool:
+        """Returns False when this rank must skip the step's exchanges."""
+        if self.kind is None or step != self.step:
+            return True
+        if self.kind == "kill":
+            sys.stderr.write(f"[fault] rank exits at step {step}\n")
+            sys.stderr.flush()
+            os._exit(17)
+        if self.kind == "hang":
+            time.sleep(3600)
+        return self.kind != "drop_a2a"
+
+
+def injector_from_env(rank: int) -> FaultInjector:
+    return FaultInjector(os.environ.get("XFLOW_FAULT"), rank)
