@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="CPU backend (smoke only)")
     ap.add_argument("--sharded", action="store_true",
                     help="force the multi-rank (all-to-all) step even at 1 GPU (overhead probe)")
+    ap.add_argument("--async", dest="async_p2p", action="store_true",
+                    help="config 4: staleness-1 pipelined steps, pushes over RCCL point-to-point")
+    ap.add_argument("--lambda1", type=float, default=5e-5,
+                    help="FTRL L1 (ftrl.h:19); config 4 reports the non-zero weight count")
     return ap.parse_args()
 
 
@@ -66,7 +70,7 @@ def main():
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1 or a.sharded:
+    if world > 1 or a.sharded or a.async_p2p:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
@@ -80,16 +84,18 @@ def main():
     synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed)
     nnz = a.batch * synth.fields
     model = ModelConfig(kind=a.model, v_dim=a.v_dim)
-    engine = Engine(model, OptimConfig(kind=a.optimizer),
+    engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
                                  max_slices=1),
                     device=device)
     gen = SyntheticCriteo(engine, a.batch, synth, rank=rank)
 
-    if world > 1 or a.sharded:
+    sharded = None
+    if world > 1 or a.sharded or a.async_p2p:
+        from xflow_amd.parallel.async_p2p import AsyncShardedEngine
         from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
-        sharded = ShardedEngine(engine)
+        sharded = AsyncShardedEngine(engine) if a.async_p2p else ShardedEngine(engine)
         batch = gen.alloc_batch()
 
         def step():
@@ -112,19 +118,22 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    if hasattr(sharded, "flush"):
+        sharded.flush()  # the last pushes are part of the timed work
     sync()
     elapsed = time.perf_counter() - t0
     st = engine.read_stats(reset=True)
     tbl = engine.table_size()
-    red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl)], dtype=torch.float64,
-                       device=device)
+    nnzw = engine.nonzero_weights() if a.async_p2p else 0
+    red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw)],
+                       dtype=torch.float64, device=device)
     if world > 1:
         mx = red[:1].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         dist.all_reduce(red, op=dist.ReduceOp.SUM)
         elapsed = float(mx.item())
     vals = red.tolist()
-    ln_loss, rows, table_keys = vals[1], vals[2], vals[3]
+    ln_loss, rows, table_keys, nonzero = vals[1], vals[2], vals[3], vals[4]
     samples = a.batch * a.steps * world
     if rank == 0:
         out = {
@@ -151,6 +160,10 @@ def main():
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
         }
+        if a.async_p2p:
+            out["config"]["parallelism"] += "+async-p2p(staleness=1)"
+            out["config"]["lambda1"] = a.lambda1
+            out["nonzero_weights"] = int(nonzero)
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -395,6 +395,16 @@ class CpuBackend final : public Backend {
       std::memcpy(t.words + (u64)slot * t.L.stride + 2, words + i * W, sizeof(u32) * W);
     }
   }
+  int64_t table_nonzero(const TableView& t, const OptSpec& o) override {
+    int64_t n = 0;
+    for (u64 s = 0; s < t.cap; ++s) {
+      const u32* sp = t.words + s * (u64)t.L.stride;
+      const u64 key = *reinterpret_cast<const u64*>(sp);
+      if (key == kEmptyKey) continue;
+      for (int p = 0; p < t.L.P; ++p) n += slot_weight(sp, key, p, t.L, o) != 0.0f;
+    }
+    return n;
+  }
 };
 
 }  // namespace

@@ -95,7 +95,8 @@ Engine::~Engine() {
                   scratch_.claims, block_counts_, pos_, uniq_keys_,
                   uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
-                  srv_slots_, host_keys_dev_, host_vals_dev_};
+                  srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
+                  host_slots_dev_};
   for (void* p : ptrs) be.free(p);
 }
 
@@ -227,11 +228,12 @@ void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& g
     be_->synchronize();
     be_->free(host_keys_dev_);
     be_->free(host_vals_dev_);
+    be_->free(host_slots_dev_);
     host_cap_ = n;
     host_keys_dev_ = balloc<u64>(*be_, n);
     host_vals_dev_ = balloc<float>(*be_, n * P);
+    host_slots_dev_ = balloc<u32>(*be_, n);
   }
-  ensure_server_capacity(n);
   be_->copy_h2d(host_keys_dev_, keys.data(), sizeof(u64) * n);
   be_->copy_h2d(host_vals_dev_, grads.data(), sizeof(float) * n * P);
   PullArgs pa;
@@ -241,7 +243,7 @@ void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& g
   pa.n_host = n;
   pa.n_max = n;
   pa.insert = true;
-  pa.out_slot = srv_slots_;
+  pa.out_slot = host_slots_dev_;
   be_->table_pull(pa);
   // Pushes of one call are applied one key at a time in order; duplicate keys
   // inside one call are applied sequentially by separate launches.
@@ -253,7 +255,7 @@ void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& g
   aa.pstride = P;
   aa.P = P;
   for (int64_t i = 0; i < n; ++i) {
-    aa.slots = srv_slots_ + i;
+    aa.slots = host_slots_dev_ + i;
     aa.grads = host_vals_dev_ + i * P;
     aa.n_host = 1;
     aa.n_max = 1;
@@ -271,11 +273,12 @@ std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
     be_->synchronize();
     be_->free(host_keys_dev_);
     be_->free(host_vals_dev_);
+    be_->free(host_slots_dev_);
     host_cap_ = n;
     host_keys_dev_ = balloc<u64>(*be_, n);
     host_vals_dev_ = balloc<float>(*be_, n * P);
+    host_slots_dev_ = balloc<u32>(*be_, n);
   }
-  ensure_server_capacity(n);
   be_->copy_h2d(host_keys_dev_, keys.data(), sizeof(u64) * n);
   PullArgs pa;
   pa.table = table_;
@@ -284,7 +287,7 @@ std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
   pa.n_host = n;
   pa.n_max = n;
   pa.insert = false;
-  pa.out_slot = srv_slots_;
+  pa.out_slot = host_slots_dev_;
   pa.out_vals = host_vals_dev_;
   pa.pstride = P;
   be_->table_pull(pa);
@@ -313,12 +316,13 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
   (void)S;  // slice masks are built in w_forward_backward with the step's global S
 }
 
-void Engine::ensure_server_capacity(int64_t n) {
-  if (n <= srv_cap_) return;
+void Engine::ensure_server_capacity(int64_t n, int buf) {
+  if (buf < 0 || buf > 1) throw std::invalid_argument("server buffer must be 0 or 1");
+  if (n <= srv_cap_[buf]) return;
   be_->synchronize();
-  be_->free(srv_slots_);
-  srv_cap_ = n + n / 4 + 1024;
-  srv_slots_ = balloc<u32>(*be_, srv_cap_);
+  be_->free(srv_slots_[buf]);
+  srv_cap_[buf] = n + n / 4 + 1024;
+  srv_slots_[buf] = balloc<u32>(*be_, srv_cap_[buf]);
 }
 
 void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr) {
@@ -335,9 +339,9 @@ void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, 
   be_->forward_backward(fa);
 }
 
-void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert) {
-  ensure_server_capacity(n);
-  srv_n_ = n;
+void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert, int buf) {
+  ensure_server_capacity(n, buf);
+  srv_n_[buf] = n;
   if (n == 0) return;
   PullArgs pa;
   pa.table = table_;
@@ -346,7 +350,7 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
   pa.n_host = n;
   pa.n_max = n;
   pa.insert = insert;
-  pa.out_slot = srv_slots_;
+  pa.out_slot = srv_slots_[buf];
   pa.out_vals = out_vals;
   pa.pstride = pstride();
   be_->table_pull(pa);
@@ -392,18 +396,19 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
 }
 
 void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
-                     const std::vector<int64_t>& src_offsets, int S) {
+                     const std::vector<int64_t>& src_offsets, int S, int buf) {
+  if (buf < 0 || buf > 1) throw std::invalid_argument("server buffer must be 0 or 1");
   const int ps = pstride();
   for (size_t src = 0; src + 1 < src_offsets.size(); ++src) {
     int64_t off = src_offsets[src];
     int64_t cnt = src_offsets[src + 1] - off;
     if (cnt <= 0) continue;
-    if (src_offsets[src + 1] > srv_n_) throw std::invalid_argument("s_apply: offsets beyond pull");
+    if (src_offsets[src + 1] > srv_n_[buf]) throw std::invalid_argument("s_apply: offsets beyond pull");
     ApplyArgs aa;
     aa.table = table_;
     aa.opt = cfg_.opt;
     aa.keys = recv_keys + off;
-    aa.slots = srv_slots_ + off;
+    aa.slots = srv_slots_[buf] + off;
     aa.n_host = cnt;
     aa.n_max = cnt;
     aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * ps;

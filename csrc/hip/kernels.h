@@ -30,6 +30,8 @@ void launch_table_export(const TableView& t, u64* keys_out, u32* words_out, int6
                          unsigned long long* counter, hipStream_t st);
 void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,
                          hipStream_t st);
+void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long long* counter,
+                          hipStream_t st);
 
 // kernels_model.hip
 void launch_forward_backward(const FwdArgs& a, hipStream_t st);

@@ -891,3 +891,34 @@ void launch_table_import(const TableView& t, const u64* keys, const u32* words, 
 
 }  // namespace hip
 }  // namespace xflow
+
+namespace xflow {
+namespace hip {
+
+// L1 sparsity report: count (key, param) weights that are exactly non-zero.
+// A full-table sweep (dwordx4-friendly for 16-B LR slots), one atomic per
+// workgroup.
+__global__ void __launch_bounds__(kBlock) k_table_nonzero(TableView t, OptSpec o,
+                                                          unsigned long long* counter) {
+  const TableLayout& L = t.L;
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  unsigned int cnt = 0;
+  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap; s += stride) {
+    const u32* sp = t.words + s * (u64)L.stride;
+    const u64 key = *reinterpret_cast<const u64*>(sp);
+    if (key == kEmptyKey) continue;
+    for (int p = 0; p < L.P; ++p) cnt += slot_weight(sp, key, p, L, o) != 0.0f;
+  }
+  block_count_add<kBlock>(counter, cnt);
+}
+
+void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long long* counter,
+                          hipStream_t st) {
+  XF_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(k_table_nonzero, dim3(grid_for((int64_t)t.cap)), dim3(kBlock), 0, st, t, o,
+                     counter);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace hip
+}  // namespace xflow

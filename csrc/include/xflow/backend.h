@@ -194,6 +194,9 @@ class Backend {
   // count occupied slots / dump table rows (checkpointing); returns rows written
   virtual int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
                                int64_t max_rows) = 0;
+  // Number of (key, param) weights that are exactly non-zero (L1 sparsity
+  // report; lambda1 > 0 makes FTRL weights exactly 0 when |z| <= lambda1).
+  virtual int64_t table_nonzero(const TableView& t, const OptSpec& o) = 0;
   virtual void table_import(const TableView& t, const u64* keys, const u32* words,
                             int64_t n) = 0;
 };

@@ -63,7 +63,8 @@ class Engine {
   void w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out);
   // server: probe/insert n received keys, write pulled rows (pstride floats)
   // into out_vals (backend memory), remember slots for s_apply.
-  void s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert = true);
+  // buf selects one of two server slot buffers (pipelined steps alternate).
+  void s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert = true, int buf = 0);
   // worker: forward only from pulled rows (sharded evaluation); pctr may be null.
   void w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr);
   // worker: place pulled rows (in send order) into the pos-indexed buffer,
@@ -74,7 +75,7 @@ class Engine {
   // server: apply received gradients source by source (deterministic order).
   // src_offsets has world+1 entries delimiting each source's rows.
   void s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
-               const std::vector<int64_t>& src_offsets, int S);
+               const std::vector<int64_t>& src_offsets, int S, int buf = 0);
   // worker: release the per-step dedup scratch.
   void w_finish();
 
@@ -86,6 +87,8 @@ class Engine {
   uint64_t table_capacity() const { return table_.cap; }
   size_t table_bytes() const { return table_bytes_; }
   bool overflowed();
+  // exactly non-zero (key, param) weights of this table shard (L1 sparsity)
+  int64_t nonzero_weights() { return be_->table_nonzero(table_, cfg_.opt); }
   int pstride() const { return cfg_.model.pstride(); }
   int slices_of(const BatchView& b) const;
 
@@ -104,7 +107,7 @@ class Engine {
   BatchView stage_host_batch(const BatchView& host);
 
  private:
-  void ensure_server_capacity(int64_t n);
+  void ensure_server_capacity(int64_t n, int buf = 0);
   const int32_t* slice_rows_dev(const BatchView& b, int S);
   void dedup_(const BatchView& b);
 
@@ -140,12 +143,15 @@ class Engine {
   float* st_labels_ = nullptr;
 
   // server buffers
-  u32* srv_slots_ = nullptr;
-  int64_t srv_cap_ = 0;
-  int64_t srv_n_ = 0;
+  // two server slot buffers: a pipelined (staleness-1) step applies the
+  // previous step's pushes after pulling into the other buffer
+  u32* srv_slots_[2] = {nullptr, nullptr};
+  int64_t srv_cap_[2] = {0, 0};
+  int64_t srv_n_[2] = {0, 0};
 
   u64* host_keys_dev_ = nullptr;   // push_host / pull_host staging
   float* host_vals_dev_ = nullptr;
+  u32* host_slots_dev_ = nullptr;
   int64_t host_cap_ = 0;
 };
 

@@ -172,10 +172,11 @@ PYBIND11_MODULE(_xflow_native, m) {
            },
            py::call_guard<py::gil_scoped_release>())
       .def("s_pull",
-           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert) {
-             e.s_pull(P<const u64>(keys), n, P<float>(out), insert);
+           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert, int buf) {
+             e.s_pull(P<const u64>(keys), n, P<float>(out), insert, buf);
            },
            py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("insert") = true,
+           py::arg("buf") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("w_forward",
            [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t pctr) {
@@ -193,10 +194,12 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("s_apply",
            [](Engine& e, uintptr_t keys, uintptr_t grads, uintptr_t masks,
-              std::vector<int64_t> offsets, int S) {
-             e.s_apply(P<const u64>(keys), P<const float>(grads), P<const u32>(masks), offsets, S);
+              std::vector<int64_t> offsets, int S, int buf) {
+             e.s_apply(P<const u64>(keys), P<const float>(grads), P<const u32>(masks), offsets, S,
+                       buf);
            },
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("keys"), py::arg("grads"), py::arg("masks"), py::arg("offsets"), py::arg("S"),
+           py::arg("buf") = 0, py::call_guard<py::gil_scoped_release>())
       .def("w_finish", &Engine::w_finish)
       .def("read_stats",
            [](Engine& e, bool reset, int which) { return stats_dict(e.read_stats(reset, which)); },
@@ -204,6 +207,7 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def("n_unique", &Engine::n_unique)
       .def("table_size", &Engine::table_size)
       .def("overflowed", &Engine::overflowed)
+      .def("nonzero_weights", &Engine::nonzero_weights)
       .def("export_table",
            [](Engine& e) {
              std::vector<u64> k;

@@ -142,3 +142,66 @@ def test_trainer_two_workers_bundled_data(tmp_path):
     run_world(_trainer_worker, 2, DATA, str(tmp_path))
     pred = np.loadtxt(tmp_path / "pred_0_0.txt")
     assert pred.shape == (200, 3)
+
+
+def _async_worker(rank, world, out_dir):
+    from xflow_amd.parallel.async_p2p import AsyncShardedEngine
+
+    eng = _make_engine("lr", 1)
+    sh = AsyncShardedEngine(eng)
+    for step in range(STEPS + 1):
+        k, rp, fg, lab = _batches(rank, step)
+        sh.train_step(to_batch(k, rp, fg, lab, torch.device("cpu")), S=1)
+    sh.flush()
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"akeys{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"avals{rank}.npy"), eng.pull(keys))
+    assert sh.p2p_ops > 0
+
+
+def test_async_p2p_staleness_one_matches_simulation(tmp_path):
+    """AsyncShardedEngine == the reference step with pulls that miss exactly
+    the previous step's pushes (staleness 1), pushes in (source) order."""
+    from xflow_amd.testing import torch_ref
+    from xflow_amd.testing.hashing import normal_init
+
+    world = 2
+    run_world(_async_worker, world, str(tmp_path))
+    ref = torch_ref.RefTable(1, 1, "ftrl", init_fn=lambda k, d: normal_init(k, d) * 1e-2)
+    pending = None
+    for step in range(STEPS + 1):
+        parts = [_batches(r, step) for r in range(world)]
+        keys = np.concatenate([p[0] for p in parts])
+        lab = np.concatenate([p[3] for p in parts])
+        rp = np.concatenate([parts[0][1]] + [p[1][1:] + len(parts[0][0]) for p in parts[1:]])
+        _, cur = torch_ref.compute_step(ref, "lr", keys, lab, rp.astype(np.int32), ROWS)
+        if pending is not None:
+            torch_ref.apply_step(ref, pending)
+        pending = cur
+    torch_ref.apply_step(ref, pending)
+    k = np.concatenate([np.load(tmp_path / f"akeys{r}.npy") for r in range(world)])
+    v = np.concatenate([np.load(tmp_path / f"avals{r}.npy") for r in range(world)])
+    want = ref.weights(k, insert=False).numpy()
+    np.testing.assert_allclose(v, want, rtol=1e-4, atol=1e-6)
+
+
+def _async_trainer_worker(rank, world, data_dir, pred_dir):
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
+                      test_prefix=os.path.join(data_dir, "small_test"), epochs=2, threads=4,
+                      pred_dir=pred_dir, async_p2p=True,
+                      optim=OptimConfig(lambda1=0.01),
+                      engine=EngineConfig(table_log2_cap=14))
+    t = Trainer(cfg, device=torch.device("cpu"))
+    res = t.train()
+    if rank == 0:
+        assert res["n"] == 200 and 0.0 < res["auc"] < 1.0
+
+
+def test_trainer_async_p2p_two_workers(tmp_path):
+    from conftest import DATA
+
+    run_world(_async_trainer_worker, 2, DATA, str(tmp_path))
+    assert np.loadtxt(tmp_path / "pred_0_0.txt").shape == (200, 3)

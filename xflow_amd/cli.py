@@ -46,6 +46,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--sum-slices", action="store_true",
                     help="one FTRL push of the summed slice gradients per step")
     ap.add_argument("--no-init-push", action="store_true")
+    ap.add_argument("--async", dest="async_p2p", action="store_true",
+                    help="multi-rank: staleness-1 pipelined steps, pushes over RCCL P2P")
     ap.add_argument("--log2-cap", type=int, default=22, help="table slots per rank = 2^N")
     ap.add_argument("--train-block-bytes", type=int, default=2 << 20)
     ap.add_argument("--test-block-bytes", type=int, default=0)
@@ -66,7 +68,7 @@ def config_from_args(a) -> TrainConfig:
         test_block_bytes=a.test_block_bytes, serial_slices=a.serial_slices,
         keep_remainder=a.keep_remainder, mvm_predict_compat=a.mvm_predict_compat,
         init_push=not a.no_init_push, pred_dir=a.pred_dir, checkpoint_dir=a.save,
-        metrics_file=a.metrics,
+        metrics_file=a.metrics, async_p2p=a.async_p2p,
         model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math),
         optim=OptimConfig(kind=a.optimizer, alpha=a.alpha, beta=a.beta, lambda1=a.lambda1,
                           lambda2=a.lambda2, lr=a.lr),

@@ -101,6 +101,7 @@ class TrainConfig:
     pred_dir: str = "."
     checkpoint_dir: str = ""
     metrics_file: str = ""
+    async_p2p: bool = False      # staleness-1 pipelined steps, pushes over RCCL point-to-point
     model: ModelConfig = field(default_factory=ModelConfig)
     optim: OptimConfig = field(default_factory=OptimConfig)
     engine: EngineConfig = field(default_factory=EngineConfig)

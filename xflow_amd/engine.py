@@ -180,9 +180,9 @@ class Engine:
         self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr())
 
     def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor,
-               insert: bool = True) -> None:
+               insert: bool = True, buf: int = 0) -> None:
         self._sync_stream()
-        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr(), insert)
+        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr(), insert, int(buf))
 
     def w_forward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
                   pctr: torch.Tensor | None) -> None:
@@ -199,11 +199,11 @@ class Engine:
                                    masks_out.data_ptr() if masks_out is not None else 0, int(S))
 
     def s_apply(self, recv_keys: torch.Tensor, recv_grads: torch.Tensor,
-                recv_masks: torch.Tensor | None, offsets, S: int) -> None:
+                recv_masks: torch.Tensor | None, offsets, S: int, buf: int = 0) -> None:
         self._sync_stream()
         self._e.s_apply(recv_keys.data_ptr(), recv_grads.data_ptr(),
                         recv_masks.data_ptr() if recv_masks is not None else 0,
-                        [int(o) for o in offsets], int(S))
+                        [int(o) for o in offsets], int(S), int(buf))
 
     def w_finish(self) -> None:
         self._sync_stream()
@@ -228,6 +228,11 @@ class Engine:
     def overflowed(self) -> bool:
         self._sync_stream()
         return bool(self._e.overflowed())
+
+    def nonzero_weights(self) -> int:
+        """Exactly non-zero (key, param) weights in this shard (L1 sparsity)."""
+        self._sync_stream()
+        return int(self._e.nonzero_weights())
 
     def export_table(self):
         self._sync_stream()

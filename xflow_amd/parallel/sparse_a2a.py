@@ -91,12 +91,12 @@ class ShardedEngine:
         self._a2a(recv_keys, self.send_keys[:n_send], recv_splits, send_splits)
         return send_splits, recv_splits, recv_keys
 
-    def _pull(self, recv_keys, send_splits, recv_splits, insert: bool) -> torch.Tensor:
+    def _pull(self, recv_keys, send_splits, recv_splits, insert: bool, buf: int = 0) -> torch.Tensor:
         e = self.engine
         ps = e.pstride
         n_send, n_recv = sum(send_splits), sum(recv_splits)
         vals = self._vals_out.get(n_recv * ps).view(n_recv, ps)
-        e.s_pull(recv_keys, n_recv, vals, insert=insert)
+        e.s_pull(recv_keys, n_recv, vals, insert=insert, buf=buf)
         pulled = self._pulled.get(n_send * ps).view(n_send, ps)
         self._a2a(pulled, vals, send_splits, recv_splits)
         return pulled

@@ -142,6 +142,30 @@ def train_step(table: RefTable, kind: str, keys: np.ndarray, labels: np.ndarray,
                row_ptr: np.ndarray, slice_rows: int, fgid: np.ndarray | None = None,
                fm_math: str = "reference", mvm_math: str = "compat", sum_slices: bool = False):
     """One engine-semantics step; returns pctr [rows]."""
+    p, pending = compute_step(table, kind, keys, labels, row_ptr, slice_rows, fgid, fm_math,
+                              mvm_math)
+    apply_step(table, pending, sum_slices)
+    return p
+
+
+def apply_step(table: RefTable, pending, sum_slices: bool = False) -> None:
+    """Push a compute_step's per-(key, slice) gradients in slice order."""
+    uniq, g, touched = pending
+    nS = g.shape[1]
+    if sum_slices:
+        gg = torch.where(touched.unsqueeze(2), g, torch.zeros_like(g)).sum(1)
+        table.push(uniq, gg)
+        return
+    for s in range(nS):
+        sel = touched[:, s].numpy()
+        if sel.any():
+            table.push(uniq[sel], g[torch.from_numpy(sel), s])
+
+
+def compute_step(table: RefTable, kind: str, keys: np.ndarray, labels: np.ndarray,
+                 row_ptr: np.ndarray, slice_rows: int, fgid: np.ndarray | None = None,
+                 fm_math: str = "reference", mvm_math: str = "compat"):
+    """Pull + forward + backward of one step; returns (pctr, pending pushes)."""
     rows = len(labels)
     counts = np.diff(row_ptr)
     row_of = torch.from_numpy(np.repeat(np.arange(rows), counts)).long()
@@ -181,12 +205,4 @@ def train_step(table: RefTable, kind: str, keys: np.ndarray, labels: np.ndarray,
     srows = [min(slice_rows, rows - s * slice_rows) if slice_rows > 0 else rows for s in range(nS)]
     norm = torch.tensor(srows, dtype=torch.float64)
     g = (gsum.double() / norm.view(1, nS, 1)).float()
-    if sum_slices:
-        gg = torch.where(touched.unsqueeze(2), g, torch.zeros_like(g)).sum(1)
-        table.push(uniq, gg)
-    else:
-        for s in range(nS):
-            sel = touched[:, s].numpy()
-            if sel.any():
-                table.push(uniq[sel], g[torch.from_numpy(sel), s])
-    return p
+    return p, (uniq, g, touched)

@@ -66,7 +66,11 @@ class Trainer:
         ecfg.max_slices = max(ecfg.max_slices, self.S)
         self.engine = Engine(cfg.model, cfg.optim, ecfg, device=self.device)
         self.sharded = None
-        if self.world > 1:
+        if self.world > 1 and cfg.async_p2p:
+            from xflow_amd.parallel.async_p2p import AsyncShardedEngine
+
+            self.sharded = AsyncShardedEngine(self.engine)
+        elif self.world > 1:
             from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
             self.sharded = ShardedEngine(self.engine)
@@ -166,16 +170,22 @@ class Trainer:
                     ep_samples += b.rows
                     if log_every and self.steps % log_every == 0:
                         self._log_progress(ep_samples, t0)
+            if hasattr(self.sharded, "flush"):
+                self.sharded.flush()
             self.samples += ep_samples
             self.epoch += 1
             if self.epoch % 30 == 0:
                 _say("epoch : %d" % (self.epoch - 1))
             st = self.engine.read_stats(reset=True)
             tot = xdist.all_sum([st["ln_loss"], st["rows"], ep_samples], self.device)
-            self.metrics.log(event="epoch", epoch=self.epoch, steps=self.steps,
-                             train_logloss=tot[0] / max(tot[1], 1.0),
-                             samples_per_s=tot[2] / max(time.perf_counter() - t0, 1e-9),
-                             table_keys=self.engine.table_size())
+            rec = dict(event="epoch", epoch=self.epoch, steps=self.steps,
+                       train_logloss=tot[0] / max(tot[1], 1.0),
+                       samples_per_s=tot[2] / max(time.perf_counter() - t0, 1e-9),
+                       table_keys=self.engine.table_size())
+            if self.cfg.optim.lambda1 > 0 and os.environ.get("XFLOW_REPORT_NNZ"):
+                rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
+                                                           self.device)[0])
+            self.metrics.log(**rec)
             if cfg.checkpoint_dir and os.environ.get("XFLOW_CKPT_EVERY_EPOCH"):
                 self.save(cfg.checkpoint_dir)
         if self.device.type == "cuda":
@@ -252,6 +262,8 @@ class Trainer:
 
     # ------------------------------------------------------------ checkpoint
     def save(self, ckpt_dir: str) -> None:
+        if hasattr(self.sharded, "flush"):
+            self.sharded.flush()
         checkpoint.save(self.engine, ckpt_dir, self.rank, self.world,
                         meta={"epoch": self.epoch, "steps": self.steps})
         xdist.barrier()
