@@ -25,14 +25,6 @@ inline int64_t count_of(const int64_t* n_dev, int64_t n_host, int64_t n_max) {
   return n < n_max ? n : n_max;
 }
 
-struct RowRange {
-  int64_t beg, end;
-};
-
-inline RowRange row_range(const BatchView& b, int64_t r) {
-  if (b.row_ptr) return {b.row_ptr[r], b.row_ptr[r + 1]};
-  return {r * b.nnz_per_row, (r + 1) * b.nnz_per_row};
-}
 
 inline int slice_of(const BatchView& b, int64_t r, int S) {
   if (b.slice_rows <= 0) return 0;
@@ -210,16 +202,16 @@ class CpuBackend final : public Backend {
     std::vector<float> vs(D > 0 ? D : 1), M(D > 0 ? D : 1);
     std::vector<float> S;
     for (int64_t r = 0; r < b.rows; ++r) {
-      RowRange rr = row_range(b, r);
+      const RowSpan rs = row_span(b, r);
       float y = 0.0f;
       float vsum = 0.0f;
       int maxf = 0, G = 0;
       if (m.kind == kLR) {
-        for (int64_t o = rr.beg; o < rr.end; ++o) y += a.wpull[a.pos[o]];
+        for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step) y += a.wpull[a.pos[o]];
       } else if (m.kind == kFM) {
         float wx = 0.0f, vp = 0.0f;
         for (int k = 0; k < D; ++k) vs[k] = 0.0f;
-        for (int64_t o = rr.beg; o < rr.end; ++o) {
+        for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step) {
           const float* w = a.wpull + (size_t)a.pos[o] * ps;
           wx += w[0];
           for (int k = 0; k < D; ++k) {
@@ -238,11 +230,11 @@ class CpuBackend final : public Backend {
         }
       } else {  // MVM
         if (!b.fgid) throw std::runtime_error("MVM needs field ids (fgid)");
-        for (int64_t o = rr.beg; o < rr.end; ++o) maxf = std::max(maxf, (int)b.fgid[o]);
+        for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step) maxf = std::max(maxf, (int)b.fgid[o]);
         G = (m.mvm_math == kMvmCompat) ? maxf : maxf + 1;
         S.assign((size_t)(maxf + 1) * D, 0.0f);
         for (int k = 0; k < D; ++k) {
-          for (int64_t o = rr.beg; o < rr.end; ++o)
+          for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step)
             S[(size_t)b.fgid[o] * D + k] += a.wpull[(size_t)a.pos[o] * ps + k];
           float prod = 1.0f;
           for (int g = 0; g < G; ++g) prod *= S[(size_t)g * D + k];
@@ -257,7 +249,7 @@ class CpuBackend final : public Backend {
       add_stats(a.stats, p, lab);
       if (!a.grad) continue;
       const int s = slice_of(b, r, a.S);
-      for (int64_t o = rr.beg; o < rr.end; ++o) {
+      for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step) {
         float* g = a.grad + ((size_t)a.pos[o] * a.S + s) * ps;
         if (m.kind == kLR) {
           g[0] += loss;
@@ -282,9 +274,9 @@ class CpuBackend final : public Backend {
   void slice_masks(const BatchView& b, const u32* pos, u32* tmask) override {
     int S = b.slice_rows > 0 ? (int)((b.rows + b.slice_rows - 1) / b.slice_rows) : 1;
     for (int64_t r = 0; r < b.rows; ++r) {
-      RowRange rr = row_range(b, r);
+      const RowSpan rs = row_span(b, r);
       u32 bit = 1u << slice_of(b, r, S);
-      for (int64_t o = rr.beg; o < rr.end; ++o) tmask[pos[o]] |= bit;
+      for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step) tmask[pos[o]] |= bit;
     }
   }
 
@@ -361,8 +353,9 @@ class CpuBackend final : public Backend {
       float logit = a.planted_bias;
       for (int f = 0; f < a.fields; ++f) {
         u64 key = synth_key(rs, f, F[f], a.hash_space);
-        a.keys[r * a.fields + f] = key;
-        if (a.fgid) a.fgid[r * a.fields + f] = f;
+        const int64_t o = a.col_stride > 0 ? f * a.col_stride + r : r * a.fields + f;
+        a.keys[o] = key;
+        if (a.fgid) a.fgid[o] = f;
         logit += synth_planted_weight(key, a.planted_scale);
       }
       a.labels[r] = synth_label(rs, logit);

@@ -61,6 +61,12 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // keys, so the load factor stays below 0.5 + 1/factor.
   scratch_.rebuild_at = scratch_.cap / 2;
   scratch_.epoch = 0;
+  if (be.is_gpu()) {
+    // adaptive active capacity (ScratchView::ctl): starts at the allocation
+    scratch_.ctl = balloc<unsigned long long>(be, 4);
+    unsigned long long c0[4] = {scratch_.cap, 0ull, 0ull, 0ull};
+    be.copy_h2d(scratch_.ctl, c0, sizeof(c0));
+  }
   block_counts_ = balloc<u32>(be, scratch_.cap / 4096 + 1);
 
   const int ps = cfg_.model.pstride();
@@ -96,7 +102,7 @@ Engine::~Engine() {
                   uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
-                  host_slots_dev_};
+                  host_slots_dev_, scratch_.ctl};
   for (void* p : ptrs) be.free(p);
 }
 
@@ -126,6 +132,8 @@ const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
 void Engine::dedup_(const BatchView& b) {
   if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
+  if (b.col_stride > 0 && (b.row_ptr || b.col_stride < b.rows || b.nnz != b.rows * b.nnz_per_row))
+    throw std::invalid_argument("field-major batch needs fixed nnz_per_row and col_stride >= rows");
   be_->memset(n_uniq_, 0, sizeof(int64_t));
   if (++scratch_.epoch == 0) scratch_.epoch = 1;  // 0 marks never-stamped slots
   DedupOut o;
@@ -457,6 +465,8 @@ BatchView Engine::synth_batch(const SynthArgs& a0, int64_t slice_rows) {
   SynthArgs a = a0;
   if (a.rows > cfg_.max_rows || a.rows * a.fields > cfg_.max_nnz)
     throw std::invalid_argument("synth batch exceeds engine capacity");
+  if (a.col_stride > 0 && (a.col_stride < a.rows || (!a0.keys && a.col_stride != a.rows)))
+    throw std::invalid_argument("synth: col_stride must be >= rows (== rows for staging)");
   // caller-provided outputs (e.g. torch tensors) or the engine's staging buffers
   a.keys = a0.keys ? a0.keys : st_keys_;
   a.labels = a0.labels ? a0.labels : st_labels_;
@@ -470,6 +480,7 @@ BatchView Engine::synth_batch(const SynthArgs& a0, int64_t slice_rows) {
   b.nnz = a.rows * a.fields;
   b.nnz_per_row = a.fields;
   b.slice_rows = slice_rows;
+  b.col_stride = a.col_stride;
   return b;
 }
 

@@ -51,6 +51,21 @@ __device__ __forceinline__ T wave_append(T* counter, bool pred) {
   return pred ? base + (T)__popcll(below) : (T)-1;
 }
 
+// Workgroup barrier that waits only for this wave's LDS operations.  A
+// __syncthreads() fence also drains vmcnt, i.e. every outstanding no-return
+// global atomic, which turns a column loop of fire-and-forget gradient flushes
+// into one L2 round trip per column.  Use only where no global memory written
+// before the barrier is read by another wave after it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

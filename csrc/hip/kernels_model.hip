@@ -17,15 +17,6 @@
 namespace xflow {
 namespace hip {
 
-struct RowRange {
-  int64_t beg, end;
-};
-
-__device__ __forceinline__ RowRange row_range(const BatchView& b, int64_t r) {
-  if (b.row_ptr) return {b.row_ptr[r], b.row_ptr[r + 1]};
-  return {r * b.nnz_per_row, (r + 1) * b.nnz_per_row};
-}
-
 __device__ __forceinline__ int slice_of(const BatchView& b, int64_t r, int S) {
   if (b.slice_rows <= 0) return 0;
   int64_t s = r / b.slice_rows;
@@ -153,66 +144,118 @@ struct ColumnAgg {
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
 
-// LR: the row gather keeps 4 independent pos->wpull chains in flight per lane;
-// the sum order is the row's feature order (bitwise equal to the CPU backend).
-// BLOCK rows per workgroup: larger workgroups aggregate mid-frequency keys
-// better (Criteo-shaped batch: 4.29 M global atomics at 256 rows, 2.95 M at
-// 1024 rows, for 10.2 M occurrences).
+// Rows of at most kLrRegCols features keep their dedup positions in registers:
+// every pos load of a row is issued before the first use (one memory latency
+// instead of one per 4 features), and the backward column walk reuses them
+// instead of re-reading pos.  Longer rows take the streaming path.
+constexpr int kLrRegCols = 40;
+
+// Backward of one column: exact LDS aggregation, then the LDS-only barrier
+// and the flush of the table (its global atomics stay in flight).
+template <int LOG2>
+__device__ __forceinline__ void lr_column(ColumnAgg<1, LOG2>& agg, int j, bool has, u32 dest,
+                                          float loss, float* __restrict__ grad) {
+  const int t = j & 1;
+  if (has) agg.add(t, agg.insert(t, dest), 0, loss);
+  lds_barrier();
+  agg.flush(t, grad);
+}
+
+// LR: one lane per row, the sum order is the row's feature order (bitwise
+// equal to the CPU backend).  BLOCK rows per workgroup: larger workgroups
+// aggregate mid-frequency keys better (Criteo-shaped batch: 4.29 M global
+// atomics at 256 rows, 2.95 M at 1024 rows, for 10.2 M occurrences).
 template <bool kGrad, bool kAgg, int BLOCK>
 __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   constexpr int LOG2 = ilog2c(2 * BLOCK);
+  constexpr int C = kLrRegCols;
   __shared__ u32 s_tag[kAgg ? 2 : 1][1 << LOG2];
   __shared__ float s_acc[kAgg ? 2 : 1][1 << LOG2];
-  __shared__ int s_maxlen;
+  __shared__ int s_wmax[BLOCK / kWave];
   const BatchView& b = a.batch;
   const u32* __restrict__ pos = a.pos;
   const float* __restrict__ wp = a.wpull;
   int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool active = r < b.rows;
-  RowRange rr{0, 0};
+  RowSpan rs;
+  if (active) rs = row_span(b, r);
+  const int len = rs.len;
+  ColumnAgg<1, LOG2> agg{s_tag, s_acc};
+  if constexpr (kAgg) agg.init();
+  // block-uniform longest row: selects the register path and bounds the
+  // backward column walk
+  int maxlen;
+  if (!b.row_ptr) {
+    maxlen = (int)b.nnz_per_row;
+    if constexpr (kAgg) __syncthreads();
+  } else {
+    int m = wave_max(len);
+    if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
+    __syncthreads();
+    maxlen = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
+  }
   StatAcc st;
   float loss = 0.0f;
-  if (active) {
-    rr = row_range(b, r);
-    float wx = 0.0f;
-    int64_t o = rr.beg;
-    for (; o + 4 <= rr.end; o += 4) {
-      u32 p0 = pos[o], p1 = pos[o + 1], p2 = pos[o + 2], p3 = pos[o + 3];
-      float w0 = wp[p0], w1 = wp[p1], w2 = wp[p2], w3 = wp[p3];
-      wx += w0;
-      wx += w1;
-      wx += w2;
-      wx += w3;
+  const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+  const u32 S = (u32)a.S;
+  if (maxlen <= C) {
+    u32 pv[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) pv[j] = j < len ? pos[rs.at(j)] : 0u;
+    float wv[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) wv[j] = j < len ? wp[pv[j]] : 0.0f;
+    if (active) {
+      float wx = 0.0f;
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        if (j < len) wx += wv[j];
+      float p = sigmoid_ref(wx);
+      float y = b.labels[r];
+      loss = p - y;
+      if (a.pctr) a.pctr[r] = p;
+      st.add(p, y);
     }
-    for (; o < rr.end; ++o) wx += wp[pos[o]];
-    float p = sigmoid_ref(wx);
-    float y = b.labels[r];
-    loss = p - y;
-    if (a.pctr) a.pctr[r] = p;
-    st.add(p, y);
-  }
-  if (kGrad) {
-    const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
-    const u32 S = (u32)a.S;
-    if (!kAgg) {
-      for (int64_t q = rr.beg; q < rr.end; ++q) atomicAdd(&a.grad[pos[q] * S + s], loss);
-    } else {
-      ColumnAgg<1, LOG2> agg{s_tag, s_acc};
-      if (threadIdx.x == 0) s_maxlen = 0;
-      agg.init();
-      __syncthreads();
-      const int len = (int)(rr.end - rr.beg);
-      if (len > 0) atomicMax(&s_maxlen, len);
-      __syncthreads();
-      const int maxlen = s_maxlen;
-      for (int j = 0; j < maxlen; ++j) {
-        const int t = j & 1;
-        if (j < len) {
-          u32 dest = pos[rr.beg + j] * S + s;
-          agg.add(t, agg.insert(t, dest), 0, loss);
-        }
-        __syncthreads();
-        agg.flush(t, a.grad);
+    if constexpr (kGrad) {
+      if constexpr (!kAgg) {
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+          if (j < len) atomicAdd(&a.grad[pv[j] * S + s], loss);
+      } else {
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+          if (j < maxlen) lr_column<LOG2>(agg, j, j < len, pv[j] * S + s, loss, a.grad);
+      }
+    }
+  } else {
+    if (active) {
+      float wx = 0.0f;
+      int j = 0;
+      for (; j + 4 <= len; j += 4) {
+        u32 p0 = pos[rs.at(j)], p1 = pos[rs.at(j + 1)], p2 = pos[rs.at(j + 2)],
+            p3 = pos[rs.at(j + 3)];
+        float w0 = wp[p0], w1 = wp[p1], w2 = wp[p2], w3 = wp[p3];
+        wx += w0;
+        wx += w1;
+        wx += w2;
+        wx += w3;
+      }
+      for (; j < len; ++j) wx += wp[pos[rs.at(j)]];
+      float p = sigmoid_ref(wx);
+      float y = b.labels[r];
+      loss = p - y;
+      if (a.pctr) a.pctr[r] = p;
+      st.add(p, y);
+    }
+    if constexpr (kGrad) {
+      if constexpr (!kAgg) {
+        for (int j = 0; j < len; ++j) atomicAdd(&a.grad[pos[rs.at(j)] * S + s], loss);
+      } else {
+        for (int j = 0; j < maxlen; ++j)
+          lr_column<LOG2>(agg, j, j < len, j < len ? pos[rs.at(j)] * S + s : 0u, loss,
+                          a.grad);
       }
     }
   }
@@ -244,18 +287,18 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
   const float4* __restrict__ wp4 = reinterpret_cast<const float4*>(a.wpull);
   int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool active = r < b.rows;
-  RowRange rr{0, 0};
+  RowSpan rs;
   StatAcc st;
   float loss = 0.0f, vsum = 0.0f;
   float vs[D];
 #pragma unroll
   for (int k = 0; k < D; ++k) vs[k] = 0.0f;
   if (active) {
-    rr = row_range(b, r);
+    rs = row_span(b, r);
     float wx = 0.0f, vp = 0.0f;
-    for (int64_t o = rr.beg; o < rr.end; ++o) {
+    for (int j = 0; j < rs.len; ++j) {
       float w[PS];
-      const float4* src = wp4 + (size_t)pos[o] * (PS / 4);
+      const float4* src = wp4 + (size_t)pos[rs.at(j)] * (PS / 4);
 #pragma unroll
       for (int q = 0; q < PS / 4; ++q) {
         float4 v4 = src[q];
@@ -308,10 +351,11 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
       for (int k = 0; k < D; ++k) c[1 + k] = loss * ((standard ? vs[k] : vsum) - w[1 + k]);
     };
     if constexpr (!kAgg) {
-      for (int64_t q = rr.beg; q < rr.end; ++q) {
+      for (int j = 0; j < rs.len; ++j) {
+        const u32 p = pos[rs.at(j)];
         float c[1 + D];
-        contrib(pos[q], c);
-        float* g = a.grad + ((size_t)pos[q] * S + s) * PS;
+        contrib(p, c);
+        float* g = a.grad + ((size_t)p * S + s) * PS;
 #pragma unroll
         for (int k = 0; k < 1 + D; ++k) atomicAdd(&g[k], c[k]);
       }
@@ -320,14 +364,14 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
       if (threadIdx.x == 0) s_maxlen = 0;
       agg.init();
       __syncthreads();
-      const int len = (int)(rr.end - rr.beg);
+      const int len = rs.len;
       if (len > 0) atomicMax(&s_maxlen, len);
       __syncthreads();
       const int maxlen = s_maxlen;
       for (int j = 0; j < maxlen; ++j) {
         const int t = j & 1;
         if (j < len) {
-          const u32 p = pos[rr.beg + j];
+          const u32 p = pos[rs.at(j)];
           float c[1 + D];
           contrib(p, c);
           const int h = agg.insert(t, p * S + s);
@@ -358,9 +402,9 @@ __global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + t;
   StatAcc st;
   if (r < b.rows) {
-    RowRange rr = row_range(b, r);
+    const RowSpan rs = row_span(b, r);
     int maxf = 0;
-    for (int64_t o = rr.beg; o < rr.end; ++o) maxf = max(maxf, (int)b.fgid[o]);
+    for (int j = 0; j < rs.len; ++j) maxf = max(maxf, (int)b.fgid[rs.at(j)]);
     maxf = min(maxf, kMvmMaxFields);
     const int G = compat ? maxf : maxf + 1;
     float M[D];
@@ -368,7 +412,8 @@ __global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
 #pragma unroll
     for (int k = 0; k < D; ++k) {
       for (int g = 0; g <= maxf; ++g) S[g][t] = 0.0f;
-      for (int64_t o = rr.beg; o < rr.end; ++o) {
+      for (int j = 0; j < rs.len; ++j) {
+        const int64_t o = rs.at(j);
         int f = b.fgid[o];
         if (f <= kMvmMaxFields) S[f][t] += a.wpull[(size_t)a.pos[o] * ps + k];
       }
@@ -387,11 +432,13 @@ __global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
 #pragma unroll
       for (int k = 0; k < D; ++k) {
         for (int g = 0; g <= maxf; ++g) S[g][t] = 0.0f;
-        for (int64_t o = rr.beg; o < rr.end; ++o) {
+        for (int j = 0; j < rs.len; ++j) {
+        const int64_t o = rs.at(j);
           int f = b.fgid[o];
           if (f <= kMvmMaxFields) S[f][t] += a.wpull[(size_t)a.pos[o] * ps + k];
         }
-        for (int64_t o = rr.beg; o < rr.end; ++o) {
+        for (int j = 0; j < rs.len; ++j) {
+        const int64_t o = rs.at(j);
           int f = b.fgid[o];
           float sg = (f <= kMvmMaxFields) ? S[f][t] : 0.0f;
           float gr = (sg == 0.0f) ? 0.0f
@@ -474,9 +521,9 @@ __global__ void k_slice_masks(BatchView b, const u32* __restrict__ pos, u32* __r
                               int S) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= b.rows) return;
-  RowRange rr = row_range(b, r);
+  const RowSpan rs = row_span(b, r);
   u32 bit = 1u << slice_of(b, r, S);
-  for (int64_t o = rr.beg; o < rr.end; ++o) atomicOr(&tmask[pos[o]], bit);
+  for (int j = 0; j < rs.len; ++j) atomicOr(&tmask[pos[rs.at(j)]], bit);
 }
 
 void launch_slice_masks(const BatchView& b, const u32* pos, u32* tmask, hipStream_t st) {

@@ -24,13 +24,23 @@ __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
   const int64_t r0 = (int64_t)blockIdx.x * kSynthRows;
   const int rows = (int)min((int64_t)kSynthRows, a.rows - r0);
   const int n = rows * F;
+  const bool field_major = a.col_stride > 0;
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    const int rl = e / F, f = e - rl * F;
+    // field-major: consecutive lanes take consecutive rows of one field
+    int rl, f;
+    if (field_major) {
+      f = e / rows;
+      rl = e - f * rows;
+    } else {
+      rl = e / F;
+      f = e - rl * F;
+    }
     const int64_t r = r0 + rl;
+    const int64_t o = field_major ? (int64_t)f * a.col_stride + r : r0 * F + e;
     const u64 key = synth_key(synth_row_seed(a.seed, a.step, r), f, c.f[f], a.hash_space);
-    a.keys[r0 * F + e] = key;
-    if (a.fgid) a.fgid[r0 * F + e] = f;
-    pw[e] = synth_planted_weight(key, a.planted_scale);
+    a.keys[o] = key;
+    if (a.fgid) a.fgid[o] = f;
+    pw[rl * F + f] = synth_planted_weight(key, a.planted_scale);
   }
   __syncthreads();
   if ((int)threadIdx.x < rows) {

@@ -35,52 +35,110 @@ constexpr u32 kNoSlot = 0xFFFFFFFFu;
 // hit.  CTR keys are extremely skewed (top-1000 keys ~60% of occurrences); a
 // table cleared every step made each hot key a same-address CAS storm.
 //
-// Step 0 -- device-side rebuild: when `claims` exceeds rebuild_at, every slot
-// is freed (grid-stride fill) before the step; otherwise the launch exits.
+// Step 0 -- device-side rebuild.  With ctl (adaptive capacity) the previous
+// batch's compaction scan decided whether to rebuild and at which capacity
+// (ctl[2]); otherwise the table is rebuilt once `claims` exceeds rebuild_at.
+// A rebuild frees the slots of the new capacity (grid-stride fill).
+__device__ __forceinline__ u64 active_cap(const ScratchView& sv) {
+  return sv.ctl ? (u64)sv.ctl[0] : sv.cap;
+}
+
 __global__ void k_scratch_maybe_clear(u64* __restrict__ skeys, u64 cap,
                                       const unsigned long long* __restrict__ claims,
-                                      u64 rebuild_at) {
-  if (*claims <= rebuild_at) return;
+                                      u64 rebuild_at, const unsigned long long* __restrict__ ctl) {
+  u64 n = cap;
+  if (ctl) {
+    n = ctl[2];
+    if (n == 0) return;
+  } else if (*claims <= rebuild_at) {
+    return;
+  }
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < cap; s += stride)
+  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < n; s += stride)
     skeys[s] = kEmptyKey;
 }
 
-__global__ void k_scratch_claims_reset(unsigned long long* claims, u64 rebuild_at) {
-  if (*claims > rebuild_at) *claims = 0ull;
+__global__ void k_scratch_claims_reset(unsigned long long* claims, u64 rebuild_at,
+                                       unsigned long long* ctl) {
+  if (ctl) {
+    if (ctl[2]) {
+      ctl[0] = ctl[2];
+      ctl[2] = 0ull;
+      *claims = 0ull;
+    }
+  } else if (*claims > rebuild_at) {
+    *claims = 0ull;
+  }
 }
 
-// Step 1 -- insert / stamp.  Each lane owns kDedupItems occurrences spaced one
-// block apart (coalesced key loads) and issues all of their first-probe loads
-// before resolving any, so a wave keeps 8 independent random reads in flight.
-// A hit writes the epoch stamp with a plain (idempotent, no-return) store; only
-// keys new to the table CAS.
+// Step 1 -- insert / stamp, two levels.
+//   (a) workgroup level: the block's kDedupChunk occurrences (~52 Criteo rows)
+//       are deduplicated in an LDS hash table (2x oversized, 64-bit ds CAS);
+//       the first occurrence of each key becomes its leader.
+//   (b) global level: only leaders probe the persistent table -- all of their
+//       first-probe loads in flight before any is resolved -- CAS new keys,
+//       write the epoch stamp and publish the slot in LDS; every occurrence
+//       then reads its slot from LDS.
+// Hot keys (an int-field value can occur in half the rows) otherwise send one
+// read and one stamp store per occurrence to the same L2 channel; with (a)
+// they cost one per workgroup.
 constexpr int kDedupItems = 8;
 constexpr int kDedupChunk = kBlock * kDedupItems;
+constexpr int kDedupLog2 = 12;  // LDS slots = 2 * kDedupChunk
+static_assert((1 << kDedupLog2) == 2 * kDedupChunk, "LDS dedup table sizing");
 
 __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__ keys, int64_t nnz,
                                                          ScratchView sv, u32* __restrict__ pos,
                                                          u32* __restrict__ overflow) {
+  constexpr u32 kL = 1u << kDedupLog2;
+  __shared__ u64 t_key[kL];  // keys during the LDS level, then leaders' slots
   u64* __restrict__ skeys = sv.keys;
-  const u64 cap = sv.cap, mask = cap - 1;
+  const u64 cap = active_cap(sv), mask = cap - 1;
   const int64_t base = (int64_t)blockIdx.x * kDedupChunk + threadIdx.x;
-  u64 k[kDedupItems], s[kDedupItems], cur[kDedupItems];
+  for (u32 i = threadIdx.x; i < kL; i += kBlock) t_key[i] = kEmptyKey;
+  u64 k[kDedupItems], s[kDedupItems];
+  u32 h[kDedupItems];
 #pragma unroll
   for (int j = 0; j < kDedupItems; ++j) {
     int64_t i = base + (int64_t)j * kBlock;
     k[j] = i < nnz ? sanitize_key(keys[i]) : 0ull;
-    s[j] = fmix64(k[j]) & mask;
+    const u64 f = fmix64(k[j]);
+    s[j] = f & mask;
+    h[j] = (u32)(f >> (64 - kDedupLog2));
   }
+  __syncthreads();
+  u32 lead = 0;
 #pragma unroll
   for (int j = 0; j < kDedupItems; ++j) {
-    int64_t i = base + (int64_t)j * kBlock;
-    cur[j] = i < nnz ? skeys[s[j]] : k[j];
+    if (base + (int64_t)j * kBlock >= nnz) continue;
+    u32 x = h[j];
+    while (true) {
+      const u64 c = t_key[x];
+      if (c == k[j]) break;
+      if (c == kEmptyKey) {
+        const u64 prev = atomicCAS((unsigned long long*)&t_key[x], (unsigned long long)kEmptyKey,
+                                   (unsigned long long)k[j]);
+        if (prev == kEmptyKey) {
+          lead |= 1u << j;
+          break;
+        }
+        if (prev == k[j]) break;
+      }
+      x = (x + 1) & (kL - 1);  // <= kDedupChunk keys in kL slots: terminates
+    }
+    h[j] = x;
   }
+  // every LDS lookup is done: the leaders' table entries can now carry slots
+  __syncthreads();
+  // global level, leaders only: all first-probe loads in flight, then each
+  // leader resolves (CAS only for keys new to the table)
+  u64 cur[kDedupItems];
+#pragma unroll
+  for (int j = 0; j < kDedupItems; ++j) cur[j] = (lead >> j) & 1u ? skeys[s[j]] : k[j];
   unsigned int claimed = 0;
 #pragma unroll
   for (int j = 0; j < kDedupItems; ++j) {
-    int64_t i = base + (int64_t)j * kBlock;
-    if (i >= nnz) continue;
+    if (!((lead >> j) & 1u)) continue;
     u64 sj = s[j], c = cur[j];
     u64 n = 0;
     while (c != k[j]) {
@@ -100,8 +158,14 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
       sj = (sj + 1) & mask;
       c = skeys[sj];
     }
-    pos[i] = (u32)sj;
+    t_key[h[j]] = sj;
     sv.stamps[sj] = sv.epoch;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kDedupItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    if (i < nnz) pos[i] = (u32)t_key[h[j]];
   }
   // one no-return atomic per workgroup for the rebuild counter
   block_count_add<kBlock>(sv.claims, claimed);
@@ -122,7 +186,7 @@ __device__ __forceinline__ unsigned int compact_hits(const ScratchView& sv, u64 
                                                      unsigned int& cnt) {
   unsigned int hit = 0;
   cnt = 0;
-  if (base >= sv.cap) return 0;
+  if (base >= active_cap(sv)) return 0;
   const uint4* p = reinterpret_cast<const uint4*>(sv.stamps + base);
   uint4 q[kCompactItems / 4];
 #pragma unroll
@@ -175,9 +239,14 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
   if (threadIdx.x == 0) counts[blockIdx.x] = tot;
 }
 
-__global__ void __launch_bounds__(kScanBlock) k_compact_scan(unsigned int* __restrict__ counts,
-                                                             int nb,
-                                                             unsigned long long* __restrict__ n_out) {
+// Also sizes the scratch for the next batch (ctl): active cap = the power of
+// two >= kScratchHeadroom x the largest batch seen, rebuilt when it should
+// grow, when it is 4x too large, or when the keys claimed since the last
+// rebuild fill half of it.
+__global__ void __launch_bounds__(kScanBlock) k_compact_scan(
+    unsigned int* __restrict__ counts, int nb, unsigned long long* __restrict__ n_out,
+    const unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
+    u64 cap_alloc) {
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
     int i = c0 + (int)threadIdx.x;
@@ -187,7 +256,18 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(unsigned int* __res
     if (i < nb) counts[i] = (unsigned int)(carry + ex);  // exclusive offsets (< 2^32 slots)
     carry += tot;
   }
-  if (threadIdx.x == 0) *n_out = carry;
+  if (threadIdx.x == 0) {
+    *n_out = carry;
+    if (ctl) {
+      const u64 mx = ctl[1] > carry ? ctl[1] : carry;
+      ctl[1] = mx;
+      u64 want = kScratchMinCap;
+      while (want < kScratchHeadroom * mx && want < cap_alloc) want <<= 1;
+      if (want > cap_alloc) want = cap_alloc;
+      const u64 cur = ctl[0];
+      ctl[2] = (*claims > cur / 2 || want > cur || want * 4 <= cur) ? want : 0ull;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
@@ -213,16 +293,18 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
 void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st) {
   if (nnz <= 0) return;
   hipLaunchKernelGGL(k_scratch_maybe_clear, dim3(grid_for((int64_t)s.cap)), dim3(kBlock), 0, st,
-                     s.keys, s.cap, s.claims, s.rebuild_at);
-  hipLaunchKernelGGL(k_scratch_claims_reset, dim3(1), dim3(1), 0, st, s.claims, s.rebuild_at);
+                     s.keys, s.cap, s.claims, s.rebuild_at, s.ctl);
+  hipLaunchKernelGGL(k_scratch_claims_reset, dim3(1), dim3(1), 0, st, s.claims, s.rebuild_at,
+                     s.ctl);
   int g1 = (int)((nnz + kDedupChunk - 1) / kDedupChunk);
   hipLaunchKernelGGL(k_dedup_insert, dim3(g1), dim3(kBlock), 0, st, keys, nnz, s, o.pos,
                      o.overflow);
   if (!o.block_counts) throw std::runtime_error("dedup: block_counts workspace missing");
+  // sized for the allocated capacity; blocks past the active one count zero
   int g2 = (int)((s.cap + kCompactChunk - 1) / kCompactChunk);
   hipLaunchKernelGGL(k_compact_count, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts);
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanBlock), 0, st, o.block_counts, g2,
-                     reinterpret_cast<unsigned long long*>(o.n_uniq));
+                     reinterpret_cast<unsigned long long*>(o.n_uniq), s.claims, s.ctl, s.cap);
   hipLaunchKernelGGL(k_compact_write, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts,
                      o.uniq_keys, o.uniq_pos);
   XF_HIP_CHECK(hipGetLastError());

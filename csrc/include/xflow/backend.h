@@ -44,7 +44,16 @@ struct ScratchView {
   u32 epoch = 1;               // current step (never 0)
   unsigned long long* claims = nullptr;  // device counter of inserted keys
   u64 rebuild_at = 0;          // clear the table before a step once claims > rebuild_at
+  // HIP backend: adaptive active capacity, kept on the device (no host sync).
+  // ctl[0] = active cap (power of two <= cap), ctl[1] = most unique keys seen
+  // in one batch, ctl[2] = cap to rebuild at before the next batch (0: none).
+  // The table is probed modulo ctl[0]; the compaction scan re-sizes it to
+  // kScratchHeadroom x the largest batch seen (a table that fits the Infinity
+  // Cache instead of one sized for all-distinct batches).  Null: use cap.
+  unsigned long long* ctl = nullptr;
 };
+constexpr u64 kScratchHeadroom = 8;      // active cap >= 8 x max unique keys per batch
+constexpr u64 kScratchMinCap = 1ull << 16;
 
 struct DedupOut {
   u32* pos = nullptr;          // [nnz] scratch slot of each occurrence
@@ -147,6 +156,7 @@ struct SynthArgs {                 // synthetic Criteo-shaped batch generator
   uint64_t step = 0;
   float planted_scale = 0.3f;
   float planted_bias = -1.2f;
+  int64_t col_stride = 0;            // > 0: field-major output (BatchView::col_stride)
 };
 
 class Backend {

@@ -111,7 +111,14 @@ XF_HD void slot_push(u32* slot, u64 key, int p, float g, const TableLayout& L,
   }
 }
 
-// A batch in CSR form (device or host pointers, depending on the backend).
+// A batch (device or host pointers, depending on the backend).  Three layouts
+// of the per-occurrence arrays (keys, fgid, and the engine's dedup positions):
+//   CSR          row_ptr != null: row r = [row_ptr[r], row_ptr[r+1])
+//   row-major    fixed nnz_per_row, col_stride == 0: (r, j) at r*nnz_per_row + j
+//   field-major  fixed nnz_per_row, col_stride > 0: (r, j) at j*col_stride + r
+// Field-major is the layout of fixed-width CTR batches on the device: a
+// workgroup's rows of one field are contiguous, so per-field passes (dedup
+// windows, gradient aggregation) read and write coalesced.
 struct BatchView {
   const u64* keys = nullptr;      // [nnz]
   const int32_t* row_ptr = nullptr;  // [rows+1]; null => fixed nnz_per_row
@@ -121,7 +128,31 @@ struct BatchView {
   int64_t nnz = 0;
   int nnz_per_row = 0;            // used when row_ptr == null
   int64_t slice_rows = 0;         // rows per slice (gradient normaliser); 0 => rows
+  int64_t col_stride = 0;         // field-major stride (>= rows), 0 => row-major
 };
+
+// Occurrences of one row: j-th at base + j*step.
+struct RowSpan {
+  int64_t base = 0, step = 1;
+  int len = 0;
+  XF_HD int64_t at(int j) const { return base + (int64_t)j * step; }
+};
+
+XF_HD RowSpan row_span(const BatchView& b, int64_t r) {
+  RowSpan s;
+  if (b.row_ptr) {
+    s.base = b.row_ptr[r];
+    s.len = (int)(b.row_ptr[r + 1] - b.row_ptr[r]);
+  } else if (b.col_stride > 0) {
+    s.base = r;
+    s.step = b.col_stride;
+    s.len = b.nnz_per_row;
+  } else {
+    s.base = r * b.nnz_per_row;
+    s.len = b.nnz_per_row;
+  }
+  return s;
+}
 
 // Loss statistics accumulated by forward passes (device or host memory).
 struct LossStats {

@@ -119,7 +119,8 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_readwrite("rows", &BatchView::rows)
       .def_readwrite("nnz", &BatchView::nnz)
       .def_readwrite("nnz_per_row", &BatchView::nnz_per_row)
-      .def_readwrite("slice_rows", &BatchView::slice_rows);
+      .def_readwrite("slice_rows", &BatchView::slice_rows)
+      .def_readwrite("col_stride", &BatchView::col_stride);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,
@@ -226,8 +227,10 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def("synth_batch",
            [](Engine& e, int64_t rows, std::vector<uint64_t> vocab, std::vector<float> zipf,
               uint64_t hash_space, uint64_t seed, uint64_t step, float scale, float bias,
-              int64_t slice_rows, uintptr_t keys, uintptr_t labels, uintptr_t fgid) {
+              int64_t slice_rows, uintptr_t keys, uintptr_t labels, uintptr_t fgid,
+              bool field_major) {
              SynthArgs a;
+             a.col_stride = field_major ? rows : 0;
              a.keys = P<u64>(keys);
              a.labels = P<float>(labels);
              a.fgid = P<int32_t>(fgid);
@@ -245,7 +248,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("rows"), py::arg("vocab"), py::arg("zipf"), py::arg("hash_space"),
            py::arg("seed"), py::arg("step"), py::arg("scale"), py::arg("bias"),
            py::arg("slice_rows"), py::arg("keys") = 0, py::arg("labels") = 0,
-           py::arg("fgid") = 0)
+           py::arg("fgid") = 0, py::arg("field_major") = false)
       .def("stage_host_batch",
            [](Engine& e, py::array_t<uint64_t> keys, py::object row_ptr, py::object fgid,
               py::array_t<float> labels, int nnz_per_row, int64_t slice_rows) {

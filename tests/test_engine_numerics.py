@@ -23,7 +23,15 @@ CASES = [
 ]
 
 
-def _run(device, kind, opt, fm_math, mvm_math, slices, steps=3, rows=96, v_dim=4):
+def _batch(layout, rows, step):
+    """CSR (variable rows) or fixed-width rows stored row-major / field-major."""
+    fixed = layout != "csr"
+    keys, rp, fg, lab = random_csr(rows, fields=6, vocab=60, seed=100 + step, variable=not fixed)
+    return keys, rp, fg, lab
+
+
+def _run(device, kind, opt, fm_math, mvm_math, slices, steps=3, rows=96, v_dim=4,
+         layout="csr"):
     m = ModelConfig(kind=kind, v_dim=v_dim, fm_math=fm_math, mvm_math=mvm_math)
     o = OptimConfig(kind=opt)
     eng = Engine(m, o, EngineConfig(table_log2_cap=14, max_rows=rows, max_nnz=rows * 16,
@@ -33,12 +41,16 @@ def _run(device, kind, opt, fm_math, mvm_math, slices, steps=3, rows=96, v_dim=4
                              init_fn=lambda k, d: normal_init(k, d) * np.float32(1e-2))
     slice_rows = rows // slices
     for step in range(steps):
-        keys, rp, fg, lab = random_csr(rows, fields=6, vocab=60, seed=100 + step)
+        keys, rp, fg, lab = _batch(layout, rows, step)
         b = to_batch(keys, rp, fg, lab, device, slice_rows=slice_rows)
+        if layout != "csr":
+            b.row_ptr, b.nnz_per_row = None, 6
+            if layout == "field":
+                b = b.to_field_major()
         eng.train_step(b)
         torch_ref.train_step(ref, kind, keys, lab, rp, slice_rows, fg, fm_math, mvm_math)
     # all keys seen
-    allk = np.unique(np.concatenate([random_csr(rows, 6, 60, 100 + s)[0] for s in range(steps)]))
+    allk = np.unique(np.concatenate([_batch(layout, rows, s)[0] for s in range(steps)]))
     got = eng.pull(allk)
     want = ref.weights(allk, insert=False).numpy()
     assert eng.table_size() == len(allk)
@@ -56,6 +68,29 @@ def test_engine_matches_torch_reference_cpu(kind, opt, fm_math, mvm_math, slices
 def test_engine_matches_torch_reference_gpu(gpu_device, kind, opt, fm_math, mvm_math, slices):
     got, want, eng = _run(gpu_device, kind, opt, fm_math, mvm_math, slices)
     assert eng.is_gpu and eng.backend_name.startswith("hip:gfx950")
+    np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+
+
+LAYOUT_CASES = [
+    ("lr", "ftrl", "reference", "compat", 1, "field"),
+    ("lr", "ftrl", "reference", "compat", 4, "field"),
+    ("lr", "sgd", "reference", "compat", 1, "fixed"),
+    ("fm", "ftrl", "standard", "compat", 3, "field"),
+    ("mvm", "ftrl", "reference", "fixed", 2, "field"),
+]
+
+
+@pytest.mark.parametrize("kind,opt,fm_math,mvm_math,slices,layout", LAYOUT_CASES)
+def test_fixed_width_layouts_cpu(kind, opt, fm_math, mvm_math, slices, layout):
+    got, want, _ = _run(torch.device("cpu"), kind, opt, fm_math, mvm_math, slices,
+                        layout=layout)
+    np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,opt,fm_math,mvm_math,slices,layout", LAYOUT_CASES)
+def test_fixed_width_layouts_gpu(gpu_device, kind, opt, fm_math, mvm_math, slices, layout):
+    got, want, _ = _run(gpu_device, kind, opt, fm_math, mvm_math, slices, layout=layout)
     np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
 
 

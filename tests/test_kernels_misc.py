@@ -59,9 +59,18 @@ def test_synthetic_criteo_shape(devname):
     gen = SyntheticCriteo(eng, rows, cfg)
     b = gen.alloc_batch()
     gen.next(out=b)
-    k = b.keys.cpu().numpy().reshape(rows, cfg.fields)
+    assert b.field_major
+    # field-major layout [field][row]; the row-major generator gives its transpose
+    k = b.keys.cpu().numpy().reshape(cfg.fields, rows).T
     assert (k >= 0).all() and (k < cfg.hash_space).all()
-    assert (b.fgid.cpu().numpy().reshape(rows, -1) == np.arange(cfg.fields)).all()
+    assert (b.fgid.cpu().numpy().reshape(cfg.fields, rows).T == np.arange(cfg.fields)).all()
+    rm = SyntheticCriteo(eng, rows, SynthConfig(field_major=False))
+    brm = rm.alloc_batch()
+    rm.next(out=brm)
+    assert not brm.field_major
+    np.testing.assert_array_equal(brm.keys.cpu().numpy().reshape(rows, cfg.fields), k)
+    assert torch.equal(brm.labels, b.labels)
+    assert torch.equal(brm.to_field_major().keys, b.keys)
     y = b.labels.cpu().numpy()
     assert set(np.unique(y)) <= {0.0, 1.0} and 0.1 < y.mean() < 0.45
     # power-law: the 3-valued field has very few distinct keys, big fields many

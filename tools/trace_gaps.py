@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Timeline summary of a rocprofv3 kernel trace: GPU busy vs idle time and the
+idle gaps that follow each kernel (the host-side stalls between launches).
+
+    python tools/trace_gaps.py gpurun_out/prof_x/run_kernel_trace.csv [--last N]
+
+--last N restricts the analysis to the last N dispatches of the most frequent
+kernel's period (the timed steps), so warmup and setup are excluded.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--skip", type=float, default=0.3,
+                    help="fraction of the trace (by time) to skip as warmup")
+    ap.add_argument("--top", type=int, default=12)
+    a = ap.parse_args()
+    rows = []
+    with open(a.trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))
+    rows.sort()
+    if not rows:
+        return
+    t0, t1 = rows[0][0], max(r[1] for r in rows)
+    cut = t0 + a.skip * (t1 - t0)
+    rows = [r for r in rows if r[0] >= cut]
+    busy = collections.Counter()
+    gaps = collections.Counter()
+    ngap = collections.Counter()
+    end = rows[0][0]
+    total_busy = 0
+    for i, (s, e, n) in enumerate(rows):
+        if i and s > end:
+            gaps[rows[i - 1][2] + " -> " + n[:30]] += s - end
+            ngap[rows[i - 1][2] + " -> " + n[:30]] += 1
+        total_busy += max(0, e - max(s, end))
+        busy[n] += e - s
+        end = max(end, e)
+    wall = end - rows[0][0]
+    print(f"window {wall / 1e6:.3f} ms  busy {total_busy / 1e6:.3f} ms "
+          f"({100.0 * total_busy / max(wall, 1):.1f}%)  idle {(wall - total_busy) / 1e6:.3f} ms")
+    print("-- busy by kernel (us total)")
+    for n, t in busy.most_common(a.top):
+        print(f"  {t / 1e3:10.1f}  {n}")
+    print("-- idle gaps after kernel (us total, count)")
+    for n, t in gaps.most_common(a.top):
+        print(f"  {t / 1e3:10.1f}  x{ngap[n]:<4d} {n}")
+
+
+if __name__ == "__main__":
+    main()

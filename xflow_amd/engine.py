@@ -20,7 +20,9 @@ from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
 
 @dataclass
 class Batch:
-    """A CSR batch of torch tensors on the engine's device."""
+    """A batch of torch tensors on the engine's device: CSR (row_ptr), or
+    fixed-width rows stored row-major or field-major (``field_major``: keys
+    and fgid laid out [nnz_per_row][rows], see csrc/include/xflow/types.h)."""
 
     keys: torch.Tensor                  # int64 [nnz] (u64 bit patterns)
     labels: torch.Tensor                # float32 [rows]
@@ -28,6 +30,7 @@ class Batch:
     fgid: Optional[torch.Tensor] = None      # int32 [nnz]
     nnz_per_row: int = 0
     slice_rows: int = 0                 # rows per slice (gradient normaliser); 0 => all rows
+    field_major: bool = False
 
     @property
     def rows(self) -> int:
@@ -48,6 +51,7 @@ class Batch:
         v.nnz = self.nnz
         v.nnz_per_row = self.nnz_per_row
         v.slice_rows = self.slice_rows
+        v.col_stride = self.rows if self.field_major else 0
         return v
 
     def check(self, device: torch.device) -> None:
@@ -66,6 +70,19 @@ class Batch:
                 raise ValueError("fixed-width batch needs nnz == rows * nnz_per_row")
         elif self.row_ptr.numel() != self.rows + 1:
             raise ValueError("row_ptr must have rows+1 entries")
+        if self.field_major and self.row_ptr is not None:
+            raise ValueError("field-major batches are fixed-width (no row_ptr)")
+
+    def to_field_major(self) -> "Batch":
+        """The same fixed-width batch stored field-major."""
+        if self.field_major:
+            return self
+        if self.row_ptr is not None:
+            raise ValueError("only fixed-width batches have a field-major form")
+        F = self.nnz_per_row
+        t = (lambda x: None if x is None else x.view(self.rows, F).t().contiguous().view(-1))
+        return Batch(keys=t(self.keys), labels=self.labels, fgid=t(self.fgid), nnz_per_row=F,
+                     slice_rows=self.slice_rows, field_major=True)
 
 
 def _device_index(device: torch.device) -> int:
@@ -144,12 +161,13 @@ class Engine:
 
     def synth_batch(self, rows: int, vocab, zipf_s, hash_space: int, seed: int, step: int,
                     planted_scale: float = 0.3, planted_bias: float = -1.2, slice_rows: int = 0,
-                    out: Batch | None = None):
+                    out: Batch | None = None, field_major: bool = False):
         """Generate a synthetic batch on the engine's device.
 
         Without ``out`` the batch lives in engine-owned staging memory and a
         native BatchView is returned; with ``out`` (a Batch of preallocated
         tensors) the generator writes into those tensors and ``out`` is returned.
+        ``field_major`` stores keys/fgid [field][row] (same rows, same values).
         """
         self._sync_stream()
         kw = {}
@@ -158,11 +176,13 @@ class Engine:
                       fgid=out.fgid.data_ptr() if out.fgid is not None else 0)
         v = self._e.synth_batch(int(rows), [int(x) for x in vocab], [float(s) for s in zipf_s],
                                 int(hash_space), int(seed), int(step), float(planted_scale),
-                                float(planted_bias), int(slice_rows), **kw)
+                                float(planted_bias), int(slice_rows), field_major=bool(field_major),
+                                **kw)
         if out is None:
             return v
         out.nnz_per_row = len(vocab)
         out.slice_rows = int(slice_rows)
+        out.field_major = bool(field_major)
         return out
 
     def push(self, keys, grads) -> None:
