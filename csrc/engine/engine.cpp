@@ -82,6 +82,19 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   be.memset(grad_, 0, sizeof(float) * scratch_.cap * cfg_.max_slices * ps);
   tmask_ = balloc<u32>(be, scratch_.cap);
   be.memset(tmask_, 0, sizeof(u32) * scratch_.cap);
+  if (be.is_gpu() && cfg_.model.kind == kLR) {
+    const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
+    const int nb = (int)((dests + (1ull << kRedShift) - 1) >> kRedShift);
+    if (nb <= kRedMaxBuckets) {
+      const int64_t groups = (cfg_.max_rows + 1023) / 1024;  // k_lr workgroup rows
+      red_nb_ = nb;
+      red_pairs_ = balloc<u64>(be, nnz);
+      red_sorted_ = balloc<u64>(be, nnz);
+      red_hist_ = balloc<u32>(be, (size_t)nb * groups);
+      red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
+      red_count_ = balloc<u32>(be, groups);
+    }
+  }
   stats_ = balloc<LossStats>(be, 2);
   be.memset(stats_, 0, 2 * sizeof(LossStats));
   bucket_ws_ = balloc<int64_t>(be, 512);
@@ -102,8 +115,19 @@ Engine::~Engine() {
                   uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
-                  host_slots_dev_, scratch_.ctl};
+                  host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
+                  red_tot_, red_count_};
   for (void* p : ptrs) be.free(p);
+}
+
+void Engine::set_reduction(FwdArgs& fa) const {
+  if (!red_pairs_) return;
+  fa.red_pairs = red_pairs_;
+  fa.red_sorted = red_sorted_;
+  fa.red_hist = red_hist_;
+  fa.red_tot = red_tot_;
+  fa.red_count = red_count_;
+  fa.red_nb = red_nb_;
 }
 
 int Engine::slices_of(const BatchView& b) const {
@@ -178,6 +202,7 @@ void Engine::train_step(const BatchView& b) {
   fa.model = cfg_.model;
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
+  set_reduction(fa);
   be_->forward_backward(fa);
 
   ApplyArgs aa;
@@ -386,6 +411,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.model = cfg_.model;
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
+  set_reduction(fa);
   be_->forward_backward(fa);
   GatherGradArgs ga;
   ga.grad = grad_;

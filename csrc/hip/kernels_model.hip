@@ -142,6 +142,85 @@ struct ColumnAgg {
   }
 };
 
+// Column aggregation for the atomic-free LR backward (PS == 1).  Tags carry
+// the column ((j << 32) | dest), so a table needs no reset between the
+// columns that reuse it; the slots a column claims are appended to a list, so
+// the flush touches only those and writes them densely -- the workgroup's
+// (dest, value) pair region fills column after column without a cursor
+// atomic -- and counts them in the LDS histogram of dest >> kRedShift that
+// drives the reduction kernels below.
+template <int LOG2>
+struct ListAgg {
+  static constexpr int kSlots = 1 << LOG2;
+  u64 (*tag)[kSlots];
+  float (*acc)[kSlots];
+  unsigned short (*list)[kSlots / 2];
+  u32* nlist;   // [3] list lengths, rotating over columns
+  u32* hist;    // [red_nb]
+  u64* region;  // this workgroup's pair region
+  u32 written;  // pairs written so far (workgroup-uniform)
+
+  __device__ __forceinline__ void init(int nb) {
+    for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
+      tag[0][i] = tag[1][i] = ~0ull;
+      acc[0][i] = acc[1][i] = 0.0f;
+    }
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0u;
+    if (threadIdx.x < 3) nlist[threadIdx.x] = 0u;
+    written = 0;
+  }
+  // at most kSlots/2 keys per column: the probe terminates
+  __device__ __forceinline__ int insert(int t, int j, u32 dest, bool& claimed) {
+    const u64 key = ((u64)(u32)j << 32) | dest;
+    u32 h = (dest * 0x9E3779B1u) >> (32 - LOG2);
+    while (true) {
+      const u64 cur = tag[t][h];
+      if (cur == key) return (int)h;
+      if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
+        const u64 old = atomicCAS((unsigned long long*)&tag[t][h], (unsigned long long)cur,
+                                  (unsigned long long)key);
+        if (old == cur) {
+          claimed = true;
+          return (int)h;
+        }
+        if (old == key) return (int)h;
+      }
+      h = (h + 1) & (kSlots - 1);
+    }
+  }
+  // called by every lane of the workgroup (wave-uniform control flow)
+  __device__ __forceinline__ void column(int j, bool has, u32 dest, float loss) {
+    const int t = j & 1;
+    if (threadIdx.x == 0) nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
+    bool claimed = false;
+    int h = 0;
+    if (has) {
+      h = insert(t, j, dest, claimed);
+      atomicAdd(&acc[t][h], loss);
+    }
+    const unsigned long long m = __ballot(claimed);
+    if (m) {
+      const int lane = lane_id();
+      const int leader = __ffsll((long long)m) - 1;
+      u32 base = 0;
+      if (lane == leader) base = atomicAdd(&nlist[j % 3], (u32)__popcll(m));
+      base = __shfl(base, leader);
+      if (claimed) list[t][base + (u32)__popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)h;
+    }
+    lds_barrier();
+    const u32 n = nlist[j % 3];
+    for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
+      const int hh = list[t][i];
+      const u32 d = (u32)tag[t][hh];
+      const float v = acc[t][hh];
+      acc[t][hh] = 0.0f;
+      region[written + i] = (u64)d | ((u64)__float_as_uint(v) << 32);
+      atomicAdd(&hist[d >> kRedShift], 1u);
+    }
+    written += n;
+  }
+};
+
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
 
 // Rows of at most kLrRegCols features keep their dedup positions in registers:
@@ -151,7 +230,7 @@ constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
 constexpr int kLrRegCols = 40;
 
 // Backward of one column: exact LDS aggregation, then the LDS-only barrier
-// and the flush of the table (its global atomics stay in flight).
+// and the flush of the table (global atomics left in flight, or pairs).
 template <int LOG2>
 __device__ __forceinline__ void lr_column(ColumnAgg<1, LOG2>& agg, int j, bool has, u32 dest,
                                           float loss, float* __restrict__ grad) {
@@ -165,13 +244,18 @@ __device__ __forceinline__ void lr_column(ColumnAgg<1, LOG2>& agg, int j, bool h
 // equal to the CPU backend).  BLOCK rows per workgroup: larger workgroups
 // aggregate mid-frequency keys better (Criteo-shaped batch: 4.29 M global
 // atomics at 256 rows, 2.95 M at 1024 rows, for 10.2 M occurrences).
-template <bool kGrad, bool kAgg, int BLOCK>
+template <bool kGrad, bool kAgg, int BLOCK, bool kRed = false>
 __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   constexpr int LOG2 = ilog2c(2 * BLOCK);
   constexpr int C = kLrRegCols;
-  __shared__ u32 s_tag[kAgg ? 2 : 1][1 << LOG2];
+  constexpr bool kCol = kAgg && !kRed;  // column tables with global atomics
+  __shared__ u32 s_tag[kCol ? 2 : 1][kCol ? (1 << LOG2) : 1];
   __shared__ float s_acc[kAgg ? 2 : 1][1 << LOG2];
   __shared__ int s_wmax[BLOCK / kWave];
+  __shared__ u64 s_tag64[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
+  __shared__ unsigned short s_list[kRed ? 2 : 1][kRed ? BLOCK : 1];
+  __shared__ u32 s_hist[kRed ? kRedMaxBuckets : 1];
+  __shared__ u32 s_nlist[3];
   const BatchView& b = a.batch;
   const u32* __restrict__ pos = a.pos;
   const float* __restrict__ wp = a.wpull;
@@ -180,8 +264,19 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   RowSpan rs;
   if (active) rs = row_span(b, r);
   const int len = rs.len;
-  ColumnAgg<1, LOG2> agg{s_tag, s_acc};
-  if constexpr (kAgg) agg.init();
+  // (the unused aggregator of an instantiation points at a 1-element array)
+  ColumnAgg<1, LOG2> agg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag[0][0]), s_acc};
+  if constexpr (kCol) agg.init();
+  ListAgg<LOG2> lagg{reinterpret_cast<u64(*)[1 << LOG2]>(&s_tag64[0][0]), s_acc,
+                     reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
+                     s_nlist, s_hist, nullptr, 0u};
+  if constexpr (kRed) {
+    // the workgroup's pair region starts at its first row's first occurrence
+    // (published to the other waves by the barrier below)
+    const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
+    lagg.region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
+    lagg.init(a.red_nb);
+  }
   // block-uniform longest row: selects the register path and bounds the
   // backward column walk
   int maxlen;
@@ -225,8 +320,11 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
           if (j < len) atomicAdd(&a.grad[pv[j] * S + s], loss);
       } else {
 #pragma unroll
-        for (int j = 0; j < C; ++j)
-          if (j < maxlen) lr_column<LOG2>(agg, j, j < len, pv[j] * S + s, loss, a.grad);
+        for (int j = 0; j < C; ++j) {
+          if (j >= maxlen) continue;
+          if constexpr (kRed) lagg.column(j, j < len, pv[j] * S + s, loss);
+          else lr_column<LOG2>(agg, j, j < len, pv[j] * S + s, loss, a.grad);
+        }
       }
     }
   } else {
@@ -253,11 +351,19 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
       if constexpr (!kAgg) {
         for (int j = 0; j < len; ++j) atomicAdd(&a.grad[pos[rs.at(j)] * S + s], loss);
       } else {
-        for (int j = 0; j < maxlen; ++j)
-          lr_column<LOG2>(agg, j, j < len, j < len ? pos[rs.at(j)] * S + s : 0u, loss,
-                          a.grad);
+        for (int j = 0; j < maxlen; ++j) {
+          const u32 dest = j < len ? pos[rs.at(j)] * S + s : 0u;
+          if constexpr (kRed) lagg.column(j, j < len, dest, loss);
+          else lr_column<LOG2>(agg, j, j < len, dest, loss, a.grad);
+        }
       }
     }
+  }
+  if constexpr (kRed) {
+    __syncthreads();
+    if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
+    for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+      a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
   flush_stats<BLOCK>(st, a.stats);
 }
@@ -451,6 +557,109 @@ __global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
   flush_stats<kMvmBlock>(st, a.stats);
 }
 
+// ---------------------------------------------------------------------------
+// LR gradient reduction without global atomics (FwdArgs::red_*).
+// Scattered float atomics execute at the memory side at ~20 G adds/s on
+// gfx950 (one 4-byte add per lane, 64 rows per wave instruction), which made
+// the ~3 M per-column partial sums of a Criteo-shaped batch cost ~145 us.
+// Here they are partitioned by destination bucket (dest >> kRedShift) with
+// plain stores and summed per bucket in a 64 KB LDS accumulator.
+//   1. k_red_scan     per bucket: exclusive scan of the workgroups' counts
+//   2. k_red_scatter  per producing workgroup: bucket starts (scan of the
+//                     bucket totals), then its pairs to their bucket ranges
+//   3. k_red_sum      per bucket: LDS sums, one plain store per non-zero dest
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_red_scan(u32* __restrict__ hist, int groups,
+                                                     u32* __restrict__ tot) {
+  const size_t row = (size_t)blockIdx.x * groups;
+  u32 carry = 0;
+  for (int c0 = 0; c0 < groups; c0 += kBlock) {
+    const int i = c0 + (int)threadIdx.x;
+    const u32 v = i < groups ? hist[row + i] : 0u;
+    u32 t;
+    const u32 ex = block_exclusive_scan<kBlock>(v, &t);
+    if (i < groups) hist[row + i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) tot[blockIdx.x] = carry;
+}
+
+constexpr int kRedBlock = 1024;
+constexpr int kRedUnroll = 4;
+
+__global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows_per_group,
+                                                           const u64* __restrict__ pairs,
+                                                           const u32* __restrict__ count,
+                                                           const u32* __restrict__ hist,
+                                                           const u32* __restrict__ tot,
+                                                           u32* __restrict__ start, int nb,
+                                                           u64* __restrict__ sorted) {
+  __shared__ u32 cur[kRedMaxBuckets];
+  const int g = blockIdx.x, groups = gridDim.x;
+  u32 carry = 0;
+  for (int c0 = 0; c0 < nb; c0 += kRedBlock) {
+    const int i = c0 + (int)threadIdx.x;
+    const u32 v = i < nb ? tot[i] : 0u;
+    u32 t;
+    const u32 ex = block_exclusive_scan<kRedBlock>(v, &t);
+    if (i < nb) {
+      cur[i] = carry + ex + hist[(size_t)i * groups + g];
+      if (g == 0) start[i] = carry + ex;
+    }
+    carry += t;
+  }
+  if (g == 0 && threadIdx.x == 0) start[nb] = carry;
+  __syncthreads();
+  const int64_t r0 = (int64_t)g * rows_per_group;
+  const u64* src = pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
+  const u32 n = count[g];
+  // kRedUnroll independent load -> LDS rank -> store chains per lane
+  for (u32 i0 = threadIdx.x; i0 < n; i0 += kRedUnroll * kRedBlock) {
+    u64 pr[kRedUnroll];
+#pragma unroll
+    for (int q = 0; q < kRedUnroll; ++q) {
+      const u32 i = i0 + (u32)q * kRedBlock;
+      pr[q] = i < n ? src[i] : 0ull;
+    }
+    u32 p[kRedUnroll];
+#pragma unroll
+    for (int q = 0; q < kRedUnroll; ++q)
+      if (i0 + (u32)q * kRedBlock < n) p[q] = atomicAdd(&cur[(u32)pr[q] >> kRedShift], 1u);
+#pragma unroll
+    for (int q = 0; q < kRedUnroll; ++q)
+      if (i0 + (u32)q * kRedBlock < n) sorted[p[q]] = pr[q];
+  }
+}
+
+__global__ void __launch_bounds__(kRedBlock) k_red_sum(const u64* __restrict__ sorted,
+                                                       const u32* __restrict__ start,
+                                                       float* __restrict__ grad) {
+  constexpr u32 kR = 1u << kRedShift;
+  __shared__ float acc[kR];
+  const u32 beg = start[blockIdx.x], end = start[blockIdx.x + 1];
+  if (beg == end) return;
+  for (u32 i = threadIdx.x; i < kR; i += kRedBlock) acc[i] = 0.0f;
+  __syncthreads();
+  for (u32 i0 = beg + threadIdx.x; i0 < end; i0 += kRedUnroll * kRedBlock) {
+    u64 pr[kRedUnroll];
+#pragma unroll
+    for (int q = 0; q < kRedUnroll; ++q) {
+      const u32 i = i0 + (u32)q * kRedBlock;
+      pr[q] = i < end ? sorted[i] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kRedUnroll; ++q)
+      if (i0 + (u32)q * kRedBlock < end)
+        atomicAdd(&acc[(u32)pr[q] & (kR - 1)], __uint_as_float((u32)(pr[q] >> 32)));
+  }
+  __syncthreads();
+  float* g = grad + ((size_t)blockIdx.x << kRedShift);
+  for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
+    const float v = acc[i];
+    if (v != 0.0f) g[i] = v;  // grad is zero outside this step's keys
+  }
+}
+
 template <bool kGrad>
 static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
@@ -494,7 +703,20 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
       // LDS aggregation needs every destination index to fit a u32 tag
       constexpr int kLrBlock = 1024;
       int g = (int)((a.batch.rows + kLrBlock - 1) / kLrBlock);
-      if (grad && a.agg_ok)
+      const bool red = grad && a.agg_ok && a.red_pairs && a.red_nb > 0 &&
+                       a.red_nb <= kRedMaxBuckets;
+      if (red) {
+        hipLaunchKernelGGL((k_lr<true, true, kLrBlock, true>), dim3(g), dim3(kLrBlock), 0, st,
+                           a);
+        hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, g,
+                           a.red_tot);
+        u32* start = a.red_tot + a.red_nb + 1;
+        hipLaunchKernelGGL(k_red_scatter, dim3(g), dim3(kRedBlock), 0, st, a.batch, kLrBlock,
+                           a.red_pairs, a.red_count, a.red_hist, a.red_tot, start, a.red_nb,
+                           a.red_sorted);
+        hipLaunchKernelGGL(k_red_sum, dim3(a.red_nb), dim3(kRedBlock), 0, st, a.red_sorted, start,
+                           a.grad);
+      } else if (grad && a.agg_ok)
         hipLaunchKernelGGL((k_lr<true, true, kLrBlock>), dim3(g), dim3(kLrBlock), 0, st, a);
       else if (grad)
         hipLaunchKernelGGL((k_lr<true, false, kBlock>), dim3(grid), dim3(kBlock), 0, st, a);

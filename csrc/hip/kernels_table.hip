@@ -202,31 +202,6 @@ __device__ __forceinline__ unsigned int compact_hits(const ScratchView& sv, u64 
   return hit;
 }
 
-// Block-wide exclusive scan of one value per lane; returns the exclusive
-// prefix and writes the block total to *total.
-template <int BLOCK>
-__device__ __forceinline__ unsigned int block_exclusive_scan(unsigned int v, unsigned int* total) {
-  __shared__ unsigned int wsum[BLOCK / kWave];
-  const int lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
-  unsigned int incl = v;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    unsigned int t = __shfl_up(incl, o);
-    if (lane >= o) incl += t;
-  }
-  if (lane == kWave - 1) wsum[w] = incl;
-  __syncthreads();
-  unsigned int off = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < BLOCK / kWave; ++i) {
-    off += (i < w) ? wsum[i] : 0u;
-    tot += wsum[i];
-  }
-  __syncthreads();
-  *total = tot;
-  return off + incl - v;
-}
-
 // lane t owns the 16 consecutive slots [base + 16t, base + 16t + 16): the
 // stamp loads are dwordx4-able and the output stays in slot order
 __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,

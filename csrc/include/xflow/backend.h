@@ -75,7 +75,18 @@ struct FwdArgs {
   ModelSpec model;
   int S = 1;                       // slices in this batch
   bool agg_ok = false;             // grad indices (pos*S+s)*pstride fit in a u32 (LDS aggregation)
+  // HIP LR gradient reduction without global float atomics (null: atomics).
+  // Workgroups write their per-column partial sums as (dest, value) pairs,
+  // which are partitioned by dest >> kRedShift and summed per bucket in LDS.
+  u64* red_pairs = nullptr;        // [nnz] per-workgroup pair regions
+  u64* red_sorted = nullptr;       // [nnz] pairs in bucket order
+  u32* red_hist = nullptr;         // [red_nb][workgroups] pairs per (bucket, workgroup)
+  u32* red_tot = nullptr;          // [red_nb + 1] pairs per bucket, then bucket starts
+  u32* red_count = nullptr;        // [workgroups] pairs per workgroup
+  int red_nb = 0;                  // buckets = ceil(grad dests / 2^kRedShift)
 };
+constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
+constexpr int kRedMaxBuckets = 4096;
 
 struct PullArgs {
   TableView table;

@@ -128,6 +128,14 @@ class Engine {
   float* wpull_ = nullptr;      // [scratch_cap * pstride]
   float* grad_ = nullptr;       // [scratch_cap * max_slices * pstride]
   u32* tmask_ = nullptr;        // [scratch_cap]
+  // HIP LR gradient reduction workspace (FwdArgs::red_*), null when unused
+  u64* red_pairs_ = nullptr;
+  u64* red_sorted_ = nullptr;
+  u32* red_hist_ = nullptr;
+  u32* red_tot_ = nullptr;
+  u32* red_count_ = nullptr;
+  int red_nb_ = 0;
+  void set_reduction(FwdArgs& fa) const;
   LossStats* stats_ = nullptr;  // [1]
   u32* send_pos_ = nullptr;     // [max_nnz]
   int64_t* bucket_ws_ = nullptr;  // [2*256]
