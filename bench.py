@@ -96,10 +96,16 @@ def main():
         from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
         sharded = AsyncShardedEngine(engine) if a.async_p2p else ShardedEngine(engine)
-        batch = gen.alloc_batch()
+        # double-buffered batches: batch t+1 is generated on the device while
+        # the host waits for step t's all-to-all split sizes
+        bufs = [gen.alloc_batch(), gen.alloc_batch()]
+        gen.next(out=bufs[0])
+        cur = [0]
 
         def step():
-            sharded.train_step(gen.next(out=batch))
+            i = cur[0]
+            sharded.train_step(bufs[i], prefetch=lambda: gen.next(out=bufs[i ^ 1]))
+            cur[0] = i ^ 1
     else:
         def step():
             engine.train_view(gen.next())

@@ -86,7 +86,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
     const int nb = (int)((dests + (1ull << kRedShift) - 1) >> kRedShift);
     if (nb <= kRedMaxBuckets) {
-      const int64_t groups = (cfg_.max_rows + 1023) / 1024;  // k_lr workgroup rows
+      const int64_t groups = (cfg_.max_rows + kLrGroupRows - 1) / kLrGroupRows;
       red_nb_ = nb;
       red_pairs_ = balloc<u64>(be, nnz);
       red_sorted_ = balloc<u64>(be, nnz);
@@ -153,16 +153,22 @@ const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
   return slice_rows_;
 }
 
-void Engine::dedup_(const BatchView& b) {
+void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out) {
   if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
   if (b.col_stride > 0 && (b.row_ptr || b.col_stride < b.rows || b.nnz != b.rows * b.nnz_per_row))
     throw std::invalid_argument("field-major batch needs fixed nnz_per_row and col_stride >= rows");
+  if (parts != scratch_.parts) {
+    // slots depend on the partitioning: start from an empty scratch table
+    be_->fill_u64(scratch_.keys, kEmptyKey, scratch_.cap);
+    be_->memset(scratch_.claims, 0, sizeof(unsigned long long));
+    scratch_.parts = parts;
+  }
   be_->memset(n_uniq_, 0, sizeof(int64_t));
   if (++scratch_.epoch == 0) scratch_.epoch = 1;  // 0 marks never-stamped slots
   DedupOut o;
   o.pos = pos_;
-  o.uniq_keys = uniq_keys_;
+  o.uniq_keys = uniq_keys_out ? uniq_keys_out : uniq_keys_;
   o.uniq_pos = uniq_pos_;
   o.n_uniq = n_uniq_;
   o.overflow = overflow_;
@@ -334,6 +340,14 @@ std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
 void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out) {
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  if (world > 1 && world <= kMaxParts && be_->partitioned_dedup()) {
+    // owner-partitioned scratch: the slot-ordered unique list is the send
+    // order already; counts are range counts
+    dedup_(b, world, send_keys_out);
+    be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
+    send_map_ = uniq_pos_;
+    return;
+  }
   dedup_(b);
   BucketArgs ba;
   ba.uniq_keys = uniq_keys_;
@@ -346,6 +360,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
   ba.send_pos = send_pos_;
   ba.scratch = bucket_ws_;
   be_->bucket(ba);
+  send_map_ = send_pos_;
   (void)S;  // slice masks are built in w_forward_backward with the step's global S
 }
 
@@ -359,7 +374,7 @@ void Engine::ensure_server_capacity(int64_t n, int buf) {
 }
 
 void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr) {
-  be_->scatter_rows(pulled, wpull_, send_pos_, nullptr, n_send, pstride());
+  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, pstride());
   FwdArgs fa;
   fa.batch = b;
   fa.pos = pos_;
@@ -400,7 +415,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
-  be_->scatter_rows(pulled, wpull_, send_pos_, nullptr, n_send, ps);
+  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, ps);
   if (masks) be_->slice_masks(b, pos_, tmask_);
   FwdArgs fa;
   fa.batch = b;
@@ -418,7 +433,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   ga.grad_rw = grad_;
   ga.tmask = masks ? tmask_ : nullptr;
   ga.tmask_rw = masks ? tmask_ : nullptr;
-  ga.map = send_pos_;
+  ga.map = send_map_;
   ga.n_max = n_send;
   ga.S = S;
   ga.pstride = ps;

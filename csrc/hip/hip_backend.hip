@@ -78,6 +78,11 @@ class HipBackend final : public Backend {
     hip::launch_slice_masks(b, pos, tmask, stream_);
   }
   void bucket(const BucketArgs& a) override { hip::launch_bucket(a, stream_); }
+  bool partitioned_dedup() const override { return true; }
+  void partition_counts(const ScratchView& s, const u32* chunk_offsets, const int64_t* n_uniq,
+                        int64_t* counts) override {
+    hip::launch_partition_counts(s, chunk_offsets, n_uniq, counts, stream_);
+  }
   void gather_grads(const GatherGradArgs& a) override { hip::launch_gather_grads(a, stream_); }
   void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                     int64_t n_max, int width) override {

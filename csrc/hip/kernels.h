@@ -16,6 +16,8 @@ void launch_table_pull(const PullArgs& a, hipStream_t st);
 void launch_table_apply(const ApplyArgs& a, hipStream_t st);
 void launch_gather_grads(const GatherGradArgs& a, hipStream_t st);
 void launch_bucket(const BucketArgs& a, hipStream_t st);
+void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
+                             const int64_t* n_uniq, int64_t* counts, hipStream_t st);
 void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                          int64_t n_max, int width, hipStream_t st);
 void launch_gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,

@@ -706,12 +706,13 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
       const bool red = grad && a.agg_ok && a.red_pairs && a.red_nb > 0 &&
                        a.red_nb <= kRedMaxBuckets;
       if (red) {
-        hipLaunchKernelGGL((k_lr<true, true, kLrBlock, true>), dim3(g), dim3(kLrBlock), 0, st,
-                           a);
-        hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, g,
+        constexpr int R = kLrGroupRows;
+        const int gr = (int)((a.batch.rows + R - 1) / R);
+        hipLaunchKernelGGL((k_lr<true, true, R, true>), dim3(gr), dim3(R), 0, st, a);
+        hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, gr,
                            a.red_tot);
         u32* start = a.red_tot + a.red_nb + 1;
-        hipLaunchKernelGGL(k_red_scatter, dim3(g), dim3(kRedBlock), 0, st, a.batch, kLrBlock,
+        hipLaunchKernelGGL(k_red_scatter, dim3(gr), dim3(kRedBlock), 0, st, a.batch, R,
                            a.red_pairs, a.red_count, a.red_hist, a.red_tot, start, a.red_nb,
                            a.red_sorted);
         hipLaunchKernelGGL(k_red_sum, dim3(a.red_nb), dim3(kRedBlock), 0, st, a.red_sorted, start,

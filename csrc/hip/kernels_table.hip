@@ -94,6 +94,8 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
   __shared__ u64 t_key[kL];  // keys during the LDS level, then leaders' slots
   u64* __restrict__ skeys = sv.keys;
   const u64 cap = active_cap(sv), mask = cap - 1;
+  const u32 parts = (u32)sv.parts;
+  const u64 R = parts > 1 ? cap / parts : cap;  // probe range per owner
   const int64_t base = (int64_t)blockIdx.x * kDedupChunk + threadIdx.x;
   for (u32 i = threadIdx.x; i < kL; i += kBlock) t_key[i] = kEmptyKey;
   u64 k[kDedupItems], s[kDedupItems];
@@ -103,7 +105,8 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
     int64_t i = base + (int64_t)j * kBlock;
     k[j] = i < nnz ? sanitize_key(keys[i]) : 0ull;
     const u64 f = fmix64(k[j]);
-    s[j] = f & mask;
+    s[j] = parts > 1 ? (u64)((u32)(f >> 32) % parts) * R + (((f & 0xffffffffull) * R) >> 32)
+                     : f & mask;
     h[j] = (u32)(f >> (64 - kDedupLog2));
   }
   __syncthreads();
@@ -151,11 +154,16 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
         }
         if (prev == k[j]) break;
       }
-      if (++n >= cap) {
+      if (++n >= R) {
         *overflow = 1u;
         break;
       }
-      sj = (sj + 1) & mask;
+      if (parts > 1) {
+        ++sj;
+        if (sj % R == 0) sj -= R;  // wrap inside the owner's range
+      } else {
+        sj = (sj + 1) & mask;
+      }
       c = skeys[sj];
     }
     t_key[h[j]] = sj;
@@ -263,6 +271,44 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
     up[dst] = (u32)s;
     ++dst;
   }
+}
+
+// Owner-partitioned dedup: the unique list is in slot order, so owner o's
+// keys start at the number of stamped slots below o*R = the compaction offset
+// of the chunk holding o*R plus the hits in that chunk below it (one wave per
+// boundary, 64 slots per lane).  counts[o] = start[o+1] - start[o].
+constexpr int kPartBlock = 1024;
+
+__global__ void __launch_bounds__(kPartBlock) k_partition_counts(
+    ScratchView sv, const unsigned int* __restrict__ offs, const int64_t* __restrict__ n_uniq,
+    int64_t* __restrict__ counts) {
+  __shared__ int64_t start[kMaxParts + 1];
+  const u32 parts = (u32)sv.parts;
+  const u64 R = active_cap(sv) / parts;
+  const int lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
+  for (u32 o = w; o <= parts; o += kPartBlock / kWave) {
+    if (o == 0 || o == parts) {
+      if (lane == 0) start[o] = o == 0 ? 0 : *n_uniq;
+      continue;
+    }
+    const u64 b = (u64)o * R, c = b / kCompactChunk, c0 = c * kCompactChunk;
+    unsigned int hits = 0;
+    for (u64 q = c0 + (u64)lane * 64; q < c0 + (u64)lane * 64 + 64; ++q)
+      hits += (q < b && sv.stamps[q] == sv.epoch) ? 1u : 0u;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) hits += __shfl_xor(hits, d);
+    if (lane == 0) start[o] = (int64_t)offs[c] + hits;
+  }
+  __syncthreads();
+  for (u32 o = threadIdx.x; o < parts; o += kPartBlock) counts[o] = start[o + 1] - start[o];
+}
+
+void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
+                             const int64_t* n_uniq, int64_t* counts, hipStream_t st) {
+  if (s.parts < 2 || s.parts > kMaxParts) throw std::runtime_error("partition_counts: bad parts");
+  hipLaunchKernelGGL(k_partition_counts, dim3(1), dim3(kPartBlock), 0, st, s, chunk_offsets,
+                     n_uniq, counts);
+  XF_HIP_CHECK(hipGetLastError());
 }
 
 void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st) {

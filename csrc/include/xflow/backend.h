@@ -17,6 +17,7 @@
 #include <stdint.h>
 
 #include <memory>
+#include <stdexcept>
 #include <string>
 
 #include "xflow/types.h"
@@ -51,7 +52,14 @@ struct ScratchView {
   // kScratchHeadroom x the largest batch seen (a table that fits the Infinity
   // Cache instead of one sized for all-distinct batches).  Null: use cap.
   unsigned long long* ctl = nullptr;
+  // HIP: owner-partitioned probing for the sharded step.  With parts > 1 the
+  // active capacity is split into `parts` equal ranges and a key probes only
+  // the range of its owner (owner_of(key, parts)), so the slot-ordered unique
+  // list comes out grouped by owner -- the all-to-all send order -- and the
+  // per-owner counts are range counts (Backend::partition_counts).
+  int parts = 1;
 };
+constexpr int kMaxParts = 1024;
 constexpr u64 kScratchHeadroom = 8;      // active cap >= 8 x max unique keys per batch
 constexpr u64 kScratchMinCap = 1ull << 16;
 
@@ -87,6 +95,7 @@ struct FwdArgs {
 };
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
+constexpr int kLrGroupRows = 1024;  // rows per LR workgroup on the reduction path
 
 struct PullArgs {
   TableView table;
@@ -199,6 +208,14 @@ class Backend {
   virtual void forward_backward(const FwdArgs& a) = 0;
   virtual void slice_masks(const BatchView& b, const u32* pos, u32* tmask) = 0;
   virtual void bucket(const BucketArgs& a) = 0;
+  // Owner-partitioned dedup (ScratchView::parts > 1, HIP only): per-owner
+  // counts of the unique list from the compaction's chunk offsets.
+  virtual bool partitioned_dedup() const { return false; }
+  virtual void partition_counts(const ScratchView& s, const u32* chunk_offsets,
+                                const int64_t* n_uniq, int64_t* counts) {
+    (void)s, (void)chunk_offsets, (void)n_uniq, (void)counts;
+    throw std::runtime_error("partitioned dedup is not supported by this backend");
+  }
   virtual void gather_grads(const GatherGradArgs& a) = 0;
   // rows of `width` floats: dst[map? map[i] : i] = src[i]   (scatter)
   virtual void scatter_rows(const float* src, float* dst, const u32* map,

@@ -109,7 +109,10 @@ class Engine {
  private:
   void ensure_server_capacity(int64_t n, int buf = 0);
   const int32_t* slice_rows_dev(const BatchView& b, int S);
-  void dedup_(const BatchView& b);
+  // parts > 1: owner-partitioned scratch (ScratchView::parts); uniq_keys_out
+  // redirects the unique-key list (the sharded step's send buffer)
+  void dedup_(const BatchView& b, int parts = 1, u64* uniq_keys_out = nullptr);
+  const u32* send_map_ = nullptr;  // send order -> scratch slot (send_pos_ or uniq_pos_)
 
   EngineConfig cfg_;
   std::unique_ptr<Backend> be_;

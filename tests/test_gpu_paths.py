@@ -66,3 +66,107 @@ def test_trainer_gpu_matches_cpu_on_bundled_data(gpu_device, tmp_path):
         Trainer(cfg, device=dev).train()
         preds.append(np.loadtxt(d / "pred_0_0.txt"))
     np.testing.assert_allclose(preds[0], preds[1], rtol=1e-4, atol=1e-5)
+
+
+class _LocalBus:
+    """In-process all-to-all between threads (one engine per 'rank' on the
+    same GPU): every rank posts its input, waits for all, copies its parts."""
+
+    def __init__(self, world):
+        import threading
+
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.posted = [None] * world
+
+    def a2a(self, rank, out, inp, out_splits, in_splits):
+        W = self.world
+        if in_splits is None:
+            in_splits = [inp.shape[0] // W] * W
+            out_splits = [out.shape[0] // W] * W
+        self.posted[rank] = (inp, [int(x) for x in in_splits])
+        self.barrier.wait()
+        ro = 0
+        for src in range(W):
+            sinp, ssplits = self.posted[src]
+            so = sum(ssplits[:rank])
+            n = int(out_splits[src])
+            assert n == ssplits[rank]
+            if n:
+                out[ro:ro + n].copy_(sinp[so:so + n])
+            ro += n
+        torch.cuda.synchronize()
+        self.barrier.wait()  # everyone copied before inputs are reused
+
+
+def _local_sharded(bus, rank, engine):
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    class LocalSharded(ShardedEngine):
+        def _a2a(self, out, inp, out_splits, in_splits):
+            bus.a2a(rank, out, inp, out_splits, in_splits)
+
+    return LocalSharded(engine, world=bus.world, rank=rank)
+
+
+@pytest.mark.parametrize("world,kind", [(2, "lr"), (3, "lr"), (2, "fm")])
+def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind):
+    """W in-process ranks on one GPU (threads + a local all-to-all) train the
+    owner-partitioned sharded step; the union of their shards equals one
+    engine trained on the concatenated batches (same check as the gloo
+    multi-rank test, here through the HIP partitioned dedup)."""
+    import threading
+
+    from xflow_amd.testing.hashing import owner_of
+
+    rows, steps = 256, 3
+
+    def mk():
+        return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
+                      EngineConfig(table_log2_cap=16, max_rows=world * rows,
+                                   max_nnz=world * rows * 16, max_slices=world),
+                      device=gpu_device)
+
+    def data(r, s):
+        return random_csr(rows, 6, 120, seed=1000 * s + r)
+
+    bus = _LocalBus(world)
+    engines = [mk() for _ in range(world)]
+    errors = []
+
+    def run(r):
+        try:
+            sh = _local_sharded(bus, r, engines[r])
+            for s in range(steps):
+                k, rp, fg, lab = data(r, s)
+                sh.train_step(to_batch(k, rp, fg, lab, gpu_device), S=1)
+            torch.cuda.synchronize()
+        except BaseException as e:  # surfaced below
+            errors.append(e)
+            bus.barrier.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
+    ref = mk()
+    for s in range(steps):
+        parts = [data(r, s) for r in range(world)]
+        keys = np.concatenate([p[0] for p in parts])
+        lab = np.concatenate([p[3] for p in parts])
+        fg = np.concatenate([p[2] for p in parts])
+        rp = np.concatenate([parts[0][1]] + [p[1][1:] + sum(len(q[0]) for q in parts[:i + 1])
+                                             for i, p in enumerate(parts[1:])])
+        ref.train_step(to_batch(keys, rp.astype(np.int32), fg, lab, gpu_device,
+                                slice_rows=rows))
+    allk, allv = [], []
+    for r, e in enumerate(engines):
+        k, _ = e.export_table()
+        assert (owner_of(k, world) == r).all()
+        allk.append(k)
+        allv.append(e.pull(k))
+    k = np.concatenate(allk)
+    assert len(np.unique(k)) == len(k) == ref.table_size()
+    np.testing.assert_allclose(np.concatenate(allv), ref.pull(k), rtol=1e-4, atol=1e-6)

@@ -71,14 +71,14 @@ class AsyncShardedEngine(ShardedEngine):
         self.engine.s_apply(recv_keys, grads_in, masks_in, offsets, S, buf=buf)
         self._pending = None
 
-    def train_step(self, batch: Batch, S: Optional[int] = None) -> None:
+    def train_step(self, batch: Batch, S: Optional[int] = None, prefetch=None) -> None:
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.pstride
         W = S * ps
         ordered_masks = S > 1 and not e.cfg.sum_slices
         buf = self._parity
-        send_splits, recv_splits, recv_keys = self._exchange_keys(batch)
+        send_splits, recv_splits, recv_keys = self._exchange_keys(batch, prefetch)
         n_send, n_recv = self.last_send, self.last_recv
         # keep this step's received keys alive until its pushes are applied
         rk = self._rk[buf].get(n_recv)

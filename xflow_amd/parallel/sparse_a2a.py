@@ -30,7 +30,7 @@ order -- a deterministic serialisation of the reference's arrival-order pushes.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
@@ -55,11 +55,15 @@ class _Buf:
 class ShardedEngine:
     """Runs Engine phases with sparse all-to-alls between them."""
 
-    def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None):
+    def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
+                 world: Optional[int] = None, rank: Optional[int] = None):
+        """world/rank default to the process group's; passing them (with _a2a
+        overridden) runs the step over another transport, e.g. in-process
+        ranks in tests."""
         self.engine = engine
         self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
+        self.world = int(world) if world is not None else dist.get_world_size(group)
+        self.rank = int(rank) if rank is not None else dist.get_rank(group)
         dev = engine.device
         self.counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
         self.recv_counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
@@ -74,16 +78,41 @@ class ShardedEngine:
         self.last_send = 0
         self.last_recv = 0
         self.bytes_moved = 0
+        self._counts_host = None
+        self._counts_ready = None
 
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def _exchange_keys(self, batch: Batch):
-        """Dedup + bucket + key all-to-all.  Returns (send, recv splits, recv keys)."""
+    def _exchange_keys(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
+        """Dedup + bucket + key all-to-all.  Returns (send, recv splits, recv keys).
+
+        ``prefetch`` (e.g. generating or staging the next batch) is enqueued on
+        the device after the counts exchange and before the host waits for
+        the split sizes, so the device works through that round trip."""
         e = self.engine
         e.w_prepare(batch, self.world, self.counts, self.send_keys)
         self._a2a(self.recv_counts, self.counts, None, None)
-        both = torch.cat([self.counts, self.recv_counts]).cpu().tolist()
+        both = torch.cat([self.counts, self.recv_counts])
+        if both.is_cuda:
+            # the split sizes come back through pinned memory right behind the
+            # counts exchange; the prefetch queues after that copy, so the
+            # device generates the next batch while the host waits and then
+            # launches the key exchange
+            if self._counts_host is None:
+                self._counts_host = torch.empty(2 * self.world, dtype=torch.int64,
+                                                pin_memory=True)
+                self._counts_ready = torch.cuda.Event()
+            self._counts_host.copy_(both, non_blocking=True)
+            self._counts_ready.record()
+            if prefetch is not None:
+                prefetch()
+            self._counts_ready.synchronize()
+            both = self._counts_host.tolist()
+        else:
+            if prefetch is not None:
+                prefetch()
+            both = both.tolist()
         send_splits, recv_splits = both[: self.world], both[self.world:]
         n_send, n_recv = int(sum(send_splits)), int(sum(recv_splits))
         self.last_send, self.last_recv = n_send, n_recv
@@ -101,15 +130,16 @@ class ShardedEngine:
         self._a2a(pulled, vals, send_splits, recv_splits)
         return pulled
 
-    def train_step(self, batch: Batch, S: Optional[int] = None) -> None:
+    def train_step(self, batch: Batch, S: Optional[int] = None,
+                   prefetch: Optional[Callable[[], None]] = None) -> None:
         """One lock-step training step.  S = slices per step, identical on every
         rank (defaults to this batch's slice count, fine when all ranks use the
-        same batch shape)."""
+        same batch shape).  ``prefetch``: see _exchange_keys."""
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.pstride
         ordered_masks = S > 1 and not e.cfg.sum_slices
-        send_splits, recv_splits, recv_keys = self._exchange_keys(batch)
+        send_splits, recv_splits, recv_keys = self._exchange_keys(batch, prefetch)
         n_send, n_recv = self.last_send, self.last_recv
         pulled = self._pull(recv_keys, send_splits, recv_splits, insert=True)
 
