@@ -162,7 +162,8 @@ def main():
                        "parallelism": f"dp{world}+table-shard{world}",
                        "rows_per_gpu": a.batch, "nnz_per_row": synth.fields,
                        "hashed_features": a.features, "table_slots_per_gpu": 2 ** log2_cap,
-                       "backend": engine.backend_name},
+                       "backend": engine.backend_name,
+                       "a2a_transport": sharded.transport if sharded is not None else "none"},
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
         }

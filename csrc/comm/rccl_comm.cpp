@@ -1,0 +1,81 @@
+// xflow-amd: native RCCL transport (see rccl_comm.h).
+#include "rccl_comm.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace xflow {
+
+namespace {
+
+void check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess)
+    throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+}
+
+}  // namespace
+
+std::vector<uint8_t> RcclComm::unique_id() {
+  ncclUniqueId id;
+  check(ncclGetUniqueId(&id), "ncclGetUniqueId");
+  std::vector<uint8_t> out(sizeof(id.internal));
+  std::memcpy(out.data(), id.internal, sizeof(id.internal));
+  return out;
+}
+
+RcclComm::RcclComm(const std::vector<uint8_t>& id, int world, int rank, int device)
+    : world_(world), rank_(rank) {
+  ncclUniqueId uid;
+  if (id.size() != sizeof(uid.internal)) throw std::invalid_argument("RCCL unique id size");
+  std::memcpy(uid.internal, id.data(), sizeof(uid.internal));
+  if (hipSetDevice(device) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
+  ncclComm_t c = nullptr;
+  check(ncclCommInitRank(&c, world, uid, rank), "ncclCommInitRank");
+  comm_ = c;
+}
+
+RcclComm::~RcclComm() {
+  if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+}
+
+void RcclComm::abort() {
+  if (comm_) {
+    ncclCommAbort(static_cast<ncclComm_t>(comm_));
+    comm_ = nullptr;
+  }
+}
+
+void RcclComm::alltoallv(const void* send, const std::vector<int64_t>& send_counts, void* recv,
+                         const std::vector<int64_t>& recv_counts, int elem_bytes,
+                         uintptr_t stream) {
+  if (!comm_) throw std::runtime_error("RCCL communicator was aborted");
+  if ((int)send_counts.size() != world_ || (int)recv_counts.size() != world_)
+    throw std::invalid_argument("alltoallv: counts must have world entries");
+  ncclComm_t c = static_cast<ncclComm_t>(comm_);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const char* s = static_cast<const char*>(send);
+  char* r = static_cast<char*>(recv);
+  size_t so = 0, ro = 0;
+  check(ncclGroupStart(), "ncclGroupStart");
+  for (int p = 0; p < world_; ++p) {
+    const size_t sb = (size_t)send_counts[p] * elem_bytes;
+    const size_t rb = (size_t)recv_counts[p] * elem_bytes;
+    if (sb) check(ncclSend(s + so, sb, ncclUint8, p, c, st), "ncclSend");
+    if (rb) check(ncclRecv(r + ro, rb, ncclUint8, p, c, st), "ncclRecv");
+    so += sb;
+    ro += rb;
+  }
+  check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+void RcclComm::alltoall(const void* send, void* recv, int64_t count, int elem_bytes,
+                        uintptr_t stream) {
+  std::vector<int64_t> cnt(world_, count);
+  alltoallv(send, cnt, recv, cnt, elem_bytes, stream);
+}
+
+}  // namespace xflow

@@ -164,7 +164,7 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out) {
     be_->memset(scratch_.claims, 0, sizeof(unsigned long long));
     scratch_.parts = parts;
   }
-  be_->memset(n_uniq_, 0, sizeof(int64_t));
+  // (n_uniq is written, not accumulated, by both backends' dedup)
   if (++scratch_.epoch == 0) scratch_.epoch = 1;  // 0 marks never-stamped slots
   DedupOut o;
   o.pos = pos_;

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <string>
 
+#include "../comm/rccl_comm.h"
 #include "xflow/engine.h"
 #include "xflow/reader.h"
 #include "xflow/trainer.h"
@@ -121,6 +122,32 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_readwrite("nnz_per_row", &BatchView::nnz_per_row)
       .def_readwrite("slice_rows", &BatchView::slice_rows)
       .def_readwrite("col_stride", &BatchView::col_stride);
+
+  py::class_<RcclComm>(m, "RcclComm")
+      .def_static("unique_id",
+                  []() {
+                    auto v = RcclComm::unique_id();
+                    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+                  })
+      .def(py::init([](py::bytes id, int world, int rank, int device) {
+             std::string s = id;
+             std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;  // blocks until every rank joined
+             return new RcclComm(v, world, rank, device);
+           }),
+           py::arg("id"), py::arg("world"), py::arg("rank"), py::arg("device"))
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def("alltoallv",
+           [](RcclComm& c, uintptr_t send, std::vector<int64_t> sc, uintptr_t recv,
+              std::vector<int64_t> rc, int elem_bytes, uintptr_t stream) {
+             c.alltoallv(P<const void>(send), sc, P<void>(recv), rc, elem_bytes, stream);
+           })
+      .def("alltoall",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, int64_t count, int elem_bytes,
+              uintptr_t stream) { c.alltoall(P<const void>(send), P<void>(recv), count,
+                                             elem_bytes, stream); })
+      .def("abort", &RcclComm::abort);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,

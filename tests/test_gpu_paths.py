@@ -26,8 +26,9 @@ def nccl_group(gpu_device):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,slices", [("lr", 1), ("lr", 4), ("fm", 2)])
-def test_rccl_sharded_step_equals_fused(gpu_device, nccl_group, kind, slices):
+@pytest.mark.parametrize("kind,slices,transport", [("lr", 1, "rccl"), ("lr", 4, "rccl"),
+                                                   ("fm", 2, "rccl"), ("lr", 4, "torch")])
+def test_rccl_sharded_step_equals_fused(gpu_device, nccl_group, kind, slices, transport):
     from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
     def mk():
@@ -36,7 +37,8 @@ def test_rccl_sharded_step_equals_fused(gpu_device, nccl_group, kind, slices):
                                    max_slices=slices), device=gpu_device)
 
     a, b = mk(), mk()
-    sh = ShardedEngine(a)
+    sh = ShardedEngine(a, transport=transport)
+    assert sh.transport == transport
     keys = []
     for step in range(4):
         k, rp, fg, lab = random_csr(512, 8, 300, seed=step)

@@ -30,6 +30,9 @@ order -- a deterministic serialisation of the reference's arrival-order pushes.
 """
 from __future__ import annotations
 
+import math
+import os
+import time
 from typing import Callable, Optional
 
 import torch
@@ -56,12 +59,14 @@ class ShardedEngine:
     """Runs Engine phases with sparse all-to-alls between them."""
 
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
-                 world: Optional[int] = None, rank: Optional[int] = None):
+                 world: Optional[int] = None, rank: Optional[int] = None,
+                 transport: str = "auto"):
         """world/rank default to the process group's; passing them (with _a2a
         overridden) runs the step over another transport, e.g. in-process
-        ranks in tests."""
+        ranks in tests.  transport: see _init_transport."""
         self.engine = engine
         self.group = group
+        custom = world is not None or rank is not None
         self.world = int(world) if world is not None else dist.get_world_size(group)
         self.rank = int(rank) if rank is not None else dist.get_rank(group)
         dev = engine.device
@@ -80,9 +85,75 @@ class ShardedEngine:
         self.bytes_moved = 0
         self._counts_host = None
         self._counts_ready = None
+        self._comm = None
+        self.transport = "custom"
+        if not custom:
+            self._init_transport(transport)
+
+    # ---- transport ----------------------------------------------------------
+    def _init_transport(self, transport: str) -> None:
+        """"rccl": the native communicator (csrc/comm/rccl_comm.h) on the
+        engine's stream; "torch": torch.distributed all_to_all_single on the
+        process group's stream; "auto": rccl on a GPU unless XFLOW_A2A=torch.
+        The native one is verified with a bounded self-test exchange on every
+        rank and the job falls back to "torch" together if any rank fails."""
+        self._comm = None
+        if transport == "auto":
+            transport = os.environ.get("XFLOW_A2A", "rccl" if self.engine.is_gpu else "torch")
+        if transport == "torch" or not self.engine.is_gpu or self.group is not None:
+            self.transport = "torch"
+            return
+        from xflow_amd import native
+
+        n = native.load()
+        ok = 1
+        comm = None
+        try:
+            obj = [n.RcclComm.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = n.RcclComm(obj[0], self.world, self.rank, self.engine.device.index)
+            ok = int(self._selftest(comm))
+        except Exception as e:  # pragma: no cover - reported, then fall back
+            print(f"[xflow] rank {self.rank}: native RCCL transport unavailable: {e}", flush=True)
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=self.engine.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 1:
+            self._comm = comm
+            self.transport = "rccl"
+        else:
+            if comm is not None:
+                comm.abort()
+            self.transport = "torch"
+
+    def _selftest(self, comm, timeout_s: float = 60.0) -> bool:
+        W = self.world
+        dev = self.engine.device
+        send = torch.full((W,), self.rank, dtype=torch.int64, device=dev)
+        recv = torch.full((W,), -1, dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        comm.alltoall(send.data_ptr(), recv.data_ptr(), 1, 8, stream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        t0 = time.monotonic()
+        while not ev.query():
+            if time.monotonic() - t0 > timeout_s:
+                return False
+            time.sleep(0.001)
+        return recv.cpu().tolist() == list(range(W))
 
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        if self._comm is None:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            return
+        row = math.prod(inp.shape[1:]) * inp.element_size()  # bytes per split unit
+        stream = torch.cuda.current_stream(self.engine.device).cuda_stream
+        if out_splits is None:
+            self._comm.alltoall(inp.data_ptr(), out.data_ptr(), inp.shape[0] // self.world, row,
+                                stream)
+        else:
+            self._comm.alltoallv(inp.data_ptr(), [int(x) for x in in_splits], out.data_ptr(),
+                                 [int(x) for x in out_splits], row, stream)
 
     def _exchange_keys(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
         """Dedup + bucket + key all-to-all.  Returns (send, recv splits, recv keys).
