@@ -82,14 +82,19 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   be.memset(grad_, 0, sizeof(float) * scratch_.cap * cfg_.max_slices * ps);
   tmask_ = balloc<u32>(be, scratch_.cap);
   be.memset(tmask_, 0, sizeof(u32) * scratch_.cap);
-  if (be.is_gpu() && cfg_.model.kind == kLR) {
+  // atomic-free gradient reduction (FwdArgs::red_*): LR (1 value per key) and
+  // reference-math FM (2 values per key, 16-byte records)
+  const bool fm_ref = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference;
+  if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref)) {
+    const int nv = fm_ref ? 2 : 1, shift = red_shift(nv);
+    const int group_rows = fm_ref ? kFmGroupRows : kLrGroupRows;
     const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
-    const int nb = (int)((dests + (1ull << kRedShift) - 1) >> kRedShift);
+    const int nb = (int)((dests + (1ull << shift) - 1) >> shift);
     if (nb <= kRedMaxBuckets) {
-      const int64_t groups = (cfg_.max_rows + kLrGroupRows - 1) / kLrGroupRows;
+      const int64_t groups = (cfg_.max_rows + group_rows - 1) / group_rows;
       red_nb_ = nb;
-      red_pairs_ = balloc<u64>(be, nnz);
-      red_sorted_ = balloc<u64>(be, nnz);
+      red_pairs_ = balloc<u64>(be, (size_t)nnz * nv);  // nv u64 words per record
+      red_sorted_ = balloc<u64>(be, (size_t)nnz * nv);
       red_hist_ = balloc<u32>(be, (size_t)nb * groups);
       red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
       red_count_ = balloc<u32>(be, groups);

@@ -149,11 +149,15 @@ struct ColumnAgg {
 // (dest, value) pair region fills column after column without a cursor
 // atomic -- and counts them in the LDS histogram of dest >> kRedShift that
 // drives the reduction kernels below.
-template <int LOG2>
+// NV = values aggregated per key: 1 (LR: Σ loss) or 2 (reference-math FM:
+// Σ loss and Σ loss*vsum, expanded to the 1+D gradient in k_red_sum).
+// Records: NV == 1 -> u64 (dest | value << 32), NV == 2 -> uint4 (dest, v0, v1, 0).
+template <int LOG2, int NV = 1>
 struct ListAgg {
   static constexpr int kSlots = 1 << LOG2;
+  static constexpr int kShift = red_shift(NV);
   u64 (*tag)[kSlots];
-  float (*acc)[kSlots];
+  float (*acc)[kSlots * NV];
   unsigned short (*list)[kSlots / 2];
   u32* nlist;   // [3] list lengths, rotating over columns
   u32* hist;    // [red_nb]
@@ -163,7 +167,8 @@ struct ListAgg {
   __device__ __forceinline__ void init(int nb) {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
       tag[0][i] = tag[1][i] = ~0ull;
-      acc[0][i] = acc[1][i] = 0.0f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[0][i * NV + v] = acc[1][i * NV + v] = 0.0f;
     }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0u;
     if (threadIdx.x < 3) nlist[threadIdx.x] = 0u;
@@ -189,14 +194,16 @@ struct ListAgg {
     }
   }
   // called by every lane of the workgroup (wave-uniform control flow)
-  __device__ __forceinline__ void column(int j, bool has, u32 dest, float loss) {
+  __device__ __forceinline__ void column(int j, bool has, u32 dest, float loss,
+                                         float loss2 = 0.0f) {
     const int t = j & 1;
     if (threadIdx.x == 0) nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
     bool claimed = false;
     int h = 0;
     if (has) {
       h = insert(t, j, dest, claimed);
-      atomicAdd(&acc[t][h], loss);
+      atomicAdd(&acc[t][h * NV], loss);
+      if constexpr (NV > 1) atomicAdd(&acc[t][h * NV + 1], loss2);
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -212,10 +219,17 @@ struct ListAgg {
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
       const int hh = list[t][i];
       const u32 d = (u32)tag[t][hh];
-      const float v = acc[t][hh];
-      acc[t][hh] = 0.0f;
-      region[written + i] = (u64)d | ((u64)__float_as_uint(v) << 32);
-      atomicAdd(&hist[d >> kRedShift], 1u);
+      const float v = acc[t][hh * NV];
+      acc[t][hh * NV] = 0.0f;
+      if constexpr (NV == 1) {
+        region[written + i] = (u64)d | ((u64)__float_as_uint(v) << 32);
+      } else {
+        const float v2 = acc[t][hh * NV + 1];
+        acc[t][hh * NV + 1] = 0.0f;
+        reinterpret_cast<uint4*>(region)[written + i] =
+            make_uint4(d, __float_as_uint(v), __float_as_uint(v2), 0u);
+      }
+      atomicAdd(&hist[d >> kShift], 1u);
     }
     written += n;
   }
@@ -587,13 +601,28 @@ __global__ void __launch_bounds__(kBlock) k_red_scan(u32* __restrict__ hist, int
 constexpr int kRedBlock = 1024;
 constexpr int kRedUnroll = 4;
 
+// record of one (dest, NV values) partial sum
+template <int NV> struct RedRec;
+template <> struct RedRec<1> {
+  using T = u64;
+  __device__ static u32 dest(T r) { return (u32)r; }
+};
+template <> struct RedRec<2> {
+  using T = uint4;
+  __device__ static u32 dest(T r) { return r.x; }
+};
+
+template <int NV>
 __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows_per_group,
-                                                           const u64* __restrict__ pairs,
+                                                           const void* __restrict__ pairs,
                                                            const u32* __restrict__ count,
                                                            const u32* __restrict__ hist,
                                                            const u32* __restrict__ tot,
                                                            u32* __restrict__ start, int nb,
-                                                           u64* __restrict__ sorted) {
+                                                           void* __restrict__ sorted) {
+  using R = RedRec<NV>;
+  using T = typename R::T;
+  constexpr int kShift = red_shift(NV);
   __shared__ u32 cur[kRedMaxBuckets];
   const int g = blockIdx.x, groups = gridDim.x;
   u32 carry = 0;
@@ -611,65 +640,210 @@ __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows
   if (g == 0 && threadIdx.x == 0) start[nb] = carry;
   __syncthreads();
   const int64_t r0 = (int64_t)g * rows_per_group;
-  const u64* src = pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
+  const T* src = static_cast<const T*>(pairs) +
+                 (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
+  T* dst = static_cast<T*>(sorted);
   const u32 n = count[g];
   // kRedUnroll independent load -> LDS rank -> store chains per lane
   for (u32 i0 = threadIdx.x; i0 < n; i0 += kRedUnroll * kRedBlock) {
-    u64 pr[kRedUnroll];
+    T pr[kRedUnroll];
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q) {
       const u32 i = i0 + (u32)q * kRedBlock;
-      pr[q] = i < n ? src[i] : 0ull;
+      if (i < n) pr[q] = src[i];
     }
     u32 p[kRedUnroll];
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q)
-      if (i0 + (u32)q * kRedBlock < n) p[q] = atomicAdd(&cur[(u32)pr[q] >> kRedShift], 1u);
+      if (i0 + (u32)q * kRedBlock < n) p[q] = atomicAdd(&cur[R::dest(pr[q]) >> kShift], 1u);
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q)
-      if (i0 + (u32)q * kRedBlock < n) sorted[p[q]] = pr[q];
+      if (i0 + (u32)q * kRedBlock < n) dst[p[q]] = pr[q];
   }
 }
 
-__global__ void __launch_bounds__(kRedBlock) k_red_sum(const u64* __restrict__ sorted,
-                                                       const u32* __restrict__ start,
-                                                       float* __restrict__ grad) {
-  constexpr u32 kR = 1u << kRedShift;
-  __shared__ float acc[kR];
+// Final gradient rows.  NV == 1: grad[dest] = Σ (LR).  NV == 2: reference-math
+// FM (fm_worker.cc:126-157), per (key, slice) dest = slot*S + s with B = Σ loss
+// and C = Σ loss*vsum: g_w = D*B, g_v[k] = Σ loss*(vsum - v_k) = C - v_k*B.
+struct RedFinal {
+  float* grad;
+  const float* wpull;  // [slot][ps] pulled rows (NV == 2)
+  int S, ps, D;
+};
+
+template <int NV>
+__global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ sorted,
+                                                       const u32* __restrict__ start, RedFinal f) {
+  using T = typename RedRec<NV>::T;
+  constexpr int kShift = red_shift(NV);
+  constexpr u32 kR = 1u << kShift;
+  __shared__ float acc[kR * NV];
   const u32 beg = start[blockIdx.x], end = start[blockIdx.x + 1];
   if (beg == end) return;
-  for (u32 i = threadIdx.x; i < kR; i += kRedBlock) acc[i] = 0.0f;
+  for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0.0f;
   __syncthreads();
+  const T* src = static_cast<const T*>(sorted);
   for (u32 i0 = beg + threadIdx.x; i0 < end; i0 += kRedUnroll * kRedBlock) {
-    u64 pr[kRedUnroll];
+    T pr[kRedUnroll];
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q) {
       const u32 i = i0 + (u32)q * kRedBlock;
-      pr[q] = i < end ? sorted[i] : 0ull;
+      if (i < end) pr[q] = src[i];
     }
 #pragma unroll
-    for (int q = 0; q < kRedUnroll; ++q)
-      if (i0 + (u32)q * kRedBlock < end)
+    for (int q = 0; q < kRedUnroll; ++q) {
+      if (i0 + (u32)q * kRedBlock >= end) continue;
+      if constexpr (NV == 1) {
         atomicAdd(&acc[(u32)pr[q] & (kR - 1)], __uint_as_float((u32)(pr[q] >> 32)));
+      } else {
+        const u32 l = pr[q].x & (kR - 1);
+        atomicAdd(&acc[l * 2], __uint_as_float(pr[q].y));
+        atomicAdd(&acc[l * 2 + 1], __uint_as_float(pr[q].z));
+      }
+    }
   }
   __syncthreads();
-  float* g = grad + ((size_t)blockIdx.x << kRedShift);
-  for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-    const float v = acc[i];
-    if (v != 0.0f) g[i] = v;  // grad is zero outside this step's keys
+  const u64 d0 = (u64)blockIdx.x << kShift;
+  if constexpr (NV == 1) {
+    float* g = f.grad + d0;
+    for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
+      const float v = acc[i];
+      if (v != 0.0f) g[i] = v;  // grad is zero outside this step's keys
+    }
+  } else {
+    for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
+      const float B = acc[2 * i], C = acc[2 * i + 1];
+      if (B == 0.0f && C == 0.0f) continue;
+      const u64 dest = d0 + i;
+      const float* v = f.wpull + (dest / (u64)f.S) * f.ps + 1;
+      float* g = f.grad + dest * f.ps;
+      g[0] = (float)f.D * B;
+      for (int k = 0; k < f.D; ++k) g[1 + k] = C - v[k] * B;
+    }
   }
+}
+
+template <int NV>
+static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, hipStream_t st) {
+  hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
+                     a.red_tot);
+  u32* start = a.red_tot + a.red_nb + 1;
+  hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
+                     rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
+                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
+  RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim};
+  hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb), dim3(kRedBlock), 0, st,
+                     static_cast<const void*>(a.red_sorted), start, f);
+}
+
+// Reference-math FM on the atomic-free reduction path.  The gradient of key i
+// in row r is loss_r*D for w and loss_r*(vsum_r - v_ik) for v (fm_worker.cc:
+// 126-157), so per (key, slice) only B = Σ loss and C = Σ loss*vsum need
+// summing -- two LDS atomics per occurrence instead of 1+D -- and k_red_sum
+// expands them with the pulled v: g_w = D*B, g_v[k] = C - v_k*B.
+template <int D, int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
+  constexpr int PS = fm_ps(D);
+  constexpr int LOG2 = ilog2c(2 * BLOCK);
+  __shared__ u64 s_tag64[2][1 << LOG2];
+  __shared__ float s_acc[2][(1 << LOG2) * 2];
+  __shared__ unsigned short s_list[2][BLOCK];
+  __shared__ u32 s_hist[kRedMaxBuckets];
+  __shared__ u32 s_nlist[3];
+  __shared__ int s_wmax[BLOCK / kWave];
+  const BatchView& b = a.batch;
+  const u32* __restrict__ pos = a.pos;
+  const float4* __restrict__ wp4 = reinterpret_cast<const float4*>(a.wpull);
+  const int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool active = r < b.rows;
+  RowSpan rs;
+  if (active) rs = row_span(b, r);
+  const int len = rs.len;
+  const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
+  u64* region = reinterpret_cast<u64*>(reinterpret_cast<uint4*>(a.red_pairs) +
+                                       (b.row_ptr ? (int64_t)b.row_ptr[r0]
+                                                  : r0 * b.nnz_per_row));
+  ListAgg<LOG2, 2> lagg{s_tag64, s_acc, s_list, s_nlist, s_hist, region, 0u};
+  lagg.init(a.red_nb);
+  int maxlen;
+  if (!b.row_ptr) {
+    maxlen = b.nnz_per_row;
+    __syncthreads();
+  } else {
+    const int m = wave_max(len);
+    if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
+    __syncthreads();
+    maxlen = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
+  }
+  StatAcc st;
+  float loss = 0.0f, vsum = 0.0f;
+  if (active) {
+    float vs[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+    float wx = 0.0f, vp = 0.0f;
+    for (int j = 0; j < len; ++j) {
+      const float4* src = wp4 + (size_t)pos[rs.at(j)] * (PS / 4);
+      float w[PS];
+#pragma unroll
+      for (int q = 0; q < PS / 4; ++q) {
+        const float4 v4 = src[q];
+        w[4 * q] = v4.x;
+        w[4 * q + 1] = v4.y;
+        w[4 * q + 2] = v4.z;
+        w[4 * q + 3] = v4.w;
+      }
+      wx += w[0];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        vs[k] += w[1 + k];
+        vp += w[1 + k] * w[1 + k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) vsum += vs[k];
+    const float p = sigmoid_ref(wx + (vsum * vsum - vp));
+    const float lab = b.labels[r];
+    loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+  }
+  const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+  const u32 S = (u32)a.S;
+  const float lv = loss * vsum;
+  for (int j = 0; j < maxlen; ++j) {
+    const u32 dest = j < len ? pos[rs.at(j)] * S + s : 0u;
+    lagg.column(j, j < len, dest, loss, lv);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
+  for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+    a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
+  flush_stats<BLOCK>(st, a.stats);
 }
 
 template <bool kGrad>
 static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
+  const bool red = agg && a.model.fm_math == kFmReference && a.red_pairs && a.red_nb > 0 &&
+                   a.red_nb <= kRedMaxBuckets;
   switch (a.model.v_dim) {
 #define XF_FM_CASE(DD)                                                                   \
   case DD: {                                                                             \
     constexpr int B = fm_block(DD);                                                      \
     int g = (int)((a.batch.rows + B - 1) / B);                                           \
-    if (agg) hipLaunchKernelGGL((k_fm<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);    \
-    else hipLaunchKernelGGL((k_fm<DD, kGrad, false>), dim3(g), dim3(B), 0, st, a);       \
+    if (red) {                                                                           \
+      constexpr int R = kFmGroupRows;                                                    \
+      const int gr = (int)((a.batch.rows + R - 1) / R);                                  \
+      hipLaunchKernelGGL((k_fm_red<DD, R>), dim3(gr), dim3(R), 0, st, a);                \
+      launch_reduction<2>(a, gr, R, st);                                                 \
+    } else if (agg) {                                                                    \
+      hipLaunchKernelGGL((k_fm<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);           \
+    } else {                                                                             \
+      hipLaunchKernelGGL((k_fm<DD, kGrad, false>), dim3(g), dim3(B), 0, st, a);          \
+    }                                                                                    \
     break;                                                                               \
   }
     XF_FM_CASE(1) XF_FM_CASE(2) XF_FM_CASE(4) XF_FM_CASE(8) XF_FM_CASE(10) XF_FM_CASE(16)
@@ -709,14 +883,7 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
         constexpr int R = kLrGroupRows;
         const int gr = (int)((a.batch.rows + R - 1) / R);
         hipLaunchKernelGGL((k_lr<true, true, R, true>), dim3(gr), dim3(R), 0, st, a);
-        hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, gr,
-                           a.red_tot);
-        u32* start = a.red_tot + a.red_nb + 1;
-        hipLaunchKernelGGL(k_red_scatter, dim3(gr), dim3(kRedBlock), 0, st, a.batch, R,
-                           a.red_pairs, a.red_count, a.red_hist, a.red_tot, start, a.red_nb,
-                           a.red_sorted);
-        hipLaunchKernelGGL(k_red_sum, dim3(a.red_nb), dim3(kRedBlock), 0, st, a.red_sorted, start,
-                           a.grad);
+        launch_reduction<1>(a, gr, R, st);
       } else if (grad && a.agg_ok)
         hipLaunchKernelGGL((k_lr<true, true, kLrBlock>), dim3(g), dim3(kLrBlock), 0, st, a);
       else if (grad)

@@ -95,7 +95,10 @@ struct FwdArgs {
 };
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
+// destinations per bucket for NV aggregated values per key (NV x 2^shift x 4 B <= 64 KB)
+constexpr int red_shift(int nv) { return nv == 1 ? kRedShift : kRedShift - 1; }
 constexpr int kLrGroupRows = 1024;  // rows per LR workgroup on the reduction path
+constexpr int kFmGroupRows = 512;   // rows per reference-FM workgroup on the reduction path
 
 struct PullArgs {
   TableView table;
