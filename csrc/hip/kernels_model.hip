@@ -506,70 +506,6 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
   flush_stats<BLOCK>(st, a.stats);
 }
 
-// ---------------------------------------------------------------------------
-// MVM: per-row field buckets in LDS, laid out [field][lane] (conflict-free).
-// ---------------------------------------------------------------------------
-constexpr int kMvmBlock = 64;
-constexpr int kMvmMaxFields = 128;
-
-template <int D, bool kGrad>
-__global__ void __launch_bounds__(kMvmBlock) k_mvm(FwdArgs a) {
-  __shared__ float S[kMvmMaxFields + 1][kMvmBlock];
-  const BatchView& b = a.batch;
-  const int ps = a.model.pstride();
-  const bool compat = a.model.mvm_math == kMvmCompat;
-  const int t = threadIdx.x;
-  int64_t r = (int64_t)blockIdx.x * blockDim.x + t;
-  StatAcc st;
-  if (r < b.rows) {
-    const RowSpan rs = row_span(b, r);
-    int maxf = 0;
-    for (int j = 0; j < rs.len; ++j) maxf = max(maxf, (int)b.fgid[rs.at(j)]);
-    maxf = min(maxf, kMvmMaxFields);
-    const int G = compat ? maxf : maxf + 1;
-    float M[D];
-    float y = 0.0f;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      for (int g = 0; g <= maxf; ++g) S[g][t] = 0.0f;
-      for (int j = 0; j < rs.len; ++j) {
-        const int64_t o = rs.at(j);
-        int f = b.fgid[o];
-        if (f <= kMvmMaxFields) S[f][t] += a.wpull[(size_t)a.pos[o] * ps + k];
-      }
-      float m = 1.0f;
-      for (int g = 0; g < G; ++g) m *= S[g][t];
-      M[k] = m;
-      y += m;
-    }
-    float p = sigmoid_ref(y);
-    float lab = b.labels[r];
-    float loss = p - lab;
-    if (a.pctr) a.pctr[r] = p;
-    st.add(p, lab);
-    if (kGrad) {
-      const int s = slice_of(b, r, a.S);
-#pragma unroll
-      for (int k = 0; k < D; ++k) {
-        for (int g = 0; g <= maxf; ++g) S[g][t] = 0.0f;
-        for (int j = 0; j < rs.len; ++j) {
-        const int64_t o = rs.at(j);
-          int f = b.fgid[o];
-          if (f <= kMvmMaxFields) S[f][t] += a.wpull[(size_t)a.pos[o] * ps + k];
-        }
-        for (int j = 0; j < rs.len; ++j) {
-        const int64_t o = rs.at(j);
-          int f = b.fgid[o];
-          float sg = (f <= kMvmMaxFields) ? S[f][t] : 0.0f;
-          float gr = (sg == 0.0f) ? 0.0f
-                                  : (float)((double)loss * ((double)M[k] / (1.0 + (double)sg)));
-          atomicAdd(&a.grad[((size_t)a.pos[o] * a.S + s) * ps + k], gr);
-        }
-      }
-    }
-  }
-  flush_stats<kMvmBlock>(st, a.stats);
-}
 
 // ---------------------------------------------------------------------------
 // LR gradient reduction without global atomics (FwdArgs::red_*).
@@ -854,12 +790,202 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// MVM, one lane per row with register-resident latent sums.  Each occurrence's
+// pulled row [v_0..v_{D-1}, pad] is read with dwordx4 loads once per pass; the
+// per-field sums S[g][k] are the occurrence's own v when every field occurs at
+// most once in the row (CTR rows; checked per row with a 64-bit field mask),
+// otherwise they are summed over the row's occurrences of that field.  The
+// backward aggregates each occurrence's D-vector per (key, slice) in the LDS
+// column tables (vector flush) instead of D global atomics per occurrence.
+// Reference math: mvm_worker.cc:137-218 (product over fields [0, G), G = maxf
+// (compat) or maxf + 1 (fixed); gradient loss*M_k/(1+S) when S != 0).
+constexpr int mvm_ps(int D) { return D == 1 ? 1 : (D + 3) & ~3; }
+constexpr int mvm_block(int D) { return mvm_ps(D) <= 12 ? 256 : (mvm_ps(D) <= 20 ? 128 : 64); }
+
+template <int PS>
+__device__ __forceinline__ void load_row(const float* __restrict__ wp, u32 p, float (&w)[PS]) {
+  if constexpr (PS % 4 == 0) {
+    const float4* src = reinterpret_cast<const float4*>(wp) + (size_t)p * (PS / 4);
+#pragma unroll
+    for (int q = 0; q < PS / 4; ++q) {
+      const float4 v4 = src[q];
+      w[4 * q] = v4.x;
+      w[4 * q + 1] = v4.y;
+      w[4 * q + 2] = v4.z;
+      w[4 * q + 3] = v4.w;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < PS; ++c) w[c] = wp[(size_t)p * PS + c];
+  }
+}
+
+template <int D, bool kGrad, bool kAgg>
+__global__ void __launch_bounds__(mvm_block(D)) k_mvm2(FwdArgs a) {
+  constexpr int PS = mvm_ps(D);
+  constexpr int BLOCK = mvm_block(D);
+  constexpr int LOG2 = ilog2c(2 * BLOCK);
+  __shared__ u32 s_tag[kAgg ? 2 : 1][kAgg ? (1 << LOG2) : 1];
+  __shared__ float s_acc[kAgg ? 2 : 1][kAgg ? (1 << LOG2) * PS : 1];
+  __shared__ int s_wmax[BLOCK / kWave];
+  const BatchView& b = a.batch;
+  const bool compat = a.model.mvm_math == kMvmCompat;
+  const u32* __restrict__ pos = a.pos;
+  const float* __restrict__ wp = a.wpull;
+  const int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool active = r < b.rows;
+  RowSpan rs;
+  if (active) rs = row_span(b, r);
+  const int len = rs.len;
+  // fields of the row: mask of those < 64, duplicate / out-of-mask flags
+  unsigned long long mask = 0ull;
+  bool dup = false, sorted = true;
+  int maxf = 0;
+  for (int j = 0; j < len; ++j) {
+    const int f = b.fgid[rs.at(j)];
+    if (j > 0 && f <= maxf) sorted = false;
+    maxf = max(maxf, f);
+    if (f < 0 || f >= 64) {
+      dup = true;
+    } else {
+      if ((mask >> f) & 1ull) dup = true;
+      mask |= 1ull << f;
+    }
+  }
+  const int G = compat ? maxf : maxf + 1;
+  // sum of the row's latent rows of field f, component-wise (slow path)
+  auto field_sum = [&](int f, float (&S)[D]) {
+#pragma unroll
+    for (int k = 0; k < D; ++k) S[k] = 0.0f;
+    for (int j = 0; j < len; ++j) {
+      if (b.fgid[rs.at(j)] != f) continue;
+      float w[PS];
+      load_row<PS>(wp, pos[rs.at(j)], w);
+#pragma unroll
+      for (int k = 0; k < D; ++k) S[k] += w[k];
+    }
+  };
+  float M[D];
+  float y = 0.0f;
+  StatAcc st;
+  float loss = 0.0f;
+  if (active) {
+    bool complete;  // every field g < G occurs (else some S[g] = 0 and M = 0)
+    if (dup || G > 64) {
+      complete = true;
+      for (int g = 0; g < G && complete; ++g) {
+        bool found = false;
+        for (int j = 0; j < len && !found; ++j) found = b.fgid[rs.at(j)] == g;
+        complete = found;
+      }
+    } else {
+      const unsigned long long need = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+      complete = (mask & need) == need;
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) M[k] = complete ? 1.0f : 0.0f;
+    if (complete) {
+      if (!dup && sorted) {
+        // occurrence order = field order g = 0..G-1 (the reference's product order)
+        for (int j = 0; j < len; ++j) {
+          if (b.fgid[rs.at(j)] >= G) break;
+          float w[PS];
+          load_row<PS>(wp, pos[rs.at(j)], w);
+#pragma unroll
+          for (int k = 0; k < D; ++k) M[k] *= w[k];
+        }
+      } else if (!dup) {
+        for (int g = 0; g < G; ++g) {
+          int jj = 0;
+          while (b.fgid[rs.at(jj)] != g) ++jj;
+          float w[PS];
+          load_row<PS>(wp, pos[rs.at(jj)], w);
+#pragma unroll
+          for (int k = 0; k < D; ++k) M[k] *= w[k];
+        }
+      } else {
+        for (int g = 0; g < G; ++g) {
+          float S[D];
+          field_sum(g, S);
+#pragma unroll
+          for (int k = 0; k < D; ++k) M[k] *= S[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) y += M[k];
+    const float p = sigmoid_ref(y);
+    const float lab = b.labels[r];
+    loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+  }
+  if constexpr (kGrad) {
+    const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+    const u32 S = (u32)a.S;
+    // gradient of the row's j-th occurrence
+    auto contrib = [&](int j, float (&c)[D]) {
+      float Sf[D];
+      if (!dup) {
+        float w[PS];
+        load_row<PS>(wp, pos[rs.at(j)], w);
+#pragma unroll
+        for (int k = 0; k < D; ++k) Sf[k] = w[k];
+      } else {
+        field_sum(b.fgid[rs.at(j)], Sf);
+      }
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        c[k] = (Sf[k] == 0.0f) ? 0.0f
+                               : (float)((double)loss * ((double)M[k] / (1.0 + (double)Sf[k])));
+    };
+    if constexpr (!kAgg) {
+      for (int j = 0; j < len; ++j) {
+        float c[D];
+        contrib(j, c);
+        float* g = a.grad + ((size_t)pos[rs.at(j)] * S + s) * PS;
+#pragma unroll
+        for (int k = 0; k < D; ++k) atomicAdd(&g[k], c[k]);
+      }
+    } else {
+      ColumnAgg<PS, LOG2> agg{s_tag, s_acc};
+      agg.init();
+      const int m = wave_max(len);
+      if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
+      __syncthreads();
+      int maxlen = 0;
+#pragma unroll
+      for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
+      for (int j = 0; j < maxlen; ++j) {
+        const int t = j & 1;
+        if (j < len) {
+          float c[D];
+          contrib(j, c);
+          const int h = agg.insert(t, pos[rs.at(j)] * S + s);
+#pragma unroll
+          for (int k = 0; k < D; ++k) agg.add(t, h, k, c[k]);
+        }
+        __syncthreads();
+        agg.flush(t, a.grad);
+      }
+    }
+  }
+  flush_stats<BLOCK>(st, a.stats);
+}
+
 template <bool kGrad>
 static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
-  int grid = (int)((a.batch.rows + kMvmBlock - 1) / kMvmBlock);
+  const bool agg = kGrad && a.agg_ok;
   switch (a.model.v_dim) {
-#define XF_MVM_CASE(DD) \
-  case DD: hipLaunchKernelGGL((k_mvm<DD, kGrad>), dim3(grid), dim3(kMvmBlock), 0, st, a); break;
+#define XF_MVM_CASE(DD)                                                                  \
+  case DD: {                                                                             \
+    constexpr int B = mvm_block(DD);                                                     \
+    const int g = (int)((a.batch.rows + B - 1) / B);                                     \
+    if (agg) hipLaunchKernelGGL((k_mvm2<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);  \
+    else hipLaunchKernelGGL((k_mvm2<DD, kGrad, false>), dim3(g), dim3(B), 0, st, a);     \
+    break;                                                                               \
+  }
     XF_MVM_CASE(1) XF_MVM_CASE(2) XF_MVM_CASE(4) XF_MVM_CASE(8) XF_MVM_CASE(10) XF_MVM_CASE(16)
     XF_MVM_CASE(32)
 #undef XF_MVM_CASE
