@@ -651,10 +651,19 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
       const float B = acc[2 * i], C = acc[2 * i + 1];
       if (B == 0.0f && C == 0.0f) continue;
       const u64 dest = d0 + i;
-      const float* v = f.wpull + (dest / (u64)f.S) * f.ps + 1;
-      float* g = f.grad + dest * f.ps;
-      g[0] = (float)f.D * B;
-      for (int k = 0; k < f.D; ++k) g[1 + k] = C - v[k] * B;
+      // rows are padded to 16 B: dwordx4 loads of v and stores of the row
+      const float4* v4 = reinterpret_cast<const float4*>(f.wpull + (dest / (u64)f.S) * f.ps);
+      float4* g4 = reinterpret_cast<float4*>(f.grad + dest * f.ps);
+      for (int q = 0; q < f.ps / 4; ++q) {
+        const float4 v = v4[q];
+        float o[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * q + e;  // component: 0 = w, 1..D = v, above = pad
+          o[e] = c == 0 ? (float)f.D * B : (c <= f.D ? C - o[e] * B : 0.0f);
+        }
+        g4[q] = make_float4(o[0], o[1], o[2], o[3]);
+      }
     }
   }
 }

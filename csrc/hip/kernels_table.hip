@@ -26,6 +26,8 @@ namespace xflow {
 namespace hip {
 
 constexpr u32 kNoSlot = 0xFFFFFFFFu;
+// grid cap of the lane-group pull/apply kernels (16 K workgroups of 256)
+constexpr int kGroupGridCap = 16384;
 
 // ---------------------------------------------------------------------------
 // dedup
@@ -566,7 +568,9 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot);
     if (a.out_vals) {
       const int G = group_for(a.pstride);
-      const int g2 = grid_for(nm * G);
+      // one key per lane group where possible: the grid-stride iterations of
+      // a group are dependent random-access chains (latency bound)
+      const int g2 = grid_for(nm * G, kBlock, kGroupGridCap);
       switch (G) {
         case 2: launch_pull_values<2>(a, g2, st); break;
         case 4: launch_pull_values<4>(a, g2, st); break;
@@ -731,7 +735,7 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   } else if (a.pstride >= 2 && a.pstride <= 64 && !a.reset_pos) {
     int64_t nm = a.n_dev ? a.n_max : a.n_host;
     const int G = group_for(a.pstride);
-    const int g2 = grid_for(nm * G);
+    const int g2 = grid_for(nm * G, kBlock, kGroupGridCap);
     switch (G) {
       case 2: launch_apply_group<2>(a, g2, st); break;
       case 4: launch_apply_group<4>(a, g2, st); break;
