@@ -172,6 +172,8 @@ def main():
             out["config"]["lambda1"] = a.lambda1
             out["nonzero_weights"] = int(nonzero)
         print(json.dumps(out), flush=True)
+    if sharded is not None and hasattr(sharded, "close"):
+        sharded.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

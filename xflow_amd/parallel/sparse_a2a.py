@@ -5,8 +5,10 @@ shard of the parameter table in its HBM (owner = fmix64(key) >> 32 mod world).
 One training step, per rank (reference call sites: lr_worker.cc:170/175,
 fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
 
-  1. w_prepare    dedup the batch's keys, bucket the unique keys by owner
-  2. a2a counts   (int64 x world), one host sync for the split sizes
+  1. w_prepare    dedup the batch's keys grouped by owner (owner-partitioned
+                  scratch on the GPU, a bucket pass on the CPU backend)
+  2. a2a counts   (int64 x world), one host sync for the split sizes (hidden
+                  behind the next batch's generation, see _exchange_keys)
   3. a2a keys     -> each owner receives the keys it serves
   4. s_pull       owner probes/inserts its shard, evaluates pull values
   5. a2a values   -> back to the requesting workers (send order)
@@ -16,9 +18,10 @@ fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
   8. s_apply      owner applies contributions source by source (fixed order:
                   deterministic, the analogue of ps-lite's serialized handler)
 
-Collectives go through torch.distributed: backend "nccl" is RCCL on ROCm
-(xGMI peer links between the node's GPUs), "gloo" runs the same code on CPU for
-tests.  Each all-to-all moves only the touched keys (8 B) and their P floats,
+On GPUs the all-to-alls go through the native RCCL communicator on the
+engine's stream (csrc/comm/rccl_comm.h; xGMI peer links between the node's
+GPUs); otherwise through torch.distributed ("gloo" runs the same code on CPU
+for tests).  Each all-to-all moves only the touched keys (8 B) and their P floats,
 so a step's traffic is ~K*(8+8P) bytes per rank, spread over all 7 xGMI links
 instead of a dense all-reduce of the table.
 
@@ -241,3 +244,9 @@ class ShardedEngine:
         pulled = self._pull(recv_keys, send_splits, recv_splits, insert=False)
         e.w_forward(batch, pulled, self.last_send, pctr if batch.rows else None)
         return pctr
+
+    def close(self) -> None:
+        """Release the native communicator (before the process group goes)."""
+        if self._comm is not None:
+            torch.cuda.synchronize(self.engine.device)
+            self._comm = None
