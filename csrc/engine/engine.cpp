@@ -501,6 +501,13 @@ int64_t Engine::table_size() {
   return (int64_t)n;
 }
 
+int64_t Engine::scratch_capacity() {
+  if (!scratch_.ctl) return (int64_t)scratch_.cap;
+  unsigned long long c[3] = {0, 0, 0};
+  be_->copy_d2h(c, scratch_.ctl, sizeof(c));
+  return (int64_t)(c[2] ? c[2] : c[0]);  // a pending rebuild applies before the next batch
+}
+
 bool Engine::overflowed() {
   u32 o[2] = {0, 0};
   be_->copy_d2h(o, overflow_, sizeof(o));

@@ -84,6 +84,7 @@ class Engine {
   LossStats read_stats(bool reset, int which = 0);
   int64_t n_unique();            // unique keys of the last prepared batch (syncs)
   int64_t table_size();          // occupied slots (syncs)
+  int64_t scratch_capacity();    // active dedup scratch capacity (adaptive on the GPU; syncs)
   uint64_t table_capacity() const { return table_.cap; }
   size_t table_bytes() const { return table_bytes_; }
   bool overflowed();

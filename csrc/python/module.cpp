@@ -234,6 +234,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("reset") = false, py::arg("which") = 0)
       .def("n_unique", &Engine::n_unique)
       .def("table_size", &Engine::table_size)
+      .def("scratch_capacity", &Engine::scratch_capacity)
       .def("overflowed", &Engine::overflowed)
       .def("nonzero_weights", &Engine::nonzero_weights)
       .def("export_table",

@@ -134,3 +134,32 @@ def test_ftrl_single_key_closed_form(devname):
             tmpr = np.float32(z - l1) if z > 0 else np.float32(z + l1)
             w = np.float32(tmpr / np.float32(-1.0 * np.float32(np.float32(b + np.sqrt(n)) / a + l2)))
         assert eng.pull([12345])[0, 0] == w
+
+
+@pytest.mark.gpu
+def test_adaptive_scratch_capacity_matches_cpu(gpu_device):
+    """The GPU dedup scratch shrinks to 8x the batch's unique keys, grows again
+    on a surge (device-side rebuilds), and training still equals the CPU
+    backend's (fixed-capacity scratch) step for step."""
+    rows, fields = 8192, 8
+    engines = [Engine(ModelConfig(kind="lr"), OptimConfig(),
+                      EngineConfig(table_log2_cap=20, max_rows=rows, max_nnz=rows * fields),
+                      device=d) for d in (torch.device("cpu"), gpu_device)]
+    caps = []
+    allk = []
+    for step in range(12):
+        vocab = 400 if step < 6 else 40000  # small batches, then a surge of new keys
+        k, rp, fg, lab = random_csr(rows, fields, vocab, seed=500 + step, variable=False)
+        allk.append(k)
+        for e in engines:
+            e.train_step(to_batch(k, rp, fg, lab, e.device))
+        caps.append(engines[1].scratch_capacity())
+    alloc = 1
+    while alloc < int(rows * fields * 2.5) + 1:
+        alloc <<= 1
+    assert min(caps[:6]) < alloc, caps          # shrank while batches were small
+    assert caps[-1] > min(caps[:6]), caps       # grew again for the surge
+    assert not engines[1].overflowed()
+    keys = np.unique(np.concatenate(allk))
+    np.testing.assert_allclose(engines[1].pull(keys), engines[0].pull(keys), rtol=1e-4,
+                               atol=1e-6)

@@ -245,6 +245,11 @@ class Engine:
         self._sync_stream()
         return int(self._e.n_unique())
 
+    def scratch_capacity(self) -> int:
+        """Active dedup scratch capacity (device-adaptive on the GPU)."""
+        self._sync_stream()
+        return int(self._e.scratch_capacity())
+
     def overflowed(self) -> bool:
         self._sync_stream()
         return bool(self._e.overflowed())

@@ -278,6 +278,8 @@ class Trainer:
     def close(self) -> None:
         if self.watchdog is not None:
             self.watchdog.stop()
+        if getattr(self, "sharded", None) is not None:
+            self.sharded.close()
         xdist.finalize()
 
 
