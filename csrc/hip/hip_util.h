@@ -20,6 +20,24 @@
     }                                                                             \
   } while (0)
 
+// Device-side bounds asserts, compiled in only by a debug build
+// (XFLOW_DEVICE_ASSERT=1 python -m xflow_amd._build): a failing check prints
+// the condition and traps the wave.  GPU sanitizers are not available on the
+// MI355X pool; these asserts plus AMD_SERIALIZE_KERNEL=3 localise a fault.
+#if defined(XFLOW_DEVICE_ASSERT) && XFLOW_DEVICE_ASSERT
+#define XF_DASSERT(cond)                                                           \
+  do {                                                                             \
+    if (!(cond)) {                                                                 \
+      printf("xflow device assert failed: %s at %s:%d\n", #cond, __FILE__, __LINE__); \
+      __builtin_trap();                                                            \
+    }                                                                              \
+  } while (0)
+#else
+#define XF_DASSERT(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace xflow {
 namespace hip {
 

@@ -229,6 +229,7 @@ struct ListAgg {
         reinterpret_cast<uint4*>(region)[written + i] =
             make_uint4(d, __float_as_uint(v), __float_as_uint(v2), 0u);
       }
+      XF_DASSERT((int)(d >> kShift) < kRedMaxBuckets);
       atomicAdd(&hist[d >> kShift], 1u);
     }
     written += n;
@@ -591,7 +592,10 @@ __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows
     u32 p[kRedUnroll];
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q)
-      if (i0 + (u32)q * kRedBlock < n) p[q] = atomicAdd(&cur[R::dest(pr[q]) >> kShift], 1u);
+      if (i0 + (u32)q * kRedBlock < n) {
+        XF_DASSERT((int)(R::dest(pr[q]) >> kShift) < nb);
+        p[q] = atomicAdd(&cur[R::dest(pr[q]) >> kShift], 1u);
+      }
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q)
       if (i0 + (u32)q * kRedBlock < n) dst[p[q]] = pr[q];

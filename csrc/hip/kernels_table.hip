@@ -168,6 +168,7 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
       }
       c = skeys[sj];
     }
+    XF_DASSERT(sj < cap);
     t_key[h[j]] = sj;
     sv.stamps[sj] = sv.epoch;
   }
@@ -302,7 +303,10 @@ __global__ void __launch_bounds__(kPartBlock) k_partition_counts(
     if (lane == 0) start[o] = (int64_t)offs[c] + hits;
   }
   __syncthreads();
-  for (u32 o = threadIdx.x; o < parts; o += kPartBlock) counts[o] = start[o + 1] - start[o];
+  for (u32 o = threadIdx.x; o < parts; o += kPartBlock) {
+    XF_DASSERT(start[o + 1] >= start[o]);
+    counts[o] = start[o + 1] - start[o];
+  }
 }
 
 void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
@@ -670,6 +674,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; i < n; i += stride) {
     const u32 slot = a.slots[i];
+    XF_DASSERT(slot == kNoSlot || slot < a.table.cap);
     const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
     float* g = a.grads + (size_t)row * S * ps;
     const u32 m = a.masks ? a.masks[row] : all;

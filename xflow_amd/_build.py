@@ -23,7 +23,10 @@ import sysconfig
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build")
-OBJ = os.path.join(BUILD, "obj")
+# XFLOW_DEVICE_ASSERT=1: debug build with device-side bounds asserts
+# (XF_DASSERT in csrc/hip/hip_util.h); objects go to their own directory
+DEVICE_ASSERT = os.environ.get("XFLOW_DEVICE_ASSERT", "0") not in ("", "0")
+OBJ = os.path.join(BUILD, "obj-dassert" if DEVICE_ASSERT else "obj")
 PKG = os.path.join(ROOT, "xflow_amd")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("XFLOW_OFFLOAD_ARCH", "gfx950")
@@ -36,7 +39,8 @@ COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
 # -ffp-contract=off: keep the device FTRL / loss math bit-identical to the CPU
 # backend and the reference (no silent FMA contraction).
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-ffp-contract=off", "-mcode-object-version=5",
-             "-I" + os.path.join(CSRC, "hip"), "-Wno-unused-result"]
+             "-I" + os.path.join(CSRC, "hip"), "-Wno-unused-result"] + \
+            (["-DXFLOW_DEVICE_ASSERT=1"] if DEVICE_ASSERT else [])
 
 HOST_SOURCES = ["io/reader.cpp", "cpu/cpu_backend.cpp", "engine/engine.cpp", "engine/trainer.cpp"]
 
