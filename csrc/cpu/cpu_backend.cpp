@@ -352,11 +352,12 @@ class CpuBackend final : public Backend {
       const u64 rs = synth_row_seed(a.seed, a.step, r);
       float logit = a.planted_bias;
       for (int f = 0; f < a.fields; ++f) {
-        u64 key = synth_key(rs, f, F[f], a.hash_space);
+        float w;
+        const u64 key = synth_sample(rs, f, F[f], a.hash_space, a.planted_scale, w);
         const int64_t o = a.col_stride > 0 ? f * a.col_stride + r : r * a.fields + f;
         a.keys[o] = key;
         if (a.fgid) a.fgid[o] = f;
-        logit += synth_planted_weight(key, a.planted_scale);
+        logit += w;
       }
       a.labels[r] = synth_label(rs, logit);
     }

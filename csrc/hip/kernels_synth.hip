@@ -12,42 +12,48 @@ struct SynthConsts {
   SynthField f[kSynthMaxFields];
 };
 
-// A workgroup owns kSynthRows rows.  Lanes walk the tile's (row, field)
-// elements in memory order, so key/fgid stores are coalesced; each element's
-// planted weight is parked in LDS and one lane per row sums them in field
-// order (deterministic, the same order as the CPU backend).
+// A workgroup owns kSynthRows rows.  The row seeds (two fmix64 rounds each, a
+// large share of an element's 64-bit multiplies if recomputed per element)
+// and the field constants are staged in LDS once.  Lanes then walk the tile's
+// (row, field) elements in memory order, so key/fgid stores are coalesced;
+// each element's planted weight is parked in LDS and one lane per row sums
+// them in field order (deterministic, the same order as the CPU backend).
 constexpr int kSynthRows = 64;
 
 __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
   __shared__ float pw[kSynthRows * kSynthMaxFields];
+  __shared__ u64 rseed[kSynthRows];
+  __shared__ SynthField fc[kSynthMaxFields];
   const int F = a.fields;
   const int64_t r0 = (int64_t)blockIdx.x * kSynthRows;
   const int rows = (int)min((int64_t)kSynthRows, a.rows - r0);
   const int n = rows * F;
   const bool field_major = a.col_stride > 0;
+  if ((int)threadIdx.x < rows)
+    rseed[threadIdx.x] = synth_row_seed_mixed(a.seed, synth_step_mix(a.step), r0 + threadIdx.x);
+  if ((int)threadIdx.x < F) fc[threadIdx.x] = c.f[threadIdx.x];
+  __syncthreads();
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
-    // field-major: consecutive lanes take consecutive rows of one field
     int rl, f;
-    if (field_major) {
-      f = e / rows;
+    if (field_major) {  // consecutive lanes take consecutive rows of one field
+      f = rows == kSynthRows ? e / kSynthRows : e / rows;
       rl = e - f * rows;
     } else {
       rl = e / F;
       f = e - rl * F;
     }
-    const int64_t r = r0 + rl;
-    const int64_t o = field_major ? (int64_t)f * a.col_stride + r : r0 * F + e;
-    const u64 key = synth_key(synth_row_seed(a.seed, a.step, r), f, c.f[f], a.hash_space);
+    float w;
+    const u64 key = synth_sample(rseed[rl], f, fc[f], a.hash_space, a.planted_scale, w);
+    const int64_t o = field_major ? (int64_t)f * a.col_stride + r0 + rl : r0 * F + e;
     a.keys[o] = key;
     if (a.fgid) a.fgid[o] = f;
-    pw[rl * F + f] = synth_planted_weight(key, a.planted_scale);
+    pw[rl * F + f] = w;
   }
   __syncthreads();
   if ((int)threadIdx.x < rows) {
-    const int64_t r = r0 + threadIdx.x;
     float logit = a.planted_bias;
     for (int f = 0; f < F; ++f) logit += pw[threadIdx.x * F + f];
-    a.labels[r] = synth_label(synth_row_seed(a.seed, a.step, r), logit);
+    a.labels[r0 + threadIdx.x] = synth_label(rseed[threadIdx.x], logit);
   }
 }
 

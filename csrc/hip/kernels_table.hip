@@ -598,6 +598,9 @@ __device__ __forceinline__ float norm_grad(float raw, const int32_t* slice_rows,
 }
 
 // LR-FTRL, one slice, 16-byte slots: read (n,z) as one dwordx2, write it back.
+// One key per lane, grid-stride: measured faster than issuing four keys per
+// lane up front (54 vs 49 us for 850 K keys) -- twice the waves in flight hide
+// the dependent slot -> state chain better than per-lane ILP.
 __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
   int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;

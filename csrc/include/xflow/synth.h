@@ -5,7 +5,16 @@
 // model's hashed feature space, and the label is drawn from a planted logistic
 // model over the same hashed keys so that logloss is meaningful.  Counter
 // based: (seed, step, row, field) fully determine a sample.
+//
+// The per-element math uses IEEE basic float operations only (no libm; both
+// builds compile without FMA contraction), so the host and gfx950 produce
+// bit-identical batches.  The inverse CDF x = (A*u + 1)^(1/e) is evaluated as
+// exp2(log2(A*u + 1) / e) with the short log2/exp2 below: ~40 VALU ops per
+// element instead of a double-precision pow, which made the generator
+// VALU-bound (PMC: ~356 VALU instructions per element).
 #pragma once
+
+#include <string.h>
 
 #include "xflow/common.h"
 
@@ -21,50 +30,111 @@ XF_HD u64 mulhi64(u64 a, u64 b) {
 #endif
 }
 
+XF_HD u32 synth_f2u(float f) {
+  u32 u;
+  memcpy(&u, &f, 4);
+  return u;
+}
+
+XF_HD float synth_u2f(u32 u) {
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
 XF_HD double synth_unit(u64 h) {  // (0,1)
   return ((double)(h >> 11) + 0.5) * (1.0 / 9007199254740992.0);
 }
 
-XF_HD float synth_planted_weight(u64 key, float scale) {
-  u64 h = fmix64(key ^ 0x6a09e667f3bcc909ull);
-  return scale * (float)(2.0 * synth_unit(h) - 1.0);
+XF_HD float synth_unit_f(u64 h) {  // (0,1), exact in float
+  return ((float)(u32)(h >> 41) + 0.5f) * (1.0f / 8388608.0f);
+}
+
+// log2(x) of a positive normal float: exponent + atanh series of the mantissa
+// reduced to [sqrt(1/2), sqrt(2)) (|t| <= 0.172, truncation error < 2e-8).
+XF_HD float synth_log2(float x) {
+  const u32 b = synth_f2u(x);
+  int e = (int)((b >> 23) & 0xFFu) - 127;
+  float m = synth_u2f((b & 0x7FFFFFu) | 0x3F800000u);  // [1, 2)
+  if (m > 1.41421356f) {
+    m = m * 0.5f;
+    e += 1;
+  }
+  const float t = (m - 1.0f) / (m + 1.0f);
+  const float t2 = t * t;
+  // 2/ln2 * (t + t^3/3 + t^5/5 + t^7/7 + t^9/9)
+  float p = 0.11111111f;
+  p = p * t2 + 0.14285714f;
+  p = p * t2 + 0.2f;
+  p = p * t2 + 0.33333333f;
+  p = p * t2 + 1.0f;
+  return (float)e + (p * t) * 2.88539008f;
+}
+
+// 2^y for y in [-126, 126]: the integer part goes into the exponent bits, 2^f
+// for f in [-0.5, 0.5] is a degree-6 Taylor polynomial (error < 2e-7).
+XF_HD float synth_exp2(float y) {
+  const float r = y + 0.5f;
+  int n = (int)r;
+  if ((float)n > r) n -= 1;  // floor
+  const float f = (y - (float)n) * 0.69314718f;
+  float p = 0.0013888889f;
+  p = p * f + 0.0083333333f;
+  p = p * f + 0.041666667f;
+  p = p * f + 0.16666667f;
+  p = p * f + 0.5f;
+  p = p * f + 1.0f;
+  p = p * f + 1.0f;
+  return synth_u2f(synth_f2u(p) + ((u32)n << 23));
+}
+
+XF_HD u64 synth_step_mix(u64 step) { return fmix64(step + 0x51ed27); }
+
+XF_HD u64 synth_row_seed_mixed(u64 seed, u64 step_mix, int64_t r) {
+  return fmix64(seed * 0x9e3779b97f4a7c15ull ^ step_mix ^ ((u64)r * 0xd1b54a32d192ed03ull));
 }
 
 XF_HD u64 synth_row_seed(u64 seed, u64 step, int64_t r) {
-  return fmix64(seed * 0x9e3779b97f4a7c15ull ^ fmix64(step + 0x51ed27) ^
-                ((u64)r * 0xd1b54a32d192ed03ull));
+  return synth_row_seed_mixed(seed, synth_step_mix(step), r);
 }
 
-// Per-field constants of the truncated power law, computed once per batch.
+// Per-field constants of the truncated power law, computed once per batch in
+// double on the host and rounded to float for the per-element recipe.
 struct SynthField {
   u64 vocab;
-  double A;      // (V+1)^(1-s) - 1
-  double inv_e;  // 1/(1-s)
-  double logv1;  // ln(V+1), for s == 1
+  float A;       // (V+1)^(1-s) - 1
+  float inv_e;   // 1/(1-s)
+  float log2v1;  // log2(V+1), for s == 1
   int unit_s;
 };
 
-XF_HD SynthField synth_field(u64 vocab, double s) {
+inline SynthField synth_field(u64 vocab, double s) {
   SynthField F;
   F.vocab = vocab ? vocab : 1;
-  double V = (double)F.vocab;
+  const double V = (double)F.vocab;
   F.unit_s = fabs(s - 1.0) < 1e-9;
-  F.logv1 = log(V + 1.0);
-  double e = 1.0 - s;
-  F.A = F.unit_s ? 0.0 : pow(V + 1.0, e) - 1.0;
-  F.inv_e = F.unit_s ? 0.0 : 1.0 / e;
+  F.log2v1 = (float)log2(V + 1.0);
+  const double e = 1.0 - s;
+  F.A = F.unit_s ? 0.0f : (float)(pow(V + 1.0, e) - 1.0);
+  F.inv_e = F.unit_s ? 0.0f : (float)(1.0 / e);
   return F;
 }
 
-XF_HD u64 synth_key(u64 rowseed, int f, const SynthField& F, u64 hash_space) {
-  u64 h = fmix64(rowseed + (u64)(f + 1) * 0x94d049bb133111ebull);
-  double u = synth_unit(h);
-  double x = F.unit_s ? exp(u * F.logv1) : pow(F.A * u + 1.0, F.inv_e);
-  u64 rank = (u64)x;
+// Key of field f for the row, and its planted weight.  Both come from one
+// hash of (field, rank): the key from its high bits (multiply-high into
+// [0, hash_space), no 64-bit division), the weight from its low bits, so
+// every occurrence of a key carries the same planted weight.
+XF_HD u64 synth_sample(u64 rowseed, int f, const SynthField& F, u64 hash_space, float scale,
+                       float& weight) {
+  const u64 h = fmix64(rowseed + (u64)(f + 1) * 0x94d049bb133111ebull);
+  const float u = synth_unit_f(h);
+  const float y = F.unit_s ? u * F.log2v1 : synth_log2(F.A * u + 1.0f) * F.inv_e;
+  u64 rank = (u64)synth_exp2(y);
   if (rank < 1) rank = 1;
   if (rank > F.vocab) rank = F.vocab;
-  // hash into [0, hash_space) by multiply-high (no 64-bit division)
-  return mulhi64(fmix64(((u64)(f + 1) << 40) ^ (rank - 1) ^ 0x3c6ef372fe94f82bull), hash_space);
+  const u64 hk = fmix64(((u64)(f + 1) << 40) ^ (rank - 1) ^ 0x3c6ef372fe94f82bull);
+  weight = scale * ((float)((u32)hk >> 8) * (2.0f / 16777216.0f) - 1.0f);
+  return mulhi64(hk, hash_space);
 }
 
 XF_HD float synth_label(u64 rowseed, float logit) {

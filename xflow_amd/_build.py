@@ -34,7 +34,7 @@ ARCH = os.environ.get("XFLOW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 CXX = os.environ.get("CXX", "g++")
 
-COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function",
+COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-ffp-contract=off",
                 "-I" + os.path.join(CSRC, "include"), "-I" + os.path.join(CSRC, "capi")]
 # -ffp-contract=off: keep the device FTRL / loss math bit-identical to the CPU
 # backend and the reference (no silent FMA contraction).
