@@ -1,13 +1,13 @@
 #!/bin/bash
 # A/B of bench.py variants on one GPU (each a separate process), then the
 # rocprofv3 kernel stats of the default configuration.
-#   VARIANTS="--no-overlap|--compute-priority normal|" TAG=x bash scripts/gpu_ab.sh
+#   VARIANTS="|--overlap on|--sharded" TAG=x bash scripts/gpu_ab.sh   (empty entry = defaults)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-ab}
 mkdir -p gpurun_out
-IFS='|' read -ra VS <<< "${VARIANTS:-|--no-overlap|--compute-priority normal|--sharded}"
+IFS="|" read -ra VS <<< "${VARIANTS-|--overlap on|--sharded}"
 for v in "${VS[@]}"; do
   timeout -k 10 300 python bench.py --steps 30 --warmup 5 $v > gpurun_out/ab_$TAG.log 2>&1 || { echo "bench [$v] failed"; tail -20 gpurun_out/ab_$TAG.log; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/ab_$TAG.log').read().strip().splitlines()[-1]); print('[$v]', round(d['value']/1e6,1), 'M samples/s', round(d['ms_per_step'],3), 'ms/step')"
