@@ -10,6 +10,12 @@ Layout of ``<dir>/``:
 Resume is world-size agnostic: with the same world size each rank loads its
 own shard; otherwise every rank scans all shards and imports exactly the keys
 it owns under the new hash sharding (owner = fmix64(key) >> 32 mod world).
+
+Periodic checkpoints (``--save-every``, the tracker's recovery) are versioned:
+``<root>/epoch-NNNNNN/`` holds one complete checkpoint in the layout above and
+``<root>/LATEST`` names the newest complete one.  LATEST is replaced
+atomically by rank 0 only after every rank has written its shard, so a job
+killed mid-save resumes from the previous version.
 """
 from __future__ import annotations
 
@@ -17,6 +23,7 @@ import dataclasses
 import glob
 import json
 import os
+import shutil
 import struct
 from typing import Optional
 
@@ -81,3 +88,31 @@ def load(engine, ckpt_dir: str, rank: int, world: int) -> dict:
         if mine.any():
             engine.import_table(keys[mine], words[mine].reshape(-1))
     return meta
+
+
+LATEST = "LATEST"
+
+
+def version_dir(root: str, epoch: int) -> str:
+    return os.path.join(root, "epoch-%06d" % epoch)
+
+
+def publish(root: str, epoch: int, keep: int = 2) -> None:
+    """Rank 0, after every rank saved the epoch's shards: point LATEST at the
+    version atomically and drop all but the newest ``keep`` versions."""
+    tmp = os.path.join(root, LATEST + ".tmp")
+    with open(tmp, "w") as f:
+        f.write(os.path.basename(version_dir(root, epoch)) + "\n")
+    os.replace(tmp, os.path.join(root, LATEST))
+    for d in sorted(glob.glob(os.path.join(root, "epoch-*")))[:-keep]:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def latest(root: str) -> Optional[str]:
+    """Directory of the newest complete versioned checkpoint under root, or None."""
+    p = os.path.join(root, LATEST)
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = os.path.join(root, f.read().strip())
+    return d if os.path.exists(os.path.join(d, "meta.json")) else None

@@ -55,6 +55,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--pred-dir", default=".")
     ap.add_argument("--save", default="", help="checkpoint directory to write after training")
     ap.add_argument("--load", default="", help="checkpoint directory to resume from")
+    ap.add_argument("--resume", default="",
+                    help="versioned checkpoint root: continue from its LATEST checkpoint if one "
+                         "exists (epochs = total for the run) and write periodic saves there")
+    ap.add_argument("--save-every", type=int, default=0,
+                    help="versioned checkpoint every N epochs under --resume (or --save) root")
     ap.add_argument("--metrics", default="", help="JSON-lines metrics file (rank 0)")
     ap.add_argument("--trace-dir", default="", help="torch.profiler chrome trace directory")
     return ap
@@ -68,6 +73,7 @@ def config_from_args(a) -> TrainConfig:
         test_block_bytes=a.test_block_bytes, serial_slices=a.serial_slices,
         keep_remainder=a.keep_remainder, mvm_predict_compat=a.mvm_predict_compat,
         init_push=not a.no_init_push, pred_dir=a.pred_dir, checkpoint_dir=a.save,
+        save_every=a.save_every, resume_dir=a.resume,
         metrics_file=a.metrics, async_p2p=a.async_p2p,
         model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math),
         optim=OptimConfig(kind=a.optimizer, alpha=a.alpha, beta=a.beta, lambda1=a.lambda1,
@@ -94,6 +100,8 @@ def main(argv=None) -> int:
     try:
         if a.load:
             t.load(a.load)
+        if a.resume:
+            t.resume(a.resume)
         with torch_profile(a.trace_dir):
             t.train()
         if a.save:

@@ -100,6 +100,8 @@ class TrainConfig:
     init_push: bool = True
     pred_dir: str = "."
     checkpoint_dir: str = ""
+    save_every: int = 0          # versioned checkpoint every N epochs (checkpoint.publish)
+    resume_dir: str = ""         # versioned checkpoint root: resume from LATEST, save there
     metrics_file: str = ""
     async_p2p: bool = False      # staleness-1 pipelined steps, pushes over RCCL point-to-point
     model: ModelConfig = field(default_factory=ModelConfig)

@@ -81,6 +81,7 @@ class Trainer:
         self.epoch = 0
         self.steps = 0
         self.samples = 0
+        self.resumed = False
         self._with_fgid = model_kind(cfg.model.kind) == 2
 
     # ------------------------------------------------------------------ data
@@ -186,8 +187,10 @@ class Trainer:
                 rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
                                                            self.device)[0])
             self.metrics.log(**rec)
-            if cfg.checkpoint_dir and os.environ.get("XFLOW_CKPT_EVERY_EPOCH"):
-                self.save(cfg.checkpoint_dir)
+            root = cfg.resume_dir or cfg.checkpoint_dir
+            every = cfg.save_every or (1 if os.environ.get("XFLOW_CKPT_EVERY_EPOCH") else 0)
+            if root and every and self.epoch % every == 0:
+                self.save_versioned(root)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 
@@ -250,9 +253,10 @@ class Trainer:
     def train(self) -> Optional[dict]:
         """The reference's Worker::train(): log rank, train, rank-0 predict."""
         _say("my rank is = %d" % self.rank)
-        if self.cfg.init_push:
+        if self.cfg.init_push and not self.resumed:
             self.init_push()
-        self.train_epochs(self.cfg.epochs)
+        # cfg.epochs counts the whole run: a resumed job trains the rest
+        self.train_epochs(max(0, self.cfg.epochs - self.epoch) if self.resumed else self.cfg.epochs)
         res = None
         if self.rank == 0:
             _say("LR AUC: " if model_kind(self.cfg.model.kind) == 0 else "FM AUC: ")
@@ -273,6 +277,26 @@ class Trainer:
         self.epoch = int(meta.get("epoch", 0))
         self.steps = int(meta.get("steps", 0))
         xdist.barrier()
+        return meta
+
+    def save_versioned(self, root: str) -> None:
+        """Periodic checkpoint: every rank writes its shard of this epoch's
+        version, then rank 0 publishes it as LATEST (checkpoint.publish)."""
+        self.save(checkpoint.version_dir(root, self.epoch))
+        if self.rank == 0:
+            checkpoint.publish(root, self.epoch)
+        xdist.barrier()
+
+    def resume(self, root: str) -> Optional[dict]:
+        """Continue from root's newest complete versioned checkpoint, if any
+        (the tracker's recovery path); later periodic saves go to root."""
+        self.cfg.resume_dir = root
+        d = checkpoint.latest(root)
+        if d is None:
+            return None
+        meta = self.load(d)
+        self.resumed = True
+        _say("resumed from %s at epoch %d" % (d, self.epoch))
         return meta
 
     def close(self) -> None:
