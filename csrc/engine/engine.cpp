@@ -503,9 +503,9 @@ int64_t Engine::table_size() {
 
 int64_t Engine::scratch_capacity() {
   if (!scratch_.ctl) return (int64_t)scratch_.cap;
-  unsigned long long c[3] = {0, 0, 0};
-  be_->copy_d2h(c, scratch_.ctl, sizeof(c));
-  return (int64_t)(c[2] ? c[2] : c[0]);  // a pending rebuild applies before the next batch
+  unsigned long long c = 0;
+  be_->copy_d2h(&c, scratch_.ctl, sizeof(c));
+  return (int64_t)c;  // ctl[0]: the capacity the next batch is deduplicated with
 }
 
 bool Engine::overflowed() {

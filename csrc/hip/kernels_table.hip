@@ -37,12 +37,19 @@ constexpr int kGroupGridCap = 16384;
 // hit.  CTR keys are extremely skewed (top-1000 keys ~60% of occurrences); a
 // table cleared every step made each hot key a same-address CAS storm.
 //
-// Step 0 -- device-side rebuild.  With ctl (adaptive capacity) the previous
-// batch's compaction scan decided whether to rebuild and at which capacity
-// (ctl[2]); otherwise the table is rebuilt once `claims` exceeds rebuild_at.
-// A rebuild frees the slots of the new capacity (grid-stride fill).
+// Device-side rebuilds.  With ctl (adaptive capacity, the HIP engine) the
+// compaction decides them: k_compact_scan switches the active capacity for
+// the next batch (ctl[0]) while keeping this batch's in ctl[3], and
+// k_compact_write frees the new capacity's slots right after reading its own
+// (each thread owns 16 slots) -- no extra launches per step.  Without ctl the
+// table is rebuilt by the two kernels below once `claims` exceeds rebuild_at.
 __device__ __forceinline__ u64 active_cap(const ScratchView& sv) {
   return sv.ctl ? (u64)sv.ctl[0] : sv.cap;
+}
+
+// capacity this batch was deduplicated with (valid after k_compact_scan)
+__device__ __forceinline__ u64 batch_cap(const ScratchView& sv) {
+  return sv.ctl ? (u64)sv.ctl[3] : sv.cap;
 }
 
 __global__ void k_scratch_maybe_clear(u64* __restrict__ skeys, u64 cap,
@@ -193,11 +200,11 @@ constexpr int kScanBlock = 1024;
 
 // 16 consecutive stamps as four dwordx4 loads (cap is a power of two >= 16,
 // so a 16-slot group is either fully inside the table or fully outside).
-__device__ __forceinline__ unsigned int compact_hits(const ScratchView& sv, u64 base,
+__device__ __forceinline__ unsigned int compact_hits(const ScratchView& sv, u64 base, u64 cap,
                                                      unsigned int& cnt) {
   unsigned int hit = 0;
   cnt = 0;
-  if (base >= active_cap(sv)) return 0;
+  if (base >= cap) return 0;
   const uint4* p = reinterpret_cast<const uint4*>(sv.stamps + base);
   uint4 q[kCompactItems / 4];
 #pragma unroll
@@ -219,7 +226,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
                                                           unsigned int* __restrict__ counts) {
   const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
   unsigned int cnt;
-  compact_hits(sv, base, cnt);
+  compact_hits(sv, base, active_cap(sv), cnt);
   unsigned int tot;
   block_exclusive_scan<kBlock>(cnt, &tot);
   if (threadIdx.x == 0) counts[blockIdx.x] = tot;
@@ -228,10 +235,12 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
 // Also sizes the scratch for the next batch (ctl): active cap = the power of
 // two >= kScratchHeadroom x the largest batch seen, rebuilt when it should
 // grow, when it is 4x too large, or when the keys claimed since the last
-// rebuild fill half of it.
+// rebuild fill half of it.  A rebuild takes effect here: ctl[3] keeps this
+// batch's capacity for k_compact_write / k_partition_counts, ctl[0] becomes
+// the new one, ctl[2] tells k_compact_write how many slots to free.
 __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
     unsigned int* __restrict__ counts, int nb, unsigned long long* __restrict__ n_out,
-    const unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
+    unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
     u64 cap_alloc) {
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
@@ -251,7 +260,13 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
       while (want < kScratchHeadroom * mx && want < cap_alloc) want <<= 1;
       if (want > cap_alloc) want = cap_alloc;
       const u64 cur = ctl[0];
-      ctl[2] = (*claims > cur / 2 || want > cur || want * 4 <= cur) ? want : 0ull;
+      const bool rebuild = *claims > cur / 2 || want > cur || want * 4 <= cur;
+      ctl[3] = cur;
+      ctl[2] = rebuild ? want : 0ull;
+      if (rebuild) {
+        ctl[0] = want;
+        *claims = 0ull;
+      }
     }
   }
 }
@@ -262,7 +277,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
                                                           u32* __restrict__ up) {
   const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
   unsigned int cnt;
-  unsigned int hit = compact_hits(sv, base, cnt);
+  unsigned int hit = compact_hits(sv, base, batch_cap(sv), cnt);
   unsigned int tot;
   unsigned int ex = block_exclusive_scan<kBlock>(cnt, &tot);
   unsigned long long dst = (unsigned long long)offs[blockIdx.x] + ex;
@@ -273,6 +288,14 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
     uk[dst] = sv.keys[s];
     up[dst] = (u32)s;
     ++dst;
+  }
+  // rebuild decided by k_compact_scan: free this thread's slots of the new
+  // capacity (its own slots, already read above)
+  const u64 fresh = sv.ctl ? (u64)sv.ctl[2] : 0ull;
+  if (base < fresh) {
+    ulonglong2* kp = reinterpret_cast<ulonglong2*>(sv.keys + base);
+#pragma unroll
+    for (int j = 0; j < kCompactItems / 2; ++j) kp[j] = make_ulonglong2(kEmptyKey, kEmptyKey);
   }
 }
 
@@ -287,7 +310,7 @@ __global__ void __launch_bounds__(kPartBlock) k_partition_counts(
     int64_t* __restrict__ counts) {
   __shared__ int64_t start[kMaxParts + 1];
   const u32 parts = (u32)sv.parts;
-  const u64 R = active_cap(sv) / parts;
+  const u64 R = batch_cap(sv) / parts;
   const int lane = threadIdx.x % kWave, w = threadIdx.x / kWave;
   for (u32 o = w; o <= parts; o += kPartBlock / kWave) {
     if (o == 0 || o == parts) {
@@ -319,10 +342,12 @@ void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
 
 void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st) {
   if (nnz <= 0) return;
-  hipLaunchKernelGGL(k_scratch_maybe_clear, dim3(grid_for((int64_t)s.cap)), dim3(kBlock), 0, st,
-                     s.keys, s.cap, s.claims, s.rebuild_at, s.ctl);
-  hipLaunchKernelGGL(k_scratch_claims_reset, dim3(1), dim3(1), 0, st, s.claims, s.rebuild_at,
-                     s.ctl);
+  if (!s.ctl) {  // fixed capacity: threshold rebuild before the batch
+    hipLaunchKernelGGL(k_scratch_maybe_clear, dim3(grid_for((int64_t)s.cap)), dim3(kBlock), 0, st,
+                       s.keys, s.cap, s.claims, s.rebuild_at, s.ctl);
+    hipLaunchKernelGGL(k_scratch_claims_reset, dim3(1), dim3(1), 0, st, s.claims, s.rebuild_at,
+                       s.ctl);
+  }
   int g1 = (int)((nnz + kDedupChunk - 1) / kDedupChunk);
   hipLaunchKernelGGL(k_dedup_insert, dim3(g1), dim3(kBlock), 0, st, keys, nnz, s, o.pos,
                      o.overflow);

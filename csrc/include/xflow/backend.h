@@ -46,8 +46,9 @@ struct ScratchView {
   unsigned long long* claims = nullptr;  // device counter of inserted keys
   u64 rebuild_at = 0;          // clear the table before a step once claims > rebuild_at
   // HIP backend: adaptive active capacity, kept on the device (no host sync).
-  // ctl[0] = active cap (power of two <= cap), ctl[1] = most unique keys seen
-  // in one batch, ctl[2] = cap to rebuild at before the next batch (0: none).
+  // ctl[0] = active cap for the next batch (power of two <= cap), ctl[1] = most
+  // unique keys seen in one batch, ctl[2] = slots the compaction frees for a
+  // rebuild (0: none), ctl[3] = the cap the current batch was deduplicated with.
   // The table is probed modulo ctl[0]; the compaction scan re-sizes it to
   // kScratchHeadroom x the largest batch seen (a table that fits the Infinity
   // Cache instead of one sized for all-distinct batches).  Null: use cap.

@@ -73,8 +73,10 @@ class ShardedEngine:
         self.world = int(world) if world is not None else dist.get_world_size(group)
         self.rank = int(rank) if rank is not None else dist.get_rank(group)
         dev = engine.device
-        self.counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
-        self.recv_counts = torch.zeros(self.world, dtype=torch.int64, device=dev)
+        # send and receive counts side by side: one D2H copy returns both
+        self._counts_both = torch.zeros(2 * self.world, dtype=torch.int64, device=dev)
+        self.counts = self._counts_both[: self.world]
+        self.recv_counts = self._counts_both[self.world:]
         self.send_keys = torch.empty(max(engine.cfg.max_nnz, 1), dtype=torch.int64, device=dev)
         self._recv_keys = _Buf(torch.int64, dev)
         self._vals_out = _Buf(torch.float32, dev)
@@ -167,7 +169,7 @@ class ShardedEngine:
         e = self.engine
         e.w_prepare(batch, self.world, self.counts, self.send_keys)
         self._a2a(self.recv_counts, self.counts, None, None)
-        both = torch.cat([self.counts, self.recv_counts])
+        both = self._counts_both
         if both.is_cuda:
             # the split sizes come back through pinned memory right behind the
             # counts exchange; the prefetch queues after that copy, so the
