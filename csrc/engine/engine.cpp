@@ -121,7 +121,7 @@ Engine::~Engine() {
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_};
+                  red_tot_, red_count_, inv_};
   for (void* p : ptrs) be.free(p);
 }
 
@@ -178,6 +178,7 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out) {
   o.n_uniq = n_uniq_;
   o.overflow = overflow_;
   o.block_counts = block_counts_;
+  o.inv = parts > 1 ? inv_ : nullptr;
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 
@@ -347,13 +348,17 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
   if (world > 1 && world <= kMaxParts && be_->partitioned_dedup()) {
     // owner-partitioned scratch: the slot-ordered unique list is the send
-    // order already; counts are range counts
+    // order already; counts are range counts.  inv_ (slot -> send index) lets
+    // the LR backward write the send buffer directly.
+    if (!inv_ && red_pairs_ && cfg_.model.kind == kLR) inv_ = balloc<u32>(*be_, scratch_.cap);
     dedup_(b, world, send_keys_out);
+    inv_valid_ = inv_ != nullptr;
     be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
     send_map_ = uniq_pos_;
     return;
   }
   dedup_(b);
+  inv_valid_ = false;
   BucketArgs ba;
   ba.uniq_keys = uniq_keys_;
   ba.uniq_pos = uniq_pos_;
@@ -432,6 +437,16 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
+  if (inv_valid_ && fa.red_pairs && fa.agg_ok && S == 1 && cfg_.model.kind == kLR) {
+    // the bucket reduction writes the normalised send buffer (no gather)
+    be_->memset(grads_out, 0, sizeof(float) * (size_t)n_send);
+    fa.red_out = grads_out;
+    fa.red_inv = inv_;
+    fa.red_rows = srows;
+    be_->forward_backward(fa);
+    last_nsend_ = n_send;
+    return;
+  }
   be_->forward_backward(fa);
   GatherGradArgs ga;
   ga.grad = grad_;

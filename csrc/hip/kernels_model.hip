@@ -609,6 +609,9 @@ struct RedFinal {
   float* grad;
   const float* wpull;  // [slot][ps] pulled rows (NV == 2)
   int S, ps, D;
+  float* out;          // NV == 1 send-order output (FwdArgs::red_out), or null
+  const u32* inv;
+  const int32_t* rows;
 };
 
 template <int NV>
@@ -645,10 +648,19 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
   __syncthreads();
   const u64 d0 = (u64)blockIdx.x << kShift;
   if constexpr (NV == 1) {
-    float* g = f.grad + d0;
-    for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-      const float v = acc[i];
-      if (v != 0.0f) g[i] = v;  // grad is zero outside this step's keys
+    if (f.out) {
+      // normalised like the gather would (lr_worker.cc:116-118, in double)
+      const double rows = (double)f.rows[0];
+      for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
+        const float v = acc[i];
+        if (v != 0.0f) f.out[f.inv[d0 + i]] = (float)((double)v / rows);
+      }
+    } else {
+      float* g = f.grad + d0;
+      for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
+        const float v = acc[i];
+        if (v != 0.0f) g[i] = v;  // grad is zero outside this step's keys
+      }
     }
   } else {
     for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
@@ -680,7 +692,8 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
   hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
                      rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
-  RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim};
+  RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim,
+             NV == 1 ? a.red_out : nullptr, a.red_inv, a.red_rows};
   hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, f);
 }
@@ -1018,6 +1031,8 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
       int g = (int)((a.batch.rows + kLrBlock - 1) / kLrBlock);
       const bool red = grad && a.agg_ok && a.red_pairs && a.red_nb > 0 &&
                        a.red_nb <= kRedMaxBuckets;
+      if (a.red_out && !(red && a.S == 1))
+        throw std::runtime_error("red_out needs the one-slice LR bucket reduction");
       if (red) {
         constexpr int R = kLrGroupRows;
         const int gr = (int)((a.batch.rows + R - 1) / R);

@@ -274,7 +274,8 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
 __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
                                                           const unsigned int* __restrict__ offs,
                                                           u64* __restrict__ uk,
-                                                          u32* __restrict__ up) {
+                                                          u32* __restrict__ up,
+                                                          u32* __restrict__ inv) {
   const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
   unsigned int cnt;
   unsigned int hit = compact_hits(sv, base, batch_cap(sv), cnt);
@@ -287,6 +288,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
     u64 s = base + (u64)j;
     uk[dst] = sv.keys[s];
     up[dst] = (u32)s;
+    if (inv) inv[s] = (u32)dst;
     ++dst;
   }
   // rebuild decided by k_compact_scan: free this thread's slots of the new
@@ -358,7 +360,7 @@ void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipSt
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanBlock), 0, st, o.block_counts, g2,
                      reinterpret_cast<unsigned long long*>(o.n_uniq), s.claims, s.ctl, s.cap);
   hipLaunchKernelGGL(k_compact_write, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts,
-                     o.uniq_keys, o.uniq_pos);
+                     o.uniq_keys, o.uniq_pos, o.inv);
   XF_HIP_CHECK(hipGetLastError());
 }
 

@@ -71,6 +71,7 @@ struct DedupOut {
   int64_t* n_uniq = nullptr;   // device counter
   u32* overflow = nullptr;
   u32* block_counts = nullptr; // [cap/4096 + 1] compaction workspace (HIP backend)
+  u32* inv = nullptr;          // optional [cap]: unique-list index of each slot of the batch (HIP)
 };
 
 struct FwdArgs {
@@ -93,6 +94,12 @@ struct FwdArgs {
   u32* red_tot = nullptr;          // [red_nb + 1] pairs per bucket, then bucket starts
   u32* red_count = nullptr;        // [workgroups] pairs per workgroup
   int red_nb = 0;                  // buckets = ceil(grad dests / 2^kRedShift)
+  // LR, one slice (multi-rank step): the bucket sums go straight to the send
+  // buffer, red_out[red_inv[dest]] = sum / red_rows[0], instead of grad (no
+  // separate gather).  red_out must be zeroed by the caller.
+  float* red_out = nullptr;
+  const u32* red_inv = nullptr;
+  const int32_t* red_rows = nullptr;
 };
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;

@@ -139,6 +139,8 @@ class Engine {
   u32* red_tot_ = nullptr;
   u32* red_count_ = nullptr;
   int red_nb_ = 0;
+  u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
+  bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
   void set_reduction(FwdArgs& fa) const;
   LossStats* stats_ = nullptr;  // [1]
   u32* send_pos_ = nullptr;     // [max_nnz]
