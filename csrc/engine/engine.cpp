@@ -215,6 +215,9 @@ void Engine::train_step(const BatchView& b) {
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
+  // reference-math FM on the GPU reduction path: (B, C) rows, expanded by the apply
+  fa.fm_compact = fa.red_pairs && fa.agg_ok && cfg_.model.kind == kFM &&
+                  cfg_.model.fm_math == kFmReference;
   be_->forward_backward(fa);
 
   ApplyArgs aa;
@@ -234,6 +237,8 @@ void Engine::train_step(const BatchView& b) {
   aa.P = cfg_.model.P();
   aa.sum_slices = cfg_.sum_slices;
   aa.slice_rows = srows;
+  aa.fm_compact = fa.fm_compact;
+  aa.fm_D = cfg_.model.v_dim;
   be_->table_apply(aa);
 }
 

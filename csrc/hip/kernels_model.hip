@@ -612,6 +612,7 @@ struct RedFinal {
   float* out;          // NV == 1 send-order output (FwdArgs::red_out), or null
   const u32* inv;
   const int32_t* rows;
+  bool compact;        // NV == 2: store (B, C) only (FwdArgs::fm_compact)
 };
 
 template <int NV>
@@ -667,6 +668,10 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
       const float B = acc[2 * i], C = acc[2 * i + 1];
       if (B == 0.0f && C == 0.0f) continue;
       const u64 dest = d0 + i;
+      if (f.compact) {  // expanded by the apply (k_apply_group)
+        *reinterpret_cast<float2*>(f.grad + dest * f.ps) = make_float2(B, C);
+        continue;
+      }
       // rows are padded to 16 B: dwordx4 loads of v and stores of the row
       const float4* v4 = reinterpret_cast<const float4*>(f.wpull + (dest / (u64)f.S) * f.ps);
       float4* g4 = reinterpret_cast<float4*>(f.grad + dest * f.ps);
@@ -693,7 +698,7 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
                      rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
   RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim,
-             NV == 1 ? a.red_out : nullptr, a.red_inv, a.red_rows};
+             NV == 1 ? a.red_out : nullptr, a.red_inv, a.red_rows, NV == 2 && a.fm_compact};
   hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, f);
 }
@@ -791,6 +796,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.model.fm_math == kFmReference && a.red_pairs && a.red_nb > 0 &&
                    a.red_nb <= kRedMaxBuckets;
+  if (a.fm_compact && !red) throw std::runtime_error("fm_compact needs the FM reduction path");
   switch (a.model.v_dim) {
 #define XF_FM_CASE(DD)                                                                   \
   case DD: {                                                                             \

@@ -735,20 +735,28 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
         else w0 = w - a.opt.sgd.lr * gv;
         pushed = true;
       };
+      // compact reference-math FM rows (B, C): expand with the pre-step
+      // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
+      const float w_pre = a.fm_compact ? weight() : 0.0f;
+      auto raw_of = [&](int s) -> float {
+        if (!a.fm_compact) return g[s * ps + p];
+        const float Bv = g[s * ps], Cv = g[s * ps + 1];
+        return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
+      };
       if (a.sum_slices) {
         float acc = 0.0f;
         for (int s = 0; s < S; ++s)
-          if (m & (1u << s)) acc += norm_grad(g[s * ps + p], a.slice_rows, s);
+          if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
         if (m) push(acc);
       } else {
         for (int s = 0; s < S; ++s)
-          if (m & (1u << s)) push(norm_grad(g[s * ps + p], a.slice_rows, s));
+          if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
       }
       if (ftrl) *reinterpret_cast<float2*>(st + 2 * p) = make_float2(n0, z0);
       else st[p] = w0;
       if (L.has_flag && p == 0 && m) sp[L.flag_word] = 1u;
     }
-    if (a.zero_after && p < ps) {
+    if (a.zero_after && p < (a.fm_compact ? 2 : ps)) {
       for (int s = 0; s < S; ++s) g[s * ps + p] = 0.0f;
       if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }

@@ -100,6 +100,10 @@ struct FwdArgs {
   float* red_out = nullptr;
   const u32* red_inv = nullptr;
   const int32_t* red_rows = nullptr;
+  // Reference-math FM on the reduction path: keep only (B, C) = (Σ loss,
+  // Σ loss*vsum) in the first two floats of each gradient row; the apply
+  // expands them with the key's pre-step weights (ApplyArgs::fm_compact).
+  bool fm_compact = false;
 };
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
@@ -142,6 +146,10 @@ struct ApplyArgs {
   // Raw per-slice loss sums are divided by the slice's row count here, in
   // double like lr_worker.cc:116-118 (null => rows already normalised).
   const int32_t* slice_rows = nullptr;
+  // Gradient rows hold (B, C) of reference-math FM (FwdArgs::fm_compact):
+  // g_w = D*B, g_v[k] = C - v_k*B with v_k the key's pre-step (pulled) value.
+  bool fm_compact = false;
+  int fm_D = 0;
   // Optional fused reset of the worker dedup scratch (single-device path).
   ScratchView scratch;
   const u32* reset_pos = nullptr;
