@@ -69,6 +69,10 @@ uint64_t feature_hash(const char* p, size_t n);
 
 // Parse a NUL-free text range holding whole lines into `out` (appends).
 void parse_libffm(const char* text, size_t n, CsrBlock& out);
+// The same with the range split at line boundaries over `threads` threads
+// (segments of >= 256 KB); the result is identical to parse_libffm.
+void parse_libffm_parallel(const char* text, size_t n, CsrBlock& out, int threads);
+int default_parse_threads();  // min(hardware_concurrency, 16)
 
 class BlockReader {
  public:
@@ -80,9 +84,13 @@ class BlockReader {
   bool next(CsrBlock& out);
   void rewind();
   const std::string& path() const { return path_; }
+  // threads used to parse one block (1 = serial, the reference's LoadData)
+  void set_parse_threads(int t) { parse_threads_ = t < 1 ? 1 : t; }
+  int parse_threads() const { return parse_threads_; }
 
  private:
   size_t fill_block(const char** text);  // returns length of the block's text
+  int parse_threads_ = default_parse_threads();
   std::string path_;
   FILE* fp_ = nullptr;
   std::vector<char> buf_;

@@ -1,6 +1,7 @@
 // xflow-amd: libffm block reader implementation (see xflow/reader.h).
 #include "xflow/reader.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -66,6 +67,47 @@ void parse_libffm(const char* text, size_t n, CsrBlock& out) {
   }
 }
 
+void parse_libffm_parallel(const char* text, size_t n, CsrBlock& out, int threads) {
+  // below ~256 KB per thread the spawn costs more than the parse
+  const size_t kMinPerThread = 256 << 10;
+  int T = threads;
+  if ((size_t)T * kMinPerThread > n) T = (int)(n / kMinPerThread);
+  if (T <= 1) {
+    parse_libffm(text, n, out);
+    return;
+  }
+  // cut at line boundaries: segment t starts after the first '\n' at or past t*n/T
+  std::vector<size_t> cut((size_t)T + 1, n);
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {
+    size_t c = std::max(cut[t - 1], (size_t)t * n / T);
+    const char* nl = c < n ? static_cast<const char*>(std::memchr(text + c, '\n', n - c)) : nullptr;
+    cut[t] = nl ? (size_t)(nl - text) + 1 : n;
+  }
+  std::vector<CsrBlock> part((size_t)T);
+  std::vector<std::thread> th;
+  th.reserve((size_t)T - 1);
+  for (int t = 1; t < T; ++t)
+    th.emplace_back([&, t] { parse_libffm(text + cut[t], cut[t + 1] - cut[t], part[t]); });
+  parse_libffm(text, cut[1], part[0]);
+  for (auto& x : th) x.join();
+  // concatenate in segment order: identical to a serial parse
+  for (int t = 0; t < T; ++t) {
+    const CsrBlock& p = part[t];
+    const int32_t base = (int32_t)out.keys.size();
+    out.keys.insert(out.keys.end(), p.keys.begin(), p.keys.end());
+    out.fgid.insert(out.fgid.end(), p.fgid.begin(), p.fgid.end());
+    out.labels.insert(out.labels.end(), p.labels.begin(), p.labels.end());
+    for (size_t r = 1; r < p.row_ptr.size(); ++r) out.row_ptr.push_back(base + p.row_ptr[r]);
+    if (p.max_fgid > out.max_fgid) out.max_fgid = p.max_fgid;
+  }
+}
+
+int default_parse_threads() {
+  const unsigned hc = std::thread::hardware_concurrency();
+  return hc == 0 ? 1 : (int)std::min(hc, 16u);
+}
+
 BlockReader::BlockReader(const std::string& path, size_t block_bytes)
     : path_(path), buf_(block_bytes < 2 ? 2 : block_bytes) {
   fp_ = std::fopen(path.c_str(), "rb");
@@ -106,7 +148,7 @@ bool BlockReader::next(CsrBlock& out) {
     const char* text = nullptr;
     size_t len = fill_block(&text);
     if (len == 0) return false;
-    parse_libffm(text, len, out);
+    parse_libffm_parallel(text, len, out, parse_threads_);
     if (out.rows() > 0) return true;
     // a block of only malformed lines: keep reading until data or EOF
     if (btop_ == bmax_ && std::feof(fp_)) return false;

@@ -309,7 +309,8 @@ PYBIND11_MODULE(_xflow_native, m) {
              if (!r.next(b)) return py::none();
              return block_to_dict(b);
            })
-      .def("rewind", &BlockReader::rewind);
+      .def("rewind", &BlockReader::rewind)
+      .def_property("parse_threads", &BlockReader::parse_threads, &BlockReader::set_parse_threads);
 
   py::class_<PrefetchReader>(m, "PrefetchReader")
       .def(py::init<const std::string&, size_t>())

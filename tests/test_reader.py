@@ -109,3 +109,27 @@ def test_prefetch_reader_equals_block_reader(native):
 def test_missing_file_raises(native):
     with pytest.raises(RuntimeError):
         native.BlockReader("/nonexistent/file-00000", 1024)
+
+
+def test_parallel_parse_equals_serial(tmp_path, native):
+    """Blocks parsed on several threads (split at line boundaries) equal the
+    serial parse bit for bit, including the block carry-over."""
+    src = open(os.path.join(DATA, "small_train-00000"), "rb").read()
+    path = tmp_path / "big-00000"
+    path.write_bytes(src * 100)  # ~2.6 MB: several 1 MB blocks, >= 256 KB per thread
+    out = {}
+    for threads in (1, 4):
+        r = native.BlockReader(str(path), 1 << 20)
+        r.parse_threads = threads
+        blocks = []
+        while True:
+            b = r.next()
+            if b is None:
+                break
+            blocks.append(b)
+        out[threads] = blocks
+    assert len(out[1]) == len(out[4]) >= 3
+    for a, b in zip(out[1], out[4]):
+        for k in ("row_ptr", "keys", "fgid", "labels"):
+            np.testing.assert_array_equal(a[k], b[k])
+    assert sum(len(b["labels"]) for b in out[4]) == 200 * 100
