@@ -133,3 +133,79 @@ def test_parallel_parse_equals_serial(tmp_path, native):
         for k in ("row_ptr", "keys", "fgid", "labels"):
             np.testing.assert_array_equal(a[k], b[k])
     assert sum(len(b["labels"]) for b in out[4]) == 200 * 100
+
+
+def test_xfb_shard_blocks_equal_text_reader(tmp_path, native):
+    """An .xfb shard (binfmt.convert) holds exactly what the text reader parses."""
+    from xflow_amd.data import binfmt
+
+    src = os.path.join(DATA, "small_train-00000")
+    dst = str(tmp_path / "s.xfb")
+    info = binfmt.convert(src, dst, block_bytes=1000, threads=2)
+    r = native.BlockReader(src, 1 << 20)
+    b = r.next()
+    assert r.next() is None
+    assert info == {"rows": len(b["labels"]), "nnz": len(b["keys"])}
+    s = binfmt.ShardReader(dst, block_rows=37)
+    parts = []
+    while True:
+        x = s.next()
+        if x is None:
+            break
+        assert len(x["labels"]) <= 37 and x["row_ptr"][0] == 0
+        assert x["row_ptr"][-1] == len(x["keys"])
+        parts.append(x)
+    np.testing.assert_array_equal(np.concatenate([p["labels"] for p in parts]), b["labels"])
+    np.testing.assert_array_equal(np.concatenate([p["keys"] for p in parts]),
+                                  np.asarray(b["keys"]).view(np.uint64))
+    np.testing.assert_array_equal(np.concatenate([p["fgid"] for p in parts]), b["fgid"])
+    lens = np.concatenate([np.diff(p["row_ptr"]) for p in parts])
+    np.testing.assert_array_equal(lens, np.diff(b["row_ptr"]))
+    assert binfmt.max_block(dst, 37)[0] == 37
+
+
+def test_xfb_write_roundtrip_and_bad_magic(tmp_path):
+    from xflow_amd.data import binfmt
+
+    rp = np.array([0, 2, 2, 5])
+    keys = np.arange(5, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+    binfmt.write(str(tmp_path / "a.xfb"), np.array([1, 0, 1]), rp, keys)
+    s = binfmt.Shard(str(tmp_path / "a.xfb"))
+    assert (s.rows, s.nnz) == (3, 5)
+    np.testing.assert_array_equal(s.keys, keys)
+    np.testing.assert_array_equal(s.fgid, np.zeros(5, np.int32))
+    with pytest.raises(ValueError):
+        binfmt.write(str(tmp_path / "b.xfb"), np.array([1, 0]), rp, keys)
+    (tmp_path / "c.xfb").write_bytes(b"NOTASHARD" * 8)
+    with pytest.raises(ValueError):
+        binfmt.Shard(str(tmp_path / "c.xfb"))
+
+
+@pytest.mark.parametrize("kind", ["lr", "fm"])
+def test_trainer_on_xfb_equals_text(tmp_path, kind):
+    """Training from .xfb shards (text files absent) predicts exactly like
+    training from the libffm text (one block per epoch in both)."""
+    import shutil
+
+    import torch
+
+    from xflow_amd.config import EngineConfig, ModelConfig, TrainConfig
+    from xflow_amd.data import binfmt
+    from xflow_amd.trainer import Trainer
+
+    preds = []
+    for mode in ("text", "xfb"):
+        d = tmp_path / mode
+        d.mkdir()
+        for name in ("small_train-00000", "small_test-00000"):
+            if mode == "text":
+                shutil.copy(os.path.join(DATA, name), d / name)
+            else:
+                binfmt.convert(os.path.join(DATA, name), str(d / (name + ".xfb")))
+        cfg = TrainConfig(train_prefix=str(d / "small_train"), test_prefix=str(d / "small_test"),
+                          epochs=3, threads=8, pred_dir=str(d), model=ModelConfig(kind=kind),
+                          engine=EngineConfig(table_log2_cap=14))
+        Trainer(cfg, device=torch.device("cpu")).train()
+        preds.append(np.loadtxt(d / "pred_0_0.txt"))
+    assert len(preds[1]) == 200
+    np.testing.assert_array_equal(preds[0], preds[1])

@@ -93,6 +93,7 @@ class TrainConfig:
     epochs: int = 60
     threads: int = 0             # 0 => os.cpu_count() like hardware_concurrency
     train_block_bytes: int = 2 << 20
+    block_rows: int = 0          # rows per block of binary (.xfb) shards; 0 => 65536
     test_block_bytes: int = 0    # 0 => 4 MB LR, 2 MB FM/MVM
     serial_slices: bool = False
     keep_remainder: bool = False

@@ -22,6 +22,7 @@ Differences by design (MI355X-first):
 from __future__ import annotations
 
 import os
+import warnings
 import sys
 import time
 from typing import Optional
@@ -32,6 +33,7 @@ import torch
 from xflow_amd import checkpoint
 from xflow_amd import native as _native
 from xflow_amd.config import TrainConfig, model_kind
+from xflow_amd.data import binfmt
 from xflow_amd.engine import Batch, Engine
 from xflow_amd.metrics import MetricsLogger, reference_auc
 from xflow_amd.parallel import dist as xdist
@@ -63,6 +65,14 @@ class Trainer:
         ecfg = cfg.engine
         ecfg.max_rows = max(ecfg.max_rows, max_block // 2 + 16)
         ecfg.max_nnz = max(ecfg.max_nnz, max_block // 2 + 16)
+        # binary shards (.xfb) come in blocks of block_rows rows: size for the largest
+        self.block_rows = cfg.block_rows or 65536
+        for p in (shard_path(cfg.train_prefix, xdist.my_rank()), shard_path(cfg.test_prefix, 0)):
+            xfb = binfmt.shard_file(p)
+            if xfb:
+                rows, nnz = binfmt.max_block(xfb, self.block_rows)
+                ecfg.max_rows = max(ecfg.max_rows, rows)
+                ecfg.max_nnz = max(ecfg.max_nnz, nnz)
         ecfg.max_slices = max(ecfg.max_slices, self.S)
         self.engine = Engine(cfg.model, cfg.optim, ecfg, device=self.device)
         self.sharded = None
@@ -98,7 +108,9 @@ class Trainer:
         pin = dev.type == "cuda"
 
         def up(a):
-            t = torch.from_numpy(np.ascontiguousarray(a))
+            with warnings.catch_warnings():  # read-only .xfb mappings: only ever read
+                warnings.simplefilter("ignore", UserWarning)
+                t = torch.from_numpy(np.ascontiguousarray(a))
             if pin:
                 t = t.pin_memory()
             return t.to(dev, non_blocking=True)
@@ -152,7 +164,9 @@ class Trainer:
         nat = _native.load()
         log_every = int(os.environ.get("XFLOW_LOG_EVERY", "0"))
         for _ in range(epochs):
-            reader = nat.PrefetchReader(path, cfg.train_block_bytes)
+            xfb = binfmt.shard_file(path)
+            reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
+                      else nat.PrefetchReader(path, cfg.train_block_bytes))
             t0 = time.perf_counter()
             ep_samples = 0
             while True:
@@ -212,7 +226,10 @@ class Trainer:
         labels, preds = [], []
         reader = None
         if self.rank == 0:
-            reader = nat.BlockReader(shard_path(cfg.test_prefix, 0), cfg.resolved_test_block())
+            tpath = shard_path(cfg.test_prefix, 0)
+            xfb = binfmt.shard_file(tpath)
+            reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
+                      else nat.BlockReader(tpath, cfg.resolved_test_block()))
         compat_mvm = model_kind(cfg.model.kind) == 2 and cfg.mvm_predict_compat
         while True:
             blk = reader.next() if reader is not None else None
