@@ -51,6 +51,10 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--log2-cap", type=int, default=22, help="table slots per rank = 2^N")
     ap.add_argument("--train-block-bytes", type=int, default=2 << 20)
     ap.add_argument("--test-block-bytes", type=int, default=0)
+    ap.add_argument("--resident", action="store_true",
+                    help="keep the training shard in HBM after the first epoch (no re-read)")
+    ap.add_argument("--csr-only", action="store_true",
+                    help="train fixed-width blocks through the CSR path as well")
     ap.add_argument("--block-rows", type=int, default=0,
                     help="rows per block when <prefix>-%%05d.xfb binary shards exist "
                          "(python -m xflow_amd.data.binfmt convert); default 65536")
@@ -73,6 +77,7 @@ def config_from_args(a) -> TrainConfig:
     return TrainConfig(
         train_prefix=a.train_prefix, test_prefix=a.test_prefix, epochs=a.epochs,
         threads=a.threads, train_block_bytes=a.train_block_bytes, block_rows=a.block_rows,
+        resident=a.resident, fixed_width=not a.csr_only,
         test_block_bytes=a.test_block_bytes, serial_slices=a.serial_slices,
         keep_remainder=a.keep_remainder, mvm_predict_compat=a.mvm_predict_compat,
         init_push=not a.no_init_push, pred_dir=a.pred_dir, checkpoint_dir=a.save,

@@ -94,6 +94,9 @@ class TrainConfig:
     threads: int = 0             # 0 => os.cpu_count() like hardware_concurrency
     train_block_bytes: int = 2 << 20
     block_rows: int = 0          # rows per block of binary (.xfb) shards; 0 => 65536
+    fixed_width: bool = True     # blocks whose rows all hold F features train field-major
+    resident: bool = False       # keep the first epoch's device batches in HBM for the rest
+    copy_threads: int = 8        # host threads staging a block into pinned memory
     test_block_bytes: int = 0    # 0 => 4 MB LR, 2 MB FM/MVM
     serial_slices: bool = False
     keep_remainder: bool = False

@@ -34,6 +34,7 @@ from xflow_amd import checkpoint
 from xflow_amd import native as _native
 from xflow_amd.config import TrainConfig, model_kind
 from xflow_amd.data import binfmt
+from xflow_amd.data.upload import BlockStream
 from xflow_amd.engine import Batch, Engine
 from xflow_amd.metrics import MetricsLogger, reference_auc
 from xflow_amd.parallel import dist as xdist
@@ -48,6 +49,14 @@ def shard_path(prefix: str, rank: int) -> str:
 
 def _say(msg: str) -> None:
     print(msg, flush=True)
+
+
+def _uniform_width(row_ptr) -> int:
+    """Features per row when every row has the same (non-zero) count, else 0."""
+    lens = np.diff(np.asarray(row_ptr))
+    if len(lens) == 0 or lens[0] <= 0 or not np.all(lens == lens[0]):
+        return 0
+    return int(lens[0])
 
 
 class Trainer:
@@ -93,10 +102,13 @@ class Trainer:
         self.samples = 0
         self.resumed = False
         self._with_fgid = model_kind(cfg.model.kind) == 2
+        self._resident = None
 
     # ------------------------------------------------------------------ data
     def _to_batch(self, blk: Optional[dict], used: int, slice_rows: int) -> Batch:
         dev = self.device
+        if blk is not None and used > 0 and isinstance(blk["keys"], torch.Tensor):
+            return self._device_batch(blk, used, slice_rows)
         if blk is None or used <= 0:
             return Batch(keys=torch.empty(0, dtype=torch.int64, device=dev),
                          labels=torch.empty(0, dtype=torch.float32, device=dev),
@@ -115,9 +127,25 @@ class Trainer:
                 t = t.pin_memory()
             return t.to(dev, non_blocking=True)
 
-        return Batch(keys=up(blk["keys"][:nnz].view(np.int64)), labels=up(blk["labels"][:used]),
-                     row_ptr=up(rp), fgid=up(blk["fgid"][:nnz]) if self._with_fgid else None,
+        F = _uniform_width(rp) if self.cfg.fixed_width else 0
+        keys = up(np.asarray(blk["keys"][:nnz]).view(np.int64))
+        fgid = up(blk["fgid"][:nnz]) if self._with_fgid else None
+        if F:
+            return Batch(keys=keys, labels=up(blk["labels"][:used]), fgid=fgid, nnz_per_row=F,
+                         slice_rows=slice_rows).to_field_major()
+        return Batch(keys=keys, labels=up(blk["labels"][:used]), row_ptr=up(rp), fgid=fgid,
                      slice_rows=slice_rows)
+
+    def _device_batch(self, blk: dict, used: int, slice_rows: int) -> Batch:
+        """Batch over a block already on the device (data.upload.BlockStream)."""
+        nnz = int(blk["row_ptr_host"][used])
+        fgid = blk["fgid"][:nnz] if self._with_fgid else None
+        F = blk["nnz_per_row"] if self.cfg.fixed_width else 0
+        if F:
+            return Batch(keys=blk["keys"][:nnz], labels=blk["labels"][:used], fgid=fgid,
+                         nnz_per_row=F, slice_rows=slice_rows).to_field_major()
+        return Batch(keys=blk["keys"][:nnz], labels=blk["labels"][:used],
+                     row_ptr=blk["row_ptr"][:used + 1], fgid=fgid, slice_rows=slice_rows)
 
     def _split(self, rows: int):
         """(used rows, slice rows) under the reference's slicing rule."""
@@ -139,13 +167,17 @@ class Trainer:
         if self.concurrent or blk is None or used <= 0:
             yield self._to_batch(blk, used, sr)
             return
-        rp = blk["row_ptr"]
+        rp = np.asarray(blk.get("row_ptr_host", blk["row_ptr"]))
         for s0 in range(0, used, sr):
             n = min(sr, used - s0)
-            sub = {"row_ptr": rp[s0: s0 + n + 1] - rp[s0],
-                   "keys": blk["keys"][rp[s0]: rp[s0 + n]],
-                   "fgid": blk["fgid"][rp[s0]: rp[s0 + n]],
+            k0, k1 = int(rp[s0]), int(rp[s0 + n])
+            sub = {"row_ptr": blk["row_ptr"][s0: s0 + n + 1] - k0,
+                   "keys": blk["keys"][k0: k1],
+                   "fgid": blk["fgid"][k0: k1] if "fgid" in blk else None,
                    "labels": blk["labels"][s0: s0 + n]}
+            if "row_ptr_host" in blk:
+                sub["row_ptr_host"] = rp[s0: s0 + n + 1] - k0
+                sub["nnz_per_row"] = blk["nnz_per_row"]
             yield self._to_batch(sub, n, n)
 
     # ----------------------------------------------------------------- train
@@ -164,16 +196,33 @@ class Trainer:
         nat = _native.load()
         log_every = int(os.environ.get("XFLOW_LOG_EVERY", "0"))
         for _ in range(epochs):
-            xfb = binfmt.shard_file(path)
-            reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
-                      else nat.PrefetchReader(path, cfg.train_block_bytes))
+            stream = record = None
+            if self._resident is not None:  # batches kept in HBM by the first epoch
+                it = iter(self._resident)
+                nxt = lambda: next(it, None)  # noqa: E731
+            else:
+                xfb = binfmt.shard_file(path)
+                reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
+                          else nat.PrefetchReader(path, cfg.train_block_bytes))
+                nxt = reader.next
+                if self.device.type == "cuda" and self.concurrent:
+                    stream = BlockStream(reader.next, self.device, self._with_fgid,
+                                         copy_threads=cfg.copy_threads)
+                    nxt = stream.next
+                record = [] if cfg.resident else None
             t0 = time.perf_counter()
             ep_samples = 0
             while True:
-                blk = reader.next()
+                blk = nxt()
                 if not xdist.all_any(blk is not None, self.device):
                     break
-                for b in self._slices_of(blk):
+                if self._resident is not None and blk is not None:
+                    batches = blk
+                else:
+                    batches = list(self._slices_of(blk))
+                    if record is not None and blk is not None:
+                        record.append(batches)
+                for b in batches:
                     if self.watchdog is not None:
                         self.watchdog.beat()
                     if not self.faults.before_step(self.steps):
@@ -185,6 +234,10 @@ class Trainer:
                     ep_samples += b.rows
                     if log_every and self.steps % log_every == 0:
                         self._log_progress(ep_samples, t0)
+            if stream is not None:
+                stream.close()
+            if record is not None:
+                self._resident = record
             if hasattr(self.sharded, "flush"):
                 self.sharded.flush()
             self.samples += ep_samples
