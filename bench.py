@@ -51,6 +51,10 @@ def parse():
                     help="force the multi-rank (all-to-all) step even at 1 GPU (overhead probe)")
     ap.add_argument("--async", dest="async_p2p", action="store_true",
                     help="config 4: staleness-1 pipelined steps, pushes over RCCL point-to-point")
+    ap.add_argument("--v-init-scale", type=float, default=1e-2,
+                    help="latent init N(0,1)*scale (ftrl.h:114-120: 1e-2).  MVM on 39 fields "
+                         "at 1e-2 has a field product that underflows to 0 (no gradient "
+                         "traffic); 1.0 keeps it alive for measuring the backward")
     ap.add_argument("--lambda1", type=float, default=5e-5,
                     help="FTRL L1 (ftrl.h:19); config 4 reports the non-zero weight count")
     ap.add_argument("--overlap", choices=["on", "off"], default="off",
@@ -88,7 +92,8 @@ def main():
     synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed)
     nnz = a.batch * synth.fields
     model = ModelConfig(kind=a.model, v_dim=a.v_dim)
-    engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1),
+    engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
+                                       v_init_scale=a.v_init_scale),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
                                  max_slices=1),
                     device=device)
@@ -179,7 +184,7 @@ def main():
                        "hashed_features": a.features, "table_slots_per_gpu": 2 ** log2_cap,
                        "backend": engine.backend_name,
                        "a2a_transport": sharded.transport if sharded is not None else "none",
-                       "input_overlap": overlap},
+                       "input_overlap": overlap, "v_init_scale": a.v_init_scale},
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
         }

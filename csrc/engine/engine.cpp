@@ -85,9 +85,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // atomic-free gradient reduction (FwdArgs::red_*): LR (1 value per key) and
   // reference-math FM (2 values per key, 16-byte records)
   const bool fm_ref = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference;
-  if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref)) {
+  const bool mvm = cfg_.model.kind == kMVM;
+  if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref || mvm)) {
     const int nv = fm_ref ? 2 : 1, shift = red_shift(nv);
-    const int group_rows = fm_ref ? kFmGroupRows : kLrGroupRows;
+    const int group_rows = fm_ref ? kFmGroupRows : (mvm ? kMvmGroupRows : kLrGroupRows);
     const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
     const int nb = (int)((dests + (1ull << shift) - 1) >> shift);
     if (nb <= kRedMaxBuckets) {
@@ -98,6 +99,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       red_hist_ = balloc<u32>(be, (size_t)nb * groups);
       red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
       red_count_ = balloc<u32>(be, groups);
+      if (mvm) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
     }
   }
   stats_ = balloc<LossStats>(be, 2);
@@ -121,7 +123,7 @@ Engine::~Engine() {
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_, inv_};
+                  red_tot_, red_count_, inv_, red_rowv_};
   for (void* p : ptrs) be.free(p);
 }
 
@@ -133,6 +135,7 @@ void Engine::set_reduction(FwdArgs& fa) const {
   fa.red_tot = red_tot_;
   fa.red_count = red_count_;
   fa.red_nb = red_nb_;
+  fa.red_rowv = red_rowv_;
 }
 
 int Engine::slices_of(const BatchView& b) const {
@@ -158,7 +161,7 @@ const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
   return slice_rows_;
 }
 
-void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out) {
+void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want_inv) {
   if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
   if (b.col_stride > 0 && (b.row_ptr || b.col_stride < b.rows || b.nnz != b.rows * b.nnz_per_row))
@@ -178,7 +181,7 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out) {
   o.n_uniq = n_uniq_;
   o.overflow = overflow_;
   o.block_counts = block_counts_;
-  o.inv = parts > 1 ? inv_ : nullptr;
+  o.inv = want_inv ? inv_ : nullptr;
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 
@@ -351,14 +354,17 @@ std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
 void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out) {
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
-  if (world > 1 && world <= kMaxParts && be_->partitioned_dedup()) {
+  if (world >= 1 && world <= kMaxParts && be_->partitioned_dedup()) {
     // owner-partitioned scratch: the slot-ordered unique list is the send
-    // order already; counts are range counts.  inv_ (slot -> send index) lets
-    // the LR backward write the send buffer directly.
+    // order already; counts are range counts (one range at world 1).  inv_
+    // (slot -> send index) lets the LR backward write the send buffer directly.
     if (!inv_ && red_pairs_ && cfg_.model.kind == kLR) inv_ = balloc<u32>(*be_, scratch_.cap);
-    dedup_(b, world, send_keys_out);
+    dedup_(b, world, send_keys_out, true);
     inv_valid_ = inv_ != nullptr;
-    be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
+    if (world > 1)
+      be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
+    else
+      be_->copy_d2d(counts_out, n_uniq_, sizeof(int64_t));
     send_map_ = uniq_pos_;
     return;
   }
@@ -430,7 +436,10 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
-  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, ps);
+  const bool direct = inv_valid_ && red_pairs_ && S == 1 && cfg_.model.kind == kLR &&
+                      (double)scratch_.cap * S * ps < 4294967295.0;
+  // the direct path's send buffer is zeroed by the scatter
+  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, ps, direct ? grads_out : nullptr);
   if (masks) be_->slice_masks(b, pos_, tmask_);
   FwdArgs fa;
   fa.batch = b;
@@ -442,9 +451,9 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
-  if (inv_valid_ && fa.red_pairs && fa.agg_ok && S == 1 && cfg_.model.kind == kLR) {
+  if (direct) {
+    if (!fa.red_pairs || !fa.agg_ok) throw std::logic_error("direct send path without reduction");
     // the bucket reduction writes the normalised send buffer (no gather)
-    be_->memset(grads_out, 0, sizeof(float) * (size_t)n_send);
     fa.red_out = grads_out;
     fa.red_inv = inv_;
     fa.red_rows = srows;

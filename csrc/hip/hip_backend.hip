@@ -85,8 +85,8 @@ class HipBackend final : public Backend {
   }
   void gather_grads(const GatherGradArgs& a) override { hip::launch_gather_grads(a, stream_); }
   void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
-                    int64_t n_max, int width) override {
-    hip::launch_scatter_rows(src, dst, map, n_dev, n_max, width, stream_);
+                    int64_t n_max, int width, float* zero_out) override {
+    hip::launch_scatter_rows(src, dst, map, n_dev, n_max, width, zero_out, stream_);
   }
   void gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                    int64_t n_max, int width, bool zero_src) override {

@@ -11,6 +11,7 @@
 //   LR   lr_worker.cc:121-143 (loss), :100-119 (gradient)
 //   FM   fm_worker.cc:159-202 (loss), :126-157 (gradient)      [kFmReference]
 //   MVM  mvm_worker.cc:172-218 (loss), :137-170 (gradient)
+#include <cstdlib>
 #include "kernels.h"
 #include "hip_util.h"
 
@@ -853,14 +854,22 @@ __device__ __forceinline__ void load_row(const float* __restrict__ wp, u32 p, fl
   }
 }
 
-template <int D, bool kGrad, bool kAgg>
-__global__ void __launch_bounds__(mvm_block(D)) k_mvm2(FwdArgs a) {
+constexpr int mvm_block_for(int D, bool red) { return red ? kMvmGroupRows : mvm_block(D); }
+
+template <int D, bool kGrad, bool kAgg, bool kRed = false>
+__global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
   constexpr int PS = mvm_ps(D);
-  constexpr int BLOCK = mvm_block(D);
+  constexpr int BLOCK = mvm_block_for(D, kRed);
   constexpr int LOG2 = ilog2c(2 * BLOCK);
   __shared__ u32 s_tag[kAgg ? 2 : 1][kAgg ? (1 << LOG2) : 1];
   __shared__ float s_acc[kAgg ? 2 : 1][kAgg ? (1 << LOG2) * PS : 1];
   __shared__ int s_wmax[BLOCK / kWave];
+  __shared__ u32 s_hist[kRed ? kRedMaxBuckets : 1];
+  __shared__ u32 s_cnt;
+  if constexpr (kRed) {  // published by the barrier before the record loop
+    for (int i = threadIdx.x; i < a.red_nb; i += BLOCK) s_hist[i] = 0u;
+    if (threadIdx.x == 0) s_cnt = 0u;
+  }
   const BatchView& b = a.batch;
   const bool compat = a.model.mvm_math == kMvmCompat;
   const u32* __restrict__ pos = a.pos;
@@ -972,7 +981,60 @@ __global__ void __launch_bounds__(mvm_block(D)) k_mvm2(FwdArgs a) {
         c[k] = (Sf[k] == 0.0f) ? 0.0f
                                : (float)((double)loss * ((double)M[k] / (1.0 + (double)Sf[k])));
     };
-    if constexpr (!kAgg) {
+    if constexpr (kRed) {
+      // Dup-free rows: S of an occurrence is the key's own v, so the gradient
+      // factorises as T_k/(1+v_k) with T = loss*M per row -- one 8-byte
+      // record (dest, row) per occurrence, summed per key by k_mvm_red_sum.
+      // Rows with a repeated field (S = field sum): global atomics.
+      bool emit = false;
+      if (active && !dup && loss != 0.0f) {
+        float* t = a.red_rowv + (size_t)r * PS;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          t[k] = loss * M[k];
+          emit |= M[k] != 0.0f;
+        }
+      }
+      if (active && dup) {
+        for (int j = 0; j < len; ++j) {
+          float c[D];
+          contrib(j, c);
+          float* g = a.grad + ((size_t)pos[rs.at(j)] * S + s) * PS;
+#pragma unroll
+          for (int k = 0; k < D; ++k) atomicAdd(&g[k], c[k]);
+        }
+      }
+      const int m = wave_max(len);
+      if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
+      __syncthreads();
+      int maxlen = 0;
+#pragma unroll
+      for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
+      const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
+      u64* region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
+      const int lane = lane_id();
+      for (int j = 0; j < maxlen; ++j) {
+        const bool has = emit && j < len;
+        const u32 dest = has ? pos[rs.at(j)] * S + s : 0u;
+        const unsigned long long bm = __ballot(has);
+        if (bm) {
+          const int leader = __ffsll((long long)bm) - 1;
+          u32 base = 0;
+          if (lane == leader) base = atomicAdd(&s_cnt, (u32)__popcll(bm));
+          base = __shfl(base, leader);
+          if (has) {
+            region[base + (u32)__popcll(bm & ((1ull << lane) - 1ull))] =
+                (u64)dest | ((u64)(u32)r << 32);
+            XF_DASSERT((int)(dest >> kRedShift) < a.red_nb);
+            atomicAdd(&s_hist[dest >> kRedShift], 1u);
+          }
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) a.red_count[blockIdx.x] = s_cnt;
+      for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+        a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
+    } else if constexpr (!kAgg) {
       for (int j = 0; j < len; ++j) {
         float c[D];
         contrib(j, c);
@@ -1006,16 +1068,138 @@ __global__ void __launch_bounds__(mvm_block(D)) k_mvm2(FwdArgs a) {
   flush_stats<BLOCK>(st, a.stats);
 }
 
+// MVM bucket sums.  A bucket's 2^kRedShift destinations x D floats do not fit
+// in LDS, so NSUB workgroups share a bucket, each accumulating the records of
+// its 2^kRedShift/NSUB destinations (Σ T[row], D LDS atomics per record) and
+// skipping the rest.  The NSUB workgroups of a bucket are dispatched back to
+// back on the same XCD (workgroup i runs on XCD i % 8), so the bucket's
+// records come from HBM once and from that XCD's L2 after.  The final
+// gradient (mvm_worker.cc:137-170) is Σ T / (1 + v), 0 where v == 0, added to
+// grad (the duplicate-field rows' atomics may already be there).
+constexpr int mvm_nsub(int D) { return D <= 16 ? 16 : 32; }
+
+// XFLOW_MVM_ATOMICS=1 keeps the LDS-column + global-atomic backward (A/B)
+static bool mvm_atomics_forced() {
+  static const bool forced = std::getenv("XFLOW_MVM_ATOMICS") != nullptr;
+  return forced;
+}
+
+struct MvmRedFinal {
+  float* grad;
+  const float* wpull;
+  const float* rowv;
+  int S, nb;
+};
+
+template <int D>
+__global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict__ sorted,
+                                                           const u32* __restrict__ start,
+                                                           MvmRedFinal f) {
+  constexpr int PS = mvm_ps(D);
+  constexpr int NSUB = mvm_nsub(D);
+  constexpr int kSubShift = kRedShift - ilog2c(NSUB);
+  constexpr u32 kSub = 1u << kSubShift;
+  __shared__ float acc[kSub * D];
+  const u32 q = blockIdx.x >> 3;
+  const u32 sub = q % NSUB;
+  const int bucket = (int)((q / NSUB) * 8 + (blockIdx.x & 7));
+  if (bucket >= f.nb) return;
+  const u32 beg = start[bucket], end = start[bucket + 1];
+  if (beg == end) return;
+  for (u32 i = threadIdx.x; i < kSub * D; i += kRedBlock) acc[i] = 0.0f;
+  __syncthreads();
+  const int lane = lane_id();
+  // block-uniform trip count: every lane takes part in the wave-level combine
+  for (u32 c0 = beg; c0 < end; c0 += kRedUnroll * kRedBlock) {
+    u64 pr[kRedUnroll];
+#pragma unroll
+    for (int u = 0; u < kRedUnroll; ++u) {
+      const u32 i = c0 + (u32)u * kRedBlock + threadIdx.x;
+      pr[u] = i < end ? sorted[i] : ~0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kRedUnroll; ++u) {
+      const u32 d = (u32)pr[u];
+      bool pending = pr[u] != ~0ull && ((d >> kSubShift) & (NSUB - 1)) == sub;
+      float t[PS];
+      if (pending) load_row<PS>(f.rowv, (u32)(pr[u] >> 32), t);
+      // Power-law keys: a hot key's records arrive many to a wave and would
+      // serialise D LDS atomics per record on one address.  While some
+      // destination holds >= 4 of the wave's pending records, sum those
+      // across the wave and let one lane add them.
+#pragma unroll 1
+      for (int it = 0; it < 4; ++it) {
+        const unsigned long long m = __ballot(pending);
+        if (!m) break;
+        const int leader = __ffsll((long long)m) - 1;
+        const u32 dl = __shfl(d, leader);
+        const bool in = pending && d == dl;
+        if (__popcll(__ballot(in)) < 4) break;
+        float* a = acc + (dl & (kSub - 1)) * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+          const float v = wave_sum(in ? t[k] : 0.0f);
+          if (lane == leader) atomicAdd(&a[k], v);
+        }
+        pending = pending && !in;
+      }
+      if (pending) {
+        float* a = acc + (d & (kSub - 1)) * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) atomicAdd(&a[k], t[k]);
+      }
+    }
+  }
+  __syncthreads();
+  const u64 d0 = ((u64)bucket << kRedShift) + ((u64)sub << kSubShift);
+  for (u32 l = threadIdx.x; l < kSub; l += kRedBlock) {
+    const u64 dest = d0 + l;
+    float* g = f.grad + dest * PS;
+    const float* w = f.wpull + (dest / (u64)f.S) * PS;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+      const float v = acc[l * D + k];
+      if (v == 0.0f) continue;
+      const float wk = w[k];
+      if (wk != 0.0f) g[k] += (float)((double)v / (1.0 + (double)wk));
+    }
+  }
+}
+
+template <int D>
+static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
+  hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
+                     a.red_tot);
+  u32* start = a.red_tot + a.red_nb + 1;
+  hipLaunchKernelGGL(k_red_scatter<1>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
+                     kMvmGroupRows, static_cast<const void*>(a.red_pairs), a.red_count,
+                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
+  const int grid = ((a.red_nb + 7) / 8) * 8 * mvm_nsub(D);
+  MvmRedFinal f{a.grad, a.wpull, a.red_rowv, a.S, a.red_nb};
+  hipLaunchKernelGGL(k_mvm_red_sum<D>, dim3(grid), dim3(kRedBlock), 0, st,
+                     reinterpret_cast<const u64*>(a.red_sorted), static_cast<const u32*>(start), f);
+}
+
 template <bool kGrad>
 static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
+  const bool red = agg && a.red_pairs && a.red_rowv && a.red_nb > 0 &&
+                   a.red_nb <= kRedMaxBuckets && !mvm_atomics_forced();
   switch (a.model.v_dim) {
 #define XF_MVM_CASE(DD)                                                                  \
   case DD: {                                                                             \
     constexpr int B = mvm_block(DD);                                                     \
     const int g = (int)((a.batch.rows + B - 1) / B);                                     \
-    if (agg) hipLaunchKernelGGL((k_mvm2<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);  \
-    else hipLaunchKernelGGL((k_mvm2<DD, kGrad, false>), dim3(g), dim3(B), 0, st, a);     \
+    if (red) {                                                                           \
+      constexpr int R = kMvmGroupRows;                                                   \
+      const int gr = (int)((a.batch.rows + R - 1) / R);                                  \
+      hipLaunchKernelGGL((k_mvm2<DD, kGrad, false, true>), dim3(gr), dim3(R), 0, st, a); \
+      launch_mvm_reduction<DD>(a, gr, st);                                               \
+    } else if (agg) {                                                                    \
+      hipLaunchKernelGGL((k_mvm2<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);         \
+    } else {                                                                             \
+      hipLaunchKernelGGL((k_mvm2<DD, kGrad, false>), dim3(g), dim3(B), 0, st, a);        \
+    }                                                                                    \
     break;                                                                               \
   }
     XF_MVM_CASE(1) XF_MVM_CASE(2) XF_MVM_CASE(4) XF_MVM_CASE(8) XF_MVM_CASE(10) XF_MVM_CASE(16)

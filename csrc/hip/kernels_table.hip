@@ -910,8 +910,8 @@ void launch_bucket(const BucketArgs& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 __global__ void k_scatter_rows(const float* __restrict__ src, float* __restrict__ dst,
                                const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
-                               int width) {
-  int64_t n = dev_count(n_dev, n_max, n_max) * width;
+                               int width, float* __restrict__ zero_out) {
+  const int64_t rows = dev_count(n_dev, n_max, n_max), n = rows * width;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
     int64_t i = e / width;
@@ -919,6 +919,9 @@ __global__ void k_scatter_rows(const float* __restrict__ src, float* __restrict_
     int64_t r = map ? (int64_t)map[i] : i;
     dst[r * width + c] = src[e];
   }
+  if (zero_out)  // the send buffer the reduction fills next (saves a memset launch)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += stride)
+      zero_out[i] = 0.0f;
 }
 
 __global__ void k_gather_rows(const float* __restrict__ src, float* __restrict__ dst,
@@ -955,10 +958,10 @@ __global__ void k_scatter_u32(const u32* __restrict__ src, u32* __restrict__ dst
 }
 
 void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
-                         int64_t n_max, int width, hipStream_t st) {
+                         int64_t n_max, int width, float* zero_out, hipStream_t st) {
   if (n_max <= 0) return;
   hipLaunchKernelGGL(k_scatter_rows, dim3(grid_for(n_max * width)), dim3(kBlock), 0, st, src, dst,
-                     map, n_dev, n_max, width);
+                     map, n_dev, n_max, width, zero_out);
   XF_HIP_CHECK(hipGetLastError());
 }
 

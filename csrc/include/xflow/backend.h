@@ -104,6 +104,10 @@ struct FwdArgs {
   // Σ loss*vsum) in the first two floats of each gradient row; the apply
   // expands them with the key's pre-step weights (ApplyArgs::fm_compact).
   bool fm_compact = false;
+  // MVM on the reduction path: a dup-free row's occurrence gradient is
+  // loss*M_k/(1+v_ik), so records are (dest | row << 32), red_rowv[row] holds
+  // T = loss*M ([rows][pstride]) and the sum divides Σ T by (1 + v) per key.
+  float* red_rowv = nullptr;
 };
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
@@ -111,6 +115,7 @@ constexpr int kRedMaxBuckets = 4096;
 constexpr int red_shift(int nv) { return nv == 1 ? kRedShift : kRedShift - 1; }
 constexpr int kLrGroupRows = 1024;  // rows per LR workgroup on the reduction path
 constexpr int kFmGroupRows = 512;   // rows per reference-FM workgroup on the reduction path
+constexpr int kMvmGroupRows = 256;  // rows per MVM workgroup on the reduction path
 
 struct PullArgs {
   TableView table;
@@ -237,8 +242,10 @@ class Backend {
   }
   virtual void gather_grads(const GatherGradArgs& a) = 0;
   // rows of `width` floats: dst[map? map[i] : i] = src[i]   (scatter)
+  // (zero_out: also zero zero_out[0..n), the direct send buffer)
   virtual void scatter_rows(const float* src, float* dst, const u32* map,
-                            const int64_t* n_dev, int64_t n_max, int width) = 0;
+                            const int64_t* n_dev, int64_t n_max, int width,
+                            float* zero_out = nullptr) = 0;
   // dst[i] = src[map[i]]; optionally zero the source row   (gather)
   virtual void gather_rows(const float* src, float* dst, const u32* map,
                            const int64_t* n_dev, int64_t n_max, int width,

@@ -112,7 +112,8 @@ class Engine {
   const int32_t* slice_rows_dev(const BatchView& b, int S);
   // parts > 1: owner-partitioned scratch (ScratchView::parts); uniq_keys_out
   // redirects the unique-key list (the sharded step's send buffer)
-  void dedup_(const BatchView& b, int parts = 1, u64* uniq_keys_out = nullptr);
+  void dedup_(const BatchView& b, int parts = 1, u64* uniq_keys_out = nullptr,
+              bool want_inv = false);
   const u32* send_map_ = nullptr;  // send order -> scratch slot (send_pos_ or uniq_pos_)
 
   EngineConfig cfg_;
@@ -138,6 +139,7 @@ class Engine {
   u32* red_hist_ = nullptr;
   u32* red_tot_ = nullptr;
   u32* red_count_ = nullptr;
+  float* red_rowv_ = nullptr;    // MVM: per-row loss*M (FwdArgs::red_rowv)
   int red_nb_ = 0;
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare

@@ -23,34 +23,35 @@ CASES = [
 ]
 
 
-def _batch(layout, rows, step):
+def _batch(layout, rows, step, fields=6):
     """CSR (variable rows) or fixed-width rows stored row-major / field-major."""
     fixed = layout != "csr"
-    keys, rp, fg, lab = random_csr(rows, fields=6, vocab=60, seed=100 + step, variable=not fixed)
+    keys, rp, fg, lab = random_csr(rows, fields=fields, vocab=60, seed=100 + step,
+                                   variable=not fixed)
     return keys, rp, fg, lab
 
 
 def _run(device, kind, opt, fm_math, mvm_math, slices, steps=3, rows=96, v_dim=4,
-         layout="csr"):
+         layout="csr", fields=6, v_scale=1e-2):
     m = ModelConfig(kind=kind, v_dim=v_dim, fm_math=fm_math, mvm_math=mvm_math)
-    o = OptimConfig(kind=opt)
+    o = OptimConfig(kind=opt, v_init_scale=v_scale)
     eng = Engine(m, o, EngineConfig(table_log2_cap=14, max_rows=rows, max_nnz=rows * 16,
                                     max_slices=slices), device=device)
     P = m.params_per_key
     ref = torch_ref.RefTable(P, 0 if kind == "mvm" else 1, opt,
-                             init_fn=lambda k, d: normal_init(k, d) * np.float32(1e-2))
+                             init_fn=lambda k, d: normal_init(k, d) * np.float32(v_scale))
     slice_rows = rows // slices
     for step in range(steps):
-        keys, rp, fg, lab = _batch(layout, rows, step)
+        keys, rp, fg, lab = _batch(layout, rows, step, fields)
         b = to_batch(keys, rp, fg, lab, device, slice_rows=slice_rows)
         if layout != "csr":
-            b.row_ptr, b.nnz_per_row = None, 6
+            b.row_ptr, b.nnz_per_row = None, fields
             if layout == "field":
                 b = b.to_field_major()
         eng.train_step(b)
         torch_ref.train_step(ref, kind, keys, lab, rp, slice_rows, fg, fm_math, mvm_math)
     # all keys seen
-    allk = np.unique(np.concatenate([_batch(layout, rows, s)[0] for s in range(steps)]))
+    allk = np.unique(np.concatenate([_batch(layout, rows, s, fields)[0] for s in range(steps)]))
     got = eng.pull(allk)
     want = ref.weights(allk, insert=False).numpy()
     assert eng.table_size() == len(allk)
@@ -92,6 +93,34 @@ def test_fixed_width_layouts_cpu(kind, opt, fm_math, mvm_math, slices, layout):
 def test_fixed_width_layouts_gpu(gpu_device, kind, opt, fm_math, mvm_math, slices, layout):
     got, want, _ = _run(gpu_device, kind, opt, fm_math, mvm_math, slices, layout=layout)
     np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+
+
+# MVM with O(1) latent init and few fields: the field product stays far from
+# zero, so the gradients are large enough to move the weights (with the default
+# 1e-2 init, FTRL's L1 zeroes every touched v after its first update and the
+# comparison above could not see a wrong MVM gradient).  Covers the GPU
+# reduction path (dup-free rows: (dest, row) records; rows with a repeated
+# field in the CSR layout: atomics).
+MVM_LIVE = [("compat", 1, "csr"), ("fixed", 2, "csr"), ("compat", 1, "field"),
+            ("fixed", 1, "fixed")]
+
+
+def _mvm_live(device, mvm_math, slices, layout):
+    got, want, _ = _run(device, "mvm", "ftrl", "reference", mvm_math, slices, layout=layout,
+                        fields=4, v_scale=1.0)
+    assert np.abs(want).max() > 1e-2  # the weights did move
+    np.testing.assert_allclose(got, want, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("mvm_math,slices,layout", MVM_LIVE)
+def test_mvm_live_gradients_cpu(mvm_math, slices, layout):
+    _mvm_live(torch.device("cpu"), mvm_math, slices, layout)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mvm_math,slices,layout", MVM_LIVE)
+def test_mvm_live_gradients_gpu(gpu_device, mvm_math, slices, layout):
+    _mvm_live(gpu_device, mvm_math, slices, layout)
 
 
 @pytest.mark.gpu
