@@ -1,4 +1,5 @@
 // xflow-amd: Engine implementation (device agnostic; talks to a Backend).
+#include <cstdlib>
 #include "xflow/engine.h"
 
 #include <cstdio>
@@ -123,7 +124,7 @@ Engine::~Engine() {
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_, inv_, red_rowv_};
+                  red_tot_, red_count_, inv_, red_rowv_, lr_grad_, lr_nz_};
   for (void* p : ptrs) be.free(p);
 }
 
@@ -185,13 +186,34 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 
+// XFLOW_LR_SLOT_GRADS=1: LR-FTRL fused step with slot-indexed gradients and
+// a table re-read in the apply (the pre-stash path; A/B and fallback tests)
+static bool lr16_disabled() {
+  static const bool off = std::getenv("XFLOW_LR_SLOT_GRADS") != nullptr;
+  return off;
+}
+
 void Engine::train_step(const BatchView& b) {
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
-  dedup_(b);
+  // LR-FTRL on 16-byte slots, one slice, bucket reduction: the reduction
+  // writes normalised gradients in unique order (through the compaction's
+  // slot -> unique index map) and the apply takes (n, z) from the pull, so it
+  // reads nothing at random and writes the slot once.
+  const TableLayout& L = table_.L;
+  const bool lr16 = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 && L.P == 1 &&
+                    L.opt == kFTRL && !L.has_flag && S == 1 && red_pairs_ &&
+                    (double)scratch_.cap < 4294967295.0 && !lr16_disabled();
+  if (lr16) {
+    if (!inv_) inv_ = balloc<u32>(*be_, scratch_.cap);
+    if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz);
+    if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
+  }
+  dedup_(b, 1, nullptr, lr16);
+  inv_valid_ = false;  // (the sharded step's send order is not this one)
 
   PullArgs pa;
   pa.table = table_;
@@ -204,6 +226,10 @@ void Engine::train_step(const BatchView& b) {
   pa.out_vals = wpull_;
   pa.out_map = uniq_pos_;
   pa.pstride = ps;
+  if (lr16) {
+    pa.out_nz = lr_nz_;
+    pa.zero_out = lr_grad_;
+  }
   be_->table_pull(pa);
 
   if (masks) be_->slice_masks(b, pos_, tmask_);
@@ -221,6 +247,11 @@ void Engine::train_step(const BatchView& b) {
   // reference-math FM on the GPU reduction path: (B, C) rows, expanded by the apply
   fa.fm_compact = fa.red_pairs && fa.agg_ok && cfg_.model.kind == kFM &&
                   cfg_.model.fm_math == kFmReference;
+  if (lr16) {
+    fa.red_out = lr_grad_;
+    fa.red_inv = inv_;
+    fa.red_rows = srows;
+  }
   be_->forward_backward(fa);
 
   ApplyArgs aa;
@@ -242,6 +273,13 @@ void Engine::train_step(const BatchView& b) {
   aa.slice_rows = srows;
   aa.fm_compact = fa.fm_compact;
   aa.fm_D = cfg_.model.v_dim;
+  if (lr16) {  // unique-order, already normalised, zeroed by the next pull
+    aa.grads = lr_grad_;
+    aa.grad_map = nullptr;
+    aa.zero_after = false;
+    aa.slice_rows = nullptr;
+    aa.nz_stash = lr_nz_;
+  }
   be_->table_apply(aa);
 }
 

@@ -448,7 +448,9 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
                                                       int64_t n_max, bool insert,
                                                       u32* __restrict__ out_slot,
                                                       float* __restrict__ out_vals,
-                                                      const u32* __restrict__ out_map) {
+                                                      const u32* __restrict__ out_map,
+                                                      float2* __restrict__ out_nz,
+                                                      float* __restrict__ zero_out) {
   const int64_t n = dev_count(n_dev, n_host, n_max);
   const u64 mask = t.cap - 1;
   uint4* slots = reinterpret_cast<uint4*>(t.words);
@@ -473,13 +475,15 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
     if (i >= n) continue;
     u32 slot = kNoSlot;
     float w = 0.0f;
+    float2 nz = make_float2(0.0f, 0.0f);  // fresh slot: zero state
     u64 sj = s[j];
     uint4 vj = v[j];
     for (u64 c = 0; c < t.cap; ++c) {
       u64 cur = (u64)vj.x | ((u64)vj.y << 32);
       if (cur == key[j]) {
         slot = (u32)sj;
-        w = ftrl_weight(__uint_as_float(vj.w), __uint_as_float(vj.z), fp);
+        nz = make_float2(__uint_as_float(vj.z), __uint_as_float(vj.w));
+        w = ftrl_weight(nz.y, nz.x, fp);
         break;
       }
       if (cur == kEmptyKey) {
@@ -499,6 +503,8 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
     if (insert && slot == kNoSlot) *t.overflow = 1u;
     if (out_slot) out_slot[i] = slot;
     if (out_vals) out_vals[out_map ? out_map[i] : i] = w;
+    if (out_nz) out_nz[i] = nz;
+    if (zero_out) zero_out[i] = 0.0f;
   }
   block_count_add<kBlock>(t.size, claims);
 }
@@ -592,7 +598,8 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
     int64_t nm = a.n_dev ? a.n_max : a.n_host;
     int g = (int)((nm + kPullChunk - 1) / kPullChunk);
     hipLaunchKernelGGL(k_pull_lr16, dim3(g > 0 ? g : 1), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
-                       a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map);
+                       a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map,
+                       reinterpret_cast<float2*>(a.out_nz), a.zero_out);
   } else if (a.out_slot && a.pstride >= 2 && a.pstride <= 64) {
     int64_t nm = a.n_dev ? a.n_max : a.n_host;
     int g1 = (int)((nm + kPullChunk - 1) / kPullChunk);
@@ -641,7 +648,8 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
     if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
     if (slot == kNoSlot) continue;
     float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
-    float2 nz = *st;
+    // (n, z) as pulled this step: coalesced, instead of a second random read
+    float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
     float w = ftrl_weight(nz.y, nz.x, fp);
     float g = norm_grad(raw, a.slice_rows, 0);
     ftrl_push(nz.x, nz.y, w, g, fp);

@@ -129,6 +129,11 @@ struct PullArgs {
   float* out_vals = nullptr;       // rows of pstride floats
   const u32* out_map = nullptr;    // row index for entry i (null => i)
   int pstride = 1;
+  // LR-FTRL 16-byte slots, fused step: the (n, z) each key was pulled with,
+  // in unique order (read back by the apply instead of the table), and a
+  // unique-order gradient buffer to zero for the reduction's direct writes.
+  float* out_nz = nullptr;         // [n][2]
+  float* zero_out = nullptr;       // [n]
 };
 
 struct ApplyArgs {
@@ -155,6 +160,10 @@ struct ApplyArgs {
   // g_w = D*B, g_v[k] = C - v_k*B with v_k the key's pre-step (pulled) value.
   bool fm_compact = false;
   int fm_D = 0;
+  // LR-FTRL 16-byte slots: (n, z) of entry i as pulled this step (PullArgs::
+  // out_nz); the slot is then only written.  Valid while no other push to
+  // the key intervenes (the fused single-source step).
+  const float* nz_stash = nullptr;
   // Optional fused reset of the worker dedup scratch (single-device path).
   ScratchView scratch;
   const u32* reset_pos = nullptr;

@@ -140,6 +140,8 @@ class Engine {
   u32* red_tot_ = nullptr;
   u32* red_count_ = nullptr;
   float* red_rowv_ = nullptr;    // MVM: per-row loss*M (FwdArgs::red_rowv)
+  float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz]
+  float* lr_nz_ = nullptr;       // LR-FTRL fused step: pulled (n, z) [max_nnz][2]
   int red_nb_ = 0;
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
