@@ -449,6 +449,7 @@ void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, 
 void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert, int buf) {
   ensure_server_capacity(n, buf);
   srv_n_[buf] = n;
+  srv_vals_[buf] = out_vals;
   if (n == 0) return;
   PullArgs pa;
   pa.table = table_;
@@ -489,6 +490,9 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
+  fa.fm_compact = sharded_fm_compact() && fa.agg_ok;
+  if (sharded_fm_compact() && !fa.fm_compact)
+    throw std::logic_error("w_forward_backward: compact FM rows need the reduction path");
   if (direct) {
     if (!fa.red_pairs || !fa.agg_ok) throw std::logic_error("direct send path without reduction");
     // the bucket reduction writes the normalised send buffer (no gather)
@@ -510,6 +514,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   ga.S = S;
   ga.pstride = ps;
   ga.slice_rows = srows;
+  ga.width = grad_width();
   ga.out = grads_out;
   ga.out_mask = masks ? masks_out : nullptr;
   be_->gather_grads(ga);
@@ -532,7 +537,14 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
     aa.slots = srv_slots_[buf] + off;
     aa.n_host = cnt;
     aa.n_max = cnt;
-    aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * ps;
+    const int gw = grad_width();
+    aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * gw;
+    aa.gstride = gw;
+    if (sharded_fm_compact()) {
+      aa.fm_compact = true;
+      aa.fm_D = cfg_.model.v_dim;
+      aa.pulled = srv_vals_[buf] + off * (int64_t)ps;
+    }
     aa.masks = recv_masks ? recv_masks + off : nullptr;
     aa.zero_after = false;
     aa.S = S;

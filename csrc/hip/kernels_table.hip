@@ -707,7 +707,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   static_assert(G <= kWave, "a key's lanes must share a wave");
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
-  const int S = a.S, ps = a.pstride;
+  const int S = a.S, ps = a.pstride, gs = a.gstride ? a.gstride : ps;
   const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
   const int p = threadIdx.x % G;
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
@@ -715,7 +715,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
     const u32 slot = a.slots[i];
     XF_DASSERT(slot == kNoSlot || slot < a.table.cap);
     const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
-    float* g = a.grads + (size_t)row * S * ps;
+    float* g = a.grads + (size_t)row * S * gs;
     const u32 m = a.masks ? a.masks[row] : all;
     if (slot != kNoSlot && p < L.P) {
       u32* sp = a.table.words + (u64)slot * L.stride;
@@ -746,10 +746,11 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
       };
       // compact reference-math FM rows (B, C): expand with the pre-step
       // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
-      const float w_pre = a.fm_compact ? weight() : 0.0f;
+      const float w_pre =
+          a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : weight()) : 0.0f;
       auto raw_of = [&](int s) -> float {
-        if (!a.fm_compact) return g[s * ps + p];
-        const float Bv = g[s * ps], Cv = g[s * ps + 1];
+        if (!a.fm_compact) return g[s * gs + p];
+        const float Bv = g[s * gs], Cv = g[s * gs + 1];
         return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
       };
       if (a.sum_slices) {
@@ -766,7 +767,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
       if (L.has_flag && p == 0 && m) sp[L.flag_word] = 1u;
     }
     if (a.zero_after && p < (a.fm_compact ? 2 : ps)) {
-      for (int s = 0; s < S; ++s) g[s * ps + p] = 0.0f;
+      for (int s = 0; s < S; ++s) g[s * gs + p] = 0.0f;
       if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }
   }
@@ -809,14 +810,14 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
 __global__ void __launch_bounds__(kBlock) k_gather_grads(GatherGradArgs a) {
   int64_t n = dev_count(a.n_dev, a.n_max, a.n_max);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int S = a.S, ps = a.pstride, W = S * ps;
+  const int S = a.S, ps = a.pstride, W = S * ps, wd = a.width ? a.width : ps;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     u32 row = a.map[i];
     float* src = a.grad_rw + (size_t)row * W;
-    float* dst = a.out + (size_t)i * W;
+    float* dst = a.out + (size_t)i * S * wd;
     for (int s = 0; s < S; ++s)
-      for (int p = 0; p < ps; ++p) {
-        dst[s * ps + p] = norm_grad(src[s * ps + p], a.slice_rows, s);
+      for (int p = 0; p < wd; ++p) {
+        dst[s * wd + p] = norm_grad(src[s * ps + p], a.slice_rows, s);
         src[s * ps + p] = 0.0f;
       }
     if (a.tmask_rw) {

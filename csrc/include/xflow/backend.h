@@ -164,6 +164,12 @@ struct ApplyArgs {
   // out_nz); the slot is then only written.  Valid while no other push to
   // the key intervenes (the fused single-source step).
   const float* nz_stash = nullptr;
+  // floats per (row, slice) in grads (0 => pstride; 2 for compact FM rows)
+  int gstride = 0;
+  // fm_compact with several sources per step: the values this rank's pull
+  // served for entry i ([n][pstride], the workers' pre-step weights), since
+  // the table already holds the previous sources' updates.  Null: the table.
+  const float* pulled = nullptr;
   // Optional fused reset of the worker dedup scratch (single-device path).
   ScratchView scratch;
   const u32* reset_pos = nullptr;
@@ -180,8 +186,9 @@ struct GatherGradArgs {           // worker: pos-indexed raw sums -> send order
   int S = 1;
   int pstride = 1;
   const int32_t* slice_rows = nullptr;  // [S]
-  float* out = nullptr;            // [n][S*pstride] normalised gradients
+  float* out = nullptr;            // [n][S*width] normalised gradients
   u32* out_mask = nullptr;         // [n] (when tmask)
+  int width = 0;                   // values per (key, slice) gathered (0 => pstride)
 };
 
 struct BucketArgs {                // group unique keys by owning rank

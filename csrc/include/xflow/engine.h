@@ -91,6 +91,10 @@ class Engine {
   // exactly non-zero (key, param) weights of this table shard (L1 sparsity)
   int64_t nonzero_weights() { return be_->table_nonzero(table_, cfg_.opt); }
   int pstride() const { return cfg_.model.pstride(); }
+  // floats per (key, slice) in the multi-rank gradient exchange: pstride, or
+  // 2 for reference-math FM on the GPU reduction path ((B, C) rows, expanded
+  // by the owner with the values it served)
+  int grad_width() const { return sharded_fm_compact() ? 2 : pstride(); }
   int slices_of(const BatchView& b) const;
 
   // ---- checkpoint ------------------------------------------------------
@@ -115,6 +119,11 @@ class Engine {
   void dedup_(const BatchView& b, int parts = 1, u64* uniq_keys_out = nullptr,
               bool want_inv = false);
   const u32* send_map_ = nullptr;  // send order -> scratch slot (send_pos_ or uniq_pos_)
+  bool sharded_fm_compact() const {
+    return red_pairs_ && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference &&
+           (double)scratch_.cap * cfg_.max_slices * pstride() < 4294967295.0;
+  }
+  const float* srv_vals_[2] = {nullptr, nullptr};  // s_pull outputs (fm_compact apply)
 
   EngineConfig cfg_;
   std::unique_ptr<Backend> be_;

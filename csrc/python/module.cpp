@@ -172,6 +172,7 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_property_readonly("is_gpu", &Engine::is_gpu)
       .def_property_readonly("backend_name", [](Engine& e) { return e.backend().name(); })
       .def_property_readonly("pstride", &Engine::pstride)
+      .def_property_readonly("grad_width", &Engine::grad_width)
       .def_property_readonly("P", [](Engine& e) { return e.config().model.P(); })
       .def_property_readonly("state_words", &Engine::state_words)
       .def_property_readonly("table_capacity", &Engine::table_capacity)

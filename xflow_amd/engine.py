@@ -133,6 +133,11 @@ class Engine:
         return int(self._e.pstride)
 
     @property
+    def grad_width(self) -> int:
+        """Floats per (key, slice) in the multi-rank gradient exchange."""
+        return int(self._e.grad_width)
+
+    @property
     def params_per_key(self) -> int:
         return int(self._e.P)
 

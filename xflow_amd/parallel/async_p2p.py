@@ -75,7 +75,7 @@ class AsyncShardedEngine(ShardedEngine):
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.pstride
-        W = S * ps
+        W = S * e.grad_width
         ordered_masks = S > 1 and not e.cfg.sum_slices
         buf = self._parity
         send_splits, recv_splits, recv_keys = self._exchange_keys(batch, prefetch)

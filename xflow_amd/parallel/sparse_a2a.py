@@ -79,7 +79,9 @@ class ShardedEngine:
         self.recv_counts = self._counts_both[self.world:]
         self.send_keys = torch.empty(max(engine.cfg.max_nnz, 1), dtype=torch.int64, device=dev)
         self._recv_keys = _Buf(torch.int64, dev)
-        self._vals_out = _Buf(torch.float32, dev)
+        # one per server buffer: compact-FM applies read the values served
+        # by their step's pull (the async step applies after the next pull)
+        self._vals_out = [_Buf(torch.float32, dev), _Buf(torch.float32, dev)]
         self._pulled = _Buf(torch.float32, dev)
         self._grads_out = _Buf(torch.float32, dev)
         self._grads_in = _Buf(torch.float32, dev)
@@ -200,7 +202,7 @@ class ShardedEngine:
         e = self.engine
         ps = e.pstride
         n_send, n_recv = sum(send_splits), sum(recv_splits)
-        vals = self._vals_out.get(n_recv * ps).view(n_recv, ps)
+        vals = self._vals_out[buf].get(n_recv * ps).view(n_recv, ps)
         e.s_pull(recv_keys, n_recv, vals, insert=insert, buf=buf)
         pulled = self._pulled.get(n_send * ps).view(n_send, ps)
         self._a2a(pulled, vals, send_splits, recv_splits)
@@ -219,7 +221,7 @@ class ShardedEngine:
         n_send, n_recv = self.last_send, self.last_recv
         pulled = self._pull(recv_keys, send_splits, recv_splits, insert=True)
 
-        W = S * ps
+        W = S * e.grad_width  # (B, C) per slice for reference-math FM on the GPU
         grads_out = self._grads_out.get(n_send * W).view(n_send, W)
         masks_out = self._masks_out.get(n_send) if ordered_masks else None
         e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S)
@@ -234,7 +236,7 @@ class ShardedEngine:
             offsets.append(offsets[-1] + int(c))
         e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
         e.w_finish()
-        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)
+        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)  # W = S * grad_width
 
     def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward-only sharded step (keys looked up, never inserted).  Every
