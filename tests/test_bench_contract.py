@@ -1,0 +1,53 @@
+"""bench.py driver contract, exercised on the CPU backend: one JSON line from
+rank 0 with the whole-job aggregate, launched plain (N=1) and under
+torch.distributed.run (N=2, gloo) exactly as the round driver launches the
+multi-GPU scaling run (the N>1 path is the sharded table + sparse all-to-all
+step of xflow_amd/parallel/sparse_a2a.py)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+        "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(n, extra):
+    args = ["--gpus", str(n), "--steps", "2", "--warmup", "1", "--cpu"] + extra
+    if n == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py")] + args
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n,extra", [(1, []), (2, []), (2, ["--model", "fm", "--v-dim", "8"])])
+def test_bench_json_line(n, extra):
+    d = _run(n, extra)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    cfg = d["config"]
+    assert cfg["global_batch"] == cfg["rows_per_gpu"] * n
+    assert cfg["parallelism"].startswith(f"dp{n}")
+    # whole-job aggregate: samples over the slowest rank's time
+    assert d["value"] == pytest.approx(cfg["global_batch"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3),
+                                       rel=1e-6)
+    assert 0.0 < d["logloss"] < 1.0 and d["table_keys"] > 0
