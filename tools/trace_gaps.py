@@ -2,10 +2,12 @@
 """Timeline summary of a rocprofv3 kernel trace: GPU busy vs idle time and the
 idle gaps that follow each kernel (the host-side stalls between launches).
 
-    python tools/trace_gaps.py gpurun_out/prof_x/run_kernel_trace.csv [--last N]
+    python tools/trace_gaps.py gpurun_out/prof_x/run_kernel_trace.csv [--skip F]
+    python tools/trace_gaps.py <trace> --marker k_synth --steps 18
 
---last N restricts the analysis to the last N dispatches of the most frequent
-kernel's period (the timed steps), so warmup and setup are excluded.
+--skip drops the first fraction of the trace (warmup, setup); --marker instead
+cuts the trace at the dispatches of the step's first kernel and analyses the
+last --steps complete steps (and prints the last one's timeline).
 """
 from __future__ import annotations
 
@@ -20,6 +22,10 @@ def main():
     ap.add_argument("--skip", type=float, default=0.3,
                     help="fraction of the trace (by time) to skip as warmup")
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--marker", default="",
+                    help="kernel that opens a step (e.g. k_synth): analyse the last --steps "
+                         "complete steps only and print the last step's timeline")
+    ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -28,9 +34,21 @@ def main():
     rows.sort()
     if not rows:
         return
-    t0, t1 = rows[0][0], max(r[1] for r in rows)
-    cut = t0 + a.skip * (t1 - t0)
-    rows = [r for r in rows if r[0] >= cut]
+    if a.marker:
+        starts = [i for i, r in enumerate(rows) if a.marker in r[2]]
+        if len(starts) < 2:
+            raise SystemExit(f"fewer than two '{a.marker}' dispatches")
+        k = min(a.steps, len(starts) - 1)
+        lo, hi = starts[-1 - k], starts[-1]
+        print(f"{k} steps: {(rows[hi][0] - rows[lo][0]) / 1e3 / k:.1f} us/step (marker to marker)")
+        print("-- last step timeline (start us, duration us)")
+        for s, e, n in rows[starts[-2]:hi]:
+            print(f"  {(s - rows[starts[-2]][0]) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {n}")
+        rows = rows[lo:hi]
+    else:
+        t0, t1 = rows[0][0], max(r[1] for r in rows)
+        cut = t0 + a.skip * (t1 - t0)
+        rows = [r for r in rows if r[0] >= cut]
     busy = collections.Counter()
     gaps = collections.Counter()
     ngap = collections.Counter()
