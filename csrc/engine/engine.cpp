@@ -122,7 +122,7 @@ Engine::~Engine() {
                   scratch_.claims, block_counts_, pos_, uniq_keys_,
                   uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
                   bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
-                  srv_slots_[0], srv_slots_[1], host_keys_dev_, host_vals_dev_,
+                  srv_slots_[0], srv_slots_[1], srv_nz_[0], srv_nz_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, inv_, red_rowv_, lr_grad_, lr_nz_};
   for (void* p : ptrs) be.free(p);
@@ -194,6 +194,7 @@ static bool lr16_disabled() {
 }
 
 void Engine::train_step(const BatchView& b) {
+  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
   const int ps = pstride();
@@ -311,6 +312,7 @@ void Engine::eval_step(const BatchView& b, float* pctr) {
 }
 
 void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& grads) {
+  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
   const int64_t n = (int64_t)keys.size();
   const int P = cfg_.model.P();
   if ((int64_t)grads.size() != n * P) throw std::invalid_argument("push_host: grads != keys*P");
@@ -428,8 +430,17 @@ void Engine::ensure_server_capacity(int64_t n, int buf) {
   if (n <= srv_cap_[buf]) return;
   be_->synchronize();
   be_->free(srv_slots_[buf]);
+  be_->free(srv_nz_[buf]);
+  srv_nz_[buf] = nullptr;
   srv_cap_[buf] = n + n / 4 + 1024;
   srv_slots_[buf] = balloc<u32>(*be_, srv_cap_[buf]);
+  if (lr16_layout()) srv_nz_[buf] = balloc<float>(*be_, 2 * (size_t)srv_cap_[buf]);
+}
+
+bool Engine::lr16_layout() const {
+  const TableLayout& L = table_.L;
+  return be_->is_gpu() && L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag &&
+         !lr16_disabled();
 }
 
 void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr) {
@@ -461,6 +472,8 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
   pa.out_slot = srv_slots_[buf];
   pa.out_vals = out_vals;
   pa.pstride = pstride();
+  pa.out_nz = srv_nz_[buf];
+  srv_nz_fresh_[buf] = srv_nz_[buf] != nullptr;
   be_->table_pull(pa);
 }
 
@@ -525,6 +538,10 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
                      const std::vector<int64_t>& src_offsets, int S, int buf) {
   if (buf < 0 || buf > 1) throw std::invalid_argument("server buffer must be 0 or 1");
   const int ps = pstride();
+  // the first source applied sees the state its pull saw; a key sent by
+  // several sources is updated by the earlier ones, so later sources re-read
+  bool stash = srv_nz_fresh_[buf];
+  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;
   for (size_t src = 0; src + 1 < src_offsets.size(); ++src) {
     int64_t off = src_offsets[src];
     int64_t cnt = src_offsets[src + 1] - off;
@@ -546,6 +563,8 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
       aa.pulled = srv_vals_[buf] + off * (int64_t)ps;
     }
     aa.masks = recv_masks ? recv_masks + off : nullptr;
+    if (stash) aa.nz_stash = srv_nz_[buf] + 2 * off;
+    stash = false;
     aa.zero_after = false;
     aa.S = S;
     aa.pstride = ps;
@@ -659,6 +678,7 @@ void Engine::export_table(std::vector<u64>& keys, std::vector<u32>& words) {
 }
 
 void Engine::import_table(const std::vector<u64>& keys, const std::vector<u32>& words) {
+  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
   const int W = state_words();
   const int64_t n = (int64_t)keys.size();
   if ((int64_t)words.size() != n * W) throw std::invalid_argument("import_table: size mismatch");

@@ -175,6 +175,12 @@ class Engine {
   u32* srv_slots_[2] = {nullptr, nullptr};
   int64_t srv_cap_[2] = {0, 0};
   int64_t srv_n_[2] = {0, 0};
+  // LR-FTRL 16-byte slots: (n, z) as pulled into each buffer, and whether no
+  // apply has touched the table since that pull (then the first source's
+  // apply takes its state from here instead of re-reading the table)
+  float* srv_nz_[2] = {nullptr, nullptr};
+  bool srv_nz_fresh_[2] = {false, false};
+  bool lr16_layout() const;
 
   u64* host_keys_dev_ = nullptr;   // push_host / pull_host staging
   float* host_vals_dev_ = nullptr;
