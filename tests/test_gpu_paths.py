@@ -172,3 +172,35 @@ def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind):
     k = np.concatenate(allk)
     assert len(np.unique(k)) == len(k) == ref.table_size()
     np.testing.assert_allclose(np.concatenate(allv), ref.pull(k), rtol=1e-4, atol=1e-6)
+
+
+def test_async_staleness_one_on_gpu_matches_simulation(gpu_device, nccl_group):
+    """Config 4 on the HIP backend (1-rank RCCL group): AsyncShardedEngine ==
+    the reference step whose pulls miss exactly the previous step's pushes.
+    Also pins the owner apply's (n, z) stash: the staleness-1 step applies a
+    buffer after the other buffer's pull and apply, so it must re-read."""
+    from xflow_amd.parallel.async_p2p import AsyncShardedEngine
+    from xflow_amd.testing import torch_ref
+    from xflow_amd.testing.hashing import normal_init
+
+    rows, steps = 64, 4
+    eng = Engine(ModelConfig(kind="lr", v_dim=4), OptimConfig(),
+                 EngineConfig(table_log2_cap=14, max_rows=rows, max_nnz=rows * 16),
+                 device=gpu_device)
+    sh = AsyncShardedEngine(eng)
+    data = [random_csr(rows, 6, 80, seed=1000 * s) for s in range(steps)]
+    for k, rp, fg, lab in data:
+        sh.train_step(to_batch(k, rp, fg, lab, gpu_device), S=1)
+    sh.flush()
+    torch.cuda.synchronize()
+    ref = torch_ref.RefTable(1, 1, "ftrl", init_fn=lambda k, d: normal_init(k, d) * 1e-2)
+    pending = None
+    for k, rp, fg, lab in data:
+        _, cur = torch_ref.compute_step(ref, "lr", k, lab, rp.astype(np.int32), rows)
+        if pending is not None:
+            torch_ref.apply_step(ref, pending)
+        pending = cur
+    torch_ref.apply_step(ref, pending)
+    keys, _ = eng.export_table()
+    np.testing.assert_allclose(eng.pull(keys), ref.weights(keys, insert=False).numpy(),
+                               rtol=1e-4, atol=1e-6)
