@@ -283,14 +283,24 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
   unsigned int tot;
   unsigned int ex = block_exclusive_scan<kBlock>(cnt, &tot);
   unsigned long long dst = (unsigned long long)offs[blockIdx.x] + ex;
+  u32 iv[kCompactItems];
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j) {
+    iv[j] = 0xFFFFFFFFu;
     if (!(hit & (1u << j))) continue;
     u64 s = base + (u64)j;
     uk[dst] = sv.keys[s];
     up[dst] = (u32)s;
-    if (inv) inv[s] = (u32)dst;
+    iv[j] = (u32)dst;
     ++dst;
+  }
+  // inv for all of the thread's slots as four dwordx4 stores (whole lines
+  // instead of ~10 % scattered dword stores); non-hit slots get a sentinel
+  if (inv && hit) {
+    uint4* ip = reinterpret_cast<uint4*>(inv + base);
+#pragma unroll
+    for (int j = 0; j < kCompactItems / 4; ++j)
+      ip[j] = make_uint4(iv[4 * j], iv[4 * j + 1], iv[4 * j + 2], iv[4 * j + 3]);
   }
   // rebuild decided by k_compact_scan: free this thread's slots of the new
   // capacity (its own slots, already read above)
