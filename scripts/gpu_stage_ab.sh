@@ -1,6 +1,7 @@
 #!/bin/bash
-# GPU tests of the current tree, ABAB of variants/base vs variants/stage, and
-# kernel stats of the current tree.
+# GPU tests of the current tree, ABAB of variants named in $ABV (default
+# "base stage"; create them first with scripts/make_variant.sh), and kernel
+# stats of the current tree.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
