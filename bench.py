@@ -57,12 +57,12 @@ def parse():
                          "traffic); 1.0 keeps it alive for measuring the backward")
     ap.add_argument("--lambda1", type=float, default=5e-5,
                     help="FTRL L1 (ftrl.h:19); config 4 reports the non-zero weight count")
-    ap.add_argument("--min-warmup-s", type=float, default=0.25,
-                    help="GPU: after the --warmup steps, keep stepping (untimed) until the warmup "
-                         "has lasted this long: a first process on an idle GPU otherwise "
-                         "times its first steps at idle clocks (seen once in five cold "
-                         "boxes: 315 vs 525 M samples/s).  The steps run are reported as "
-                         "warmup_steps_run; the timed region is still exactly --steps")
+    ap.add_argument("--clock-warmup-s", type=float, default=0.25,
+                    help="GPU: before the --warmup steps, keep the GPU busy for this long with a "
+                         "dense matmul that touches no engine state: a first process on an idle "
+                         "GPU otherwise times its first steps at idle clocks (seen once in five "
+                         "cold boxes: 315 vs 525 M samples/s).  Training warmup is exactly "
+                         "--warmup steps, so logloss/table_keys do not depend on the box")
     ap.add_argument("--overlap", choices=["on", "off"], default="off",
                     help="generate batch t+1 on a side stream while step t runs (measured on "
                          "one MI355X: 2-4%% slower for the fused and the multi-rank step, the "
@@ -142,23 +142,17 @@ def main():
         if world > 1:
             dist.barrier()
 
-    tw = time.perf_counter()
+    if use_gpu and a.clock_warmup_s > 0:
+        x = torch.randn(4096, 4096, device=device, dtype=torch.bfloat16)
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < a.clock_warmup_s:
+            for _ in range(8):
+                x = torch.mm(x, x).clamp_(-1.0, 1.0)
+            torch.cuda.synchronize(device)
+        del x
     for _ in range(a.warmup):
         step()
     sync()
-    warm_run = a.warmup
-    spent = time.perf_counter() - tw
-    if use_gpu and a.warmup > 0 and spent < a.min_warmup_s:
-        # every rank runs the same number of extra steps (lock-step collectives)
-        extra = min(2000, math.ceil((a.min_warmup_s - spent) / (spent / a.warmup)))
-        if world > 1:
-            t = torch.tensor([extra], dtype=torch.int64, device=device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            extra = int(t.item())
-        for _ in range(extra):
-            step()
-        sync()
-        warm_run += extra
     engine.read_stats(reset=True)
     sync()
     t0 = time.perf_counter()
@@ -171,7 +165,8 @@ def main():
     st = engine.read_stats(reset=True)
     tbl = engine.table_size()
     nnzw = engine.nonzero_weights() if a.async_p2p else 0
-    red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw)],
+    ovf = float(engine.overflowed())  # table probe wrap / dedup scratch overflow
+    red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw), ovf],
                        dtype=torch.float64, device=device)
     if world > 1:
         mx = red[:1].clone()
@@ -180,6 +175,9 @@ def main():
         elapsed = float(mx.item())
     vals = red.tolist()
     ln_loss, rows, table_keys, nonzero = vals[1], vals[2], vals[3], vals[4]
+    if vals[5] > 0:
+        raise SystemExit("bench: a table or dedup-scratch overflow was flagged (keys would be "
+                         "dropped or isolated): the result is invalid")
     samples = a.batch * a.steps * world
     if rank == 0:
         out = {
@@ -189,7 +187,6 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "warmup_steps_run": warm_run,
             "ms_per_step": 1000.0 * elapsed / a.steps,
             "higher_is_better": True,
             "scaling": "weak",
@@ -208,6 +205,7 @@ def main():
                        "input_overlap": overlap, "v_init_scale": a.v_init_scale},
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
+            "table_load": table_keys / float(world * 2 ** log2_cap),
         }
         if a.async_p2p:
             out["config"]["parallelism"] += "+async-p2p(staleness=1)"

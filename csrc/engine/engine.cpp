@@ -78,11 +78,15 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   send_pos_ = balloc<u32>(be, nnz);
   n_uniq_ = balloc<int64_t>(be, 1);
   be.memset(n_uniq_, 0, sizeof(int64_t));
-  wpull_ = balloc<float>(be, scratch_.cap * ps);
-  grad_ = balloc<float>(be, scratch_.cap * cfg_.max_slices * ps);
-  be.memset(grad_, 0, sizeof(float) * scratch_.cap * cfg_.max_slices * ps);
-  tmask_ = balloc<u32>(be, scratch_.cap);
-  be.memset(tmask_, 0, sizeof(u32) * scratch_.cap);
+  // slot-indexed buffers carry one extra row: the trash slot (index cap) that
+  // a dedup probe overflow sends its occurrences to (flagged, never applied)
+  const uint64_t rows1 = scratch_.cap + 1;
+  wpull_ = balloc<float>(be, rows1 * ps);
+  be.memset(wpull_ + scratch_.cap * ps, 0, sizeof(float) * ps);
+  grad_ = balloc<float>(be, rows1 * cfg_.max_slices * ps);
+  be.memset(grad_, 0, sizeof(float) * rows1 * cfg_.max_slices * ps);
+  tmask_ = balloc<u32>(be, rows1);
+  be.memset(tmask_, 0, sizeof(u32) * rows1);
   // atomic-free gradient reduction (FwdArgs::red_*): LR (1 value per key) and
   // reference-math FM (2 values per key, 16-byte records)
   const bool fm_ref = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference;
@@ -90,7 +94,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref || mvm)) {
     const int nv = fm_ref ? 2 : 1, shift = red_shift(nv);
     const int group_rows = fm_ref ? kFmGroupRows : (mvm ? kMvmGroupRows : kLrGroupRows);
-    const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
+    const uint64_t dests = (scratch_.cap + 1) * (uint64_t)cfg_.max_slices;  // + trash slot
     const int nb = (int)((dests + (1ull << shift) - 1) >> shift);
     if (nb <= kRedMaxBuckets) {
       const int64_t groups = (cfg_.max_rows + group_rows - 1) / group_rows;
@@ -162,6 +166,14 @@ const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
   return slice_rows_;
 }
 
+void Engine::ensure_inv() {
+  if (inv_) return;
+  // + the trash slot's entry (and padding to a 16-slot compaction group): no
+  // unique index, so reductions skip it
+  inv_ = balloc<u32>(*be_, scratch_.cap + 16);
+  be_->memset(inv_ + scratch_.cap, 0xFF, 16 * sizeof(u32));
+}
+
 void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want_inv) {
   if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
@@ -209,7 +221,7 @@ void Engine::train_step(const BatchView& b) {
                     L.opt == kFTRL && !L.has_flag && S == 1 && red_pairs_ &&
                     (double)scratch_.cap < 4294967295.0 && !lr16_disabled();
   if (lr16) {
-    if (!inv_) inv_ = balloc<u32>(*be_, scratch_.cap);
+    ensure_inv();
     if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz);
     if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   }
@@ -398,7 +410,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
     // owner-partitioned scratch: the slot-ordered unique list is the send
     // order already; counts are range counts (one range at world 1).  inv_
     // (slot -> send index) lets the LR backward write the send buffer directly.
-    if (!inv_ && red_pairs_ && cfg_.model.kind == kLR) inv_ = balloc<u32>(*be_, scratch_.cap);
+    if (red_pairs_ && cfg_.model.kind == kLR) ensure_inv();
     dedup_(b, world, send_keys_out, true);
     inv_valid_ = inv_ != nullptr;
     if (world > 1)

@@ -655,7 +655,9 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
       const double rows = (double)f.rows[0];
       for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
         const float v = acc[i];
-        if (v != 0.0f) f.out[f.inv[d0 + i]] = (float)((double)v / rows);
+        if (v == 0.0f) continue;
+        const u32 o = f.inv[d0 + i];
+        if (o != 0xFFFFFFFFu) f.out[o] = (float)((double)v / rows);  // (not the trash slot)
       }
     } else {
       float* g = f.grad + d0;

@@ -165,7 +165,12 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
         if (prev == k[j]) break;
       }
       if (++n >= R) {
+        // no free slot: the key's occurrences go to the trash slot (index
+        // cap: never stamped, so never in the unique list; its pulled row is
+        // zero and its gradients are dropped) and the step is flagged --
+        // never merged into another key's slot
         *overflow = 1u;
+        sj = sv.cap;
         break;
       }
       if (parts > 1) {
@@ -176,9 +181,9 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
       }
       c = skeys[sj];
     }
-    XF_DASSERT(sj < cap);
+    XF_DASSERT(sj < cap || sj == sv.cap);
     t_key[h[j]] = sj;
-    sv.stamps[sj] = sv.epoch;
+    if (sj < sv.cap) sv.stamps[sj] = sv.epoch;
   }
   __syncthreads();
 #pragma unroll

@@ -102,6 +102,7 @@ class Engine {
   void export_table(std::vector<u64>& keys, std::vector<u32>& words);
   void import_table(const std::vector<u64>& keys, const std::vector<u32>& words);
   int state_words() const { return table_.L.stride - 2; }
+  const TableLayout& layout() const { return table_.L; }
   // Binary shard file: header + keys + state words.
   void save(const std::string& path);
   void load(const std::string& path);
@@ -155,6 +156,7 @@ class Engine {
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
   void set_reduction(FwdArgs& fa) const;
+  void ensure_inv();
   LossStats* stats_ = nullptr;  // [1]
   u32* send_pos_ = nullptr;     // [max_nnz]
   int64_t* bucket_ws_ = nullptr;  // [2*256]

@@ -177,6 +177,15 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_property_readonly("state_words", &Engine::state_words)
       .def_property_readonly("table_capacity", &Engine::table_capacity)
       .def_property_readonly("table_bytes", &Engine::table_bytes)
+      .def_property_readonly("layout", [](Engine& e) {
+        const TableLayout& L = e.layout();
+        py::dict d;
+        d["kind"] = e.config().model.kind;
+        d["P"] = L.P;
+        d["opt"] = L.opt;
+        d["stride"] = L.stride;
+        return d;
+      })
       .def("set_stream", [](Engine& e, uintptr_t s) { e.set_stream(reinterpret_cast<void*>(s)); })
       .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("train_step", &Engine::train_step, py::call_guard<py::gil_scoped_release>())

@@ -29,16 +29,23 @@ export MASTER_ADDR=$DMLC_PS_ROOT_URI
 export MASTER_PORT=$DMLC_PS_ROOT_PORT
 export WORLD_SIZE=$DMLC_NUM_WORKER
 
+# every started process is recorded here; scripts/stop.sh kills exactly these
+pidfile=${XFLOW_PIDFILE:-/tmp/xflow_workers.$(id -u).pid}
+: > "$pidfile"
 DMLC_ROLE=scheduler ${bin} ${arg} &
+echo $! >> "$pidfile"
 for ((i=0; i<${DMLC_NUM_SERVER}; ++i)); do
     DMLC_ROLE=server ${bin} ${arg} &
+    echo $! >> "$pidfile"
 done
 pids=()
 for ((i=0; i<${DMLC_NUM_WORKER}; ++i)); do
     DMLC_ROLE=worker DMLC_WORKER_ID=$i RANK=$i LOCAL_RANK=$i XFLOW_DEVICE=$i ${bin} ${arg} &
     pids+=($!)
+    echo $! >> "$pidfile"
 done
 rc=0
 for p in "${pids[@]}"; do wait $p || rc=$?; done
 wait
+rm -f "$pidfile"
 exit $rc

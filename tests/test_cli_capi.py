@@ -105,3 +105,37 @@ def test_c_api(tmp_path):
         lib.XFFree(ctypes.byref(bad))
     finally:
         os.chdir(cwd)
+
+
+def test_local_sh_records_pids_and_stop_sh_kills_them(tmp_path):
+    """scripts/local.sh writes every process it starts to the pid file and
+    scripts/stop.sh stops exactly those (the reference's stop.sh kill -9s
+    every xflow_lr by name)."""
+    import subprocess
+    import time
+
+    pidfile = tmp_path / "pids"
+    env = dict(os.environ, XFLOW_PIDFILE=str(pidfile))
+    launcher = subprocess.Popen(["bash", os.path.join(ROOT, "scripts", "local.sh"), "1", "2",
+                                 "sleep", "60"], env=env, stdout=subprocess.PIPE,
+                                stderr=subprocess.STDOUT)
+    try:
+        for _ in range(100):
+            if pidfile.exists() and len(pidfile.read_text().split()) == 4:
+                break
+            time.sleep(0.05)
+        pids = [int(p) for p in pidfile.read_text().split()]
+        assert len(pids) == 4  # scheduler + 1 server + 2 workers
+        for p in pids:
+            os.kill(p, 0)  # alive
+        out = subprocess.run(["bash", os.path.join(ROOT, "scripts", "stop.sh")], env=env,
+                             capture_output=True, text=True, timeout=30)
+        assert "stopped 4" in out.stdout, out.stdout + out.stderr
+        assert launcher.wait(timeout=30) != 0  # its workers were killed
+        for p in pids:
+            with pytest.raises(ProcessLookupError):
+                os.kill(p, 0)
+        assert not pidfile.exists()
+    finally:
+        if launcher.poll() is None:
+            launcher.kill()

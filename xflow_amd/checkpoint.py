@@ -25,7 +25,7 @@ import json
 import os
 import shutil
 import struct
-from typing import Optional
+from typing import Callable, Optional
 
 import numpy as np
 
@@ -52,20 +52,77 @@ def read_shard(path: str):
     return hdr, keys, words
 
 
-def save(engine, ckpt_dir: str, rank: int, world: int, meta: Optional[dict] = None) -> str:
+def _fsync_file(path: str) -> None:
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def _fsync_dir(path: str) -> None:
+    try:
+        _fsync_file(path)
+    except OSError:  # pragma: no cover - directories cannot be opened on some filesystems
+        pass
+
+
+def _default_barrier() -> None:
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+
+
+def save(engine, ckpt_dir: str, rank: int, world: int, meta: Optional[dict] = None,
+         barrier: Optional[Callable[[], None]] = None) -> str:
+    """Write this rank's shard (fsync'd), wait for every rank (``barrier``,
+    default: the torch.distributed group when one is initialised), then rank 0
+    writes meta.json -- so a valid meta.json only ever sits next to a complete
+    set of shards of one save."""
     os.makedirs(ckpt_dir, exist_ok=True)
     path = os.path.join(ckpt_dir, shard_name(rank, world))
     tmp = path + ".tmp"
     engine.save(tmp)
+    _fsync_file(tmp)
     os.replace(tmp, path)
+    (barrier or _default_barrier)()
     if rank == 0:
         m = dict(meta or {})
         m.update(world=world, model=dataclasses.asdict(engine.model),
                  optim=dataclasses.asdict(engine.optim))
-        with open(os.path.join(ckpt_dir, "meta.json.tmp"), "w") as f:
+        mtmp = os.path.join(ckpt_dir, "meta.json.tmp")
+        with open(mtmp, "w") as f:
             json.dump(m, f, indent=1)
-        os.replace(os.path.join(ckpt_dir, "meta.json.tmp"), os.path.join(ckpt_dir, "meta.json"))
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(mtmp, os.path.join(ckpt_dir, "meta.json"))
+        _fsync_dir(ckpt_dir)
     return path
+
+
+def check_compatible(engine, meta: dict) -> None:
+    """The checkpoint's model/optimizer config must equal the running one."""
+    want = {"model": dataclasses.asdict(engine.model), "optim": dataclasses.asdict(engine.optim)}
+    for k, cur in want.items():
+        saved = meta.get(k)
+        if saved is None:
+            continue
+        diff = {f: (saved.get(f), v) for f, v in cur.items() if f in saved and saved[f] != v}
+        if diff:
+            raise ValueError(f"checkpoint {k} config differs from the running one: {diff}")
+
+
+def _check_header(engine, path: str, hdr) -> None:
+    """Shard header (csrc/engine/engine.cpp Engine::save: version, kind, v_dim,
+    P, p_w, opt, stride) against the engine's table layout."""
+    if hdr[0] != 1:
+        raise ValueError(f"{path}: unsupported shard version {hdr[0]}")
+    lay = engine.layout
+    got = {"kind": hdr[1], "P": hdr[3], "opt": hdr[5], "stride": hdr[6]}
+    exp = {"kind": lay["kind"], "P": lay["P"], "opt": lay["opt"], "stride": lay["stride"]}
+    if got != exp:
+        raise ValueError(f"{path}: shard layout {got} does not match this engine {exp}")
 
 
 def load_meta(ckpt_dir: str) -> dict:
@@ -75,6 +132,7 @@ def load_meta(ckpt_dir: str) -> dict:
 
 def load(engine, ckpt_dir: str, rank: int, world: int) -> dict:
     meta = load_meta(ckpt_dir)
+    check_compatible(engine, meta)
     saved_world = int(meta["world"])
     if saved_world == world:
         engine.load(os.path.join(ckpt_dir, shard_name(rank, world)))
@@ -83,7 +141,8 @@ def load(engine, ckpt_dir: str, rank: int, world: int) -> dict:
     if len(shards) != saved_world:
         raise FileNotFoundError(f"{ckpt_dir}: expected {saved_world} shards, found {len(shards)}")
     for p in shards:
-        _, keys, words = read_shard(p)
+        hdr, keys, words = read_shard(p)
+        _check_header(engine, p, hdr)
         mine = owner_of(keys, world) == rank
         if mine.any():
             engine.import_table(keys[mine], words[mine].reshape(-1))
@@ -103,7 +162,10 @@ def publish(root: str, epoch: int, keep: int = 2) -> None:
     tmp = os.path.join(root, LATEST + ".tmp")
     with open(tmp, "w") as f:
         f.write(os.path.basename(version_dir(root, epoch)) + "\n")
+        f.flush()
+        os.fsync(f.fileno())
     os.replace(tmp, os.path.join(root, LATEST))
+    _fsync_dir(root)
     for d in sorted(glob.glob(os.path.join(root, "epoch-*")))[:-keep]:
         shutil.rmtree(d, ignore_errors=True)
 

@@ -246,6 +246,16 @@ class Engine:
         self._sync_stream()
         return int(self._e.table_size())
 
+    @property
+    def layout(self) -> dict:
+        """Table slot layout (model kind, params per key, optimizer, words per slot)."""
+        return dict(self._e.layout)
+
+    @property
+    def table_capacity(self) -> int:
+        """Slots of this rank's table shard."""
+        return int(self._e.table_capacity)
+
     def n_unique(self) -> int:
         self._sync_stream()
         return int(self._e.n_unique())

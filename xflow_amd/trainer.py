@@ -245,11 +245,16 @@ class Trainer:
             if self.epoch % 30 == 0:
                 _say("epoch : %d" % (self.epoch - 1))
             st = self.engine.read_stats(reset=True)
-            tot = xdist.all_sum([st["ln_loss"], st["rows"], ep_samples], self.device)
+            tot = xdist.all_sum([st["ln_loss"], st["rows"], ep_samples,
+                                 float(self.engine.overflowed())], self.device)
+            if tot[3] > 0:
+                raise RuntimeError("table or dedup-scratch overflow during epoch %d: keys were "
+                                   "dropped or isolated; grow --log2-cap / max_nnz" % self.epoch)
+            keys = self.engine.table_size()
             rec = dict(event="epoch", epoch=self.epoch, steps=self.steps,
                        train_logloss=tot[0] / max(tot[1], 1.0),
                        samples_per_s=tot[2] / max(time.perf_counter() - t0, 1e-9),
-                       table_keys=self.engine.table_size())
+                       table_keys=keys, table_load=keys / float(self.engine.table_capacity))
             if self.cfg.optim.lambda1 > 0 and os.environ.get("XFLOW_REPORT_NNZ"):
                 rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
                                                            self.device)[0])
@@ -339,7 +344,7 @@ class Trainer:
         if hasattr(self.sharded, "flush"):
             self.sharded.flush()
         checkpoint.save(self.engine, ckpt_dir, self.rank, self.world,
-                        meta={"epoch": self.epoch, "steps": self.steps})
+                        meta={"epoch": self.epoch, "steps": self.steps}, barrier=xdist.barrier)
         xdist.barrier()
 
     def load(self, ckpt_dir: str) -> dict:
