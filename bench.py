@@ -113,15 +113,18 @@ def main():
         sharded = AsyncShardedEngine(engine) if a.async_p2p else ShardedEngine(engine)
     overlap = a.overlap == "on"
     if not overlap and sharded is not None:
-        # double-buffered batches on the compute stream: batch t+1 is generated
-        # while the host waits for step t's all-to-all split sizes
+        # double-buffered batches on the compute stream
         bufs = [gen.alloc_batch(), gen.alloc_batch()]
         gen.next(out=bufs[0])
         cur = [0]
 
         def step():
+            # pipelined: batch t+1 is generated and prepared (dedup + counts
+            # exchange) inside step t, so the host never waits on an in-flight
+            # split-size copy (ShardedEngine.prepare)
             i = cur[0]
-            sharded.train_step(bufs[i], prefetch=lambda: gen.next(out=bufs[i ^ 1]))
+            sharded.train_step(bufs[i], prefetch=lambda: gen.next(out=bufs[i ^ 1]),
+                               next_batch=bufs[i ^ 1])
             cur[0] = i ^ 1
     elif not overlap:
         def step():
@@ -154,6 +157,8 @@ def main():
         step()
     sync()
     engine.read_stats(reset=True)
+    if sharded is not None:
+        sharded.host_waits = 0
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -206,6 +211,7 @@ def main():
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
             "table_load": table_keys / float(world * 2 ** log2_cap),
+            "host_waits": int(sharded.host_waits) if sharded is not None else 0,
         }
         if a.async_p2p:
             out["config"]["parallelism"] += "+async-p2p(staleness=1)"

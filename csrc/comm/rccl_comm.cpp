@@ -52,22 +52,52 @@ void RcclComm::abort() {
 void RcclComm::alltoallv(const void* send, const std::vector<int64_t>& send_counts, void* recv,
                          const std::vector<int64_t>& recv_counts, int elem_bytes,
                          uintptr_t stream) {
+  alltoallv_group({A2AOp{send, send_counts, recv, recv_counts, elem_bytes}}, stream);
+}
+
+void RcclComm::alltoallv_group(const std::vector<A2AOp>& ops, uintptr_t stream) {
   if (!comm_) throw std::runtime_error("RCCL communicator was aborted");
-  if ((int)send_counts.size() != world_ || (int)recv_counts.size() != world_)
-    throw std::invalid_argument("alltoallv: counts must have world entries");
+  for (const A2AOp& op : ops)
+    if ((int)op.send_counts.size() != world_ || (int)op.recv_counts.size() != world_)
+      throw std::invalid_argument("alltoallv: counts must have world entries");
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const char* s = static_cast<const char*>(send);
-  char* r = static_cast<char*>(recv);
-  size_t so = 0, ro = 0;
   check(ncclGroupStart(), "ncclGroupStart");
-  for (int p = 0; p < world_; ++p) {
-    const size_t sb = (size_t)send_counts[p] * elem_bytes;
-    const size_t rb = (size_t)recv_counts[p] * elem_bytes;
-    if (sb) check(ncclSend(s + so, sb, ncclUint8, p, c, st), "ncclSend");
-    if (rb) check(ncclRecv(r + ro, rb, ncclUint8, p, c, st), "ncclRecv");
-    so += sb;
-    ro += rb;
+  for (const A2AOp& op : ops) {
+    const char* s = static_cast<const char*>(op.send);
+    char* r = static_cast<char*>(op.recv);
+    size_t so = 0, ro = 0;
+    for (int p = 0; p < world_; ++p) {
+      const size_t sb = (size_t)op.send_counts[p] * op.elem_bytes;
+      const size_t rb = (size_t)op.recv_counts[p] * op.elem_bytes;
+      if (sb) check(ncclSend(s + so, sb, ncclUint8, p, c, st), "ncclSend");
+      if (rb) check(ncclRecv(r + ro, rb, ncclUint8, p, c, st), "ncclRecv");
+      so += sb;
+      ro += rb;
+    }
+  }
+  check(ncclGroupEnd(), "ncclGroupEnd");
+}
+
+void RcclComm::send_recv(const std::vector<int>& peers, const std::vector<uintptr_t>& sends,
+                         const std::vector<int64_t>& send_bytes,
+                         const std::vector<uintptr_t>& recvs,
+                         const std::vector<int64_t>& recv_bytes, uintptr_t stream) {
+  if (!comm_) throw std::runtime_error("RCCL communicator was aborted");
+  const size_t n = peers.size();
+  if (sends.size() != n || send_bytes.size() != n || recvs.size() != n || recv_bytes.size() != n)
+    throw std::invalid_argument("send_recv: list lengths differ");
+  ncclComm_t c = static_cast<ncclComm_t>(comm_);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  check(ncclGroupStart(), "ncclGroupStart");
+  for (size_t i = 0; i < n; ++i) {
+    if (peers[i] < 0 || peers[i] >= world_) throw std::invalid_argument("send_recv: bad peer");
+    if (send_bytes[i] > 0)
+      check(ncclSend(reinterpret_cast<const void*>(sends[i]), (size_t)send_bytes[i], ncclUint8,
+                     peers[i], c, st), "ncclSend");
+    if (recv_bytes[i] > 0)
+      check(ncclRecv(reinterpret_cast<void*>(recvs[i]), (size_t)recv_bytes[i], ncclUint8,
+                     peers[i], c, st), "ncclRecv");
   }
   check(ncclGroupEnd(), "ncclGroupEnd");
 }

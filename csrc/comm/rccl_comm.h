@@ -32,6 +32,21 @@ class RcclComm {
   // variable splits (elements of elem_bytes), host-side counts, on `stream`
   void alltoallv(const void* send, const std::vector<int64_t>& send_counts, void* recv,
                  const std::vector<int64_t>& recv_counts, int elem_bytes, uintptr_t stream);
+  // several variable all-to-alls with the same split counts in ONE group call
+  // (one RCCL kernel): e.g. gradients + slice masks, values + next counts
+  struct A2AOp {
+    const void* send;
+    std::vector<int64_t> send_counts;
+    void* recv;
+    std::vector<int64_t> recv_counts;
+    int elem_bytes;
+  };
+  void alltoallv_group(const std::vector<A2AOp>& ops, uintptr_t stream);
+  // grouped point-to-point: for each i, send send_bytes[i] bytes to peers[i]
+  // and receive recv_bytes[i] bytes from it (0 = none); one group call
+  void send_recv(const std::vector<int>& peers, const std::vector<uintptr_t>& sends,
+                 const std::vector<int64_t>& send_bytes, const std::vector<uintptr_t>& recvs,
+                 const std::vector<int64_t>& recv_bytes, uintptr_t stream);
   // equal splits: `count` elements to / from every peer
   void alltoall(const void* send, void* recv, int64_t count, int elem_bytes, uintptr_t stream);
   // abandon in-flight work (used when a self-test times out)

@@ -126,6 +126,7 @@ class CpuBackend final : public Backend {
       ++u;
     }
     *o.n_uniq = u;
+    if (o.n_uniq_copy) *o.n_uniq_copy = u;
   }
 
   void scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max) override {

@@ -78,6 +78,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   send_pos_ = balloc<u32>(be, nnz);
   n_uniq_ = balloc<int64_t>(be, 1);
   be.memset(n_uniq_, 0, sizeof(int64_t));
+  wset_[0].pos = pos_;
+  wset_[0].uniq_pos = uniq_pos_;
+  wset_[0].n_uniq = n_uniq_;
+  wset_[0].send_pos = send_pos_;
   // slot-indexed buffers carry one extra row: the trash slot (index cap) that
   // a dedup probe overflow sends its occurrences to (flagged, never applied)
   const uint64_t rows1 = scratch_.cap + 1;
@@ -122,14 +126,48 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 Engine::~Engine() {
   Backend& be = *be_;
   be.synchronize();
+  use_worker_set(cur_wb_);  // (records the current set)
   void* ptrs[] = {table_.words, table_.size, overflow_, scratch_.keys, scratch_.stamps,
-                  scratch_.claims, block_counts_, pos_, uniq_keys_,
-                  uniq_pos_, uniq_slot_, send_pos_, n_uniq_, wpull_, grad_, tmask_, stats_,
-                  bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
+                  scratch_.claims, block_counts_, uniq_keys_, uniq_slot_, wpull_, grad_, tmask_,
+                  stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   srv_slots_[0], srv_slots_[1], srv_nz_[0], srv_nz_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_, inv_, red_rowv_, lr_grad_, lr_nz_};
+                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, own_pos_[0],
+                  own_pos_[1], own_idx_[0], own_idx_[1]};
   for (void* p : ptrs) be.free(p);
+  for (WorkerSet& w : wset_) {
+    void* wp[] = {w.pos, w.uniq_pos, w.inv, w.n_uniq, w.send_pos};
+    for (void* p : wp) be.free(p);
+  }
+}
+
+void Engine::use_worker_set(int wb) {
+  if (wb < 0 || wb > 1) throw std::invalid_argument("worker buffer set must be 0 or 1");
+  WorkerSet& c = wset_[cur_wb_];
+  c.pos = pos_;
+  c.uniq_pos = uniq_pos_;
+  c.inv = inv_;
+  c.n_uniq = n_uniq_;
+  c.send_pos = send_pos_;
+  c.send_map = send_map_;
+  c.inv_valid = inv_valid_;
+  WorkerSet& w = wset_[wb];
+  if (!w.pos) {  // second set: allocated on first use (pipelined sharded step)
+    const int64_t nnz = cfg_.max_nnz;
+    w.pos = balloc<u32>(*be_, nnz);
+    w.uniq_pos = balloc<u32>(*be_, nnz);
+    w.send_pos = balloc<u32>(*be_, nnz);
+    w.n_uniq = balloc<int64_t>(*be_, 1);
+    be_->memset(w.n_uniq, 0, sizeof(int64_t));
+  }
+  pos_ = w.pos;
+  uniq_pos_ = w.uniq_pos;
+  inv_ = w.inv;
+  n_uniq_ = w.n_uniq;
+  send_pos_ = w.send_pos;
+  send_map_ = w.send_map;
+  inv_valid_ = w.inv_valid;
+  cur_wb_ = wb;
 }
 
 void Engine::set_reduction(FwdArgs& fa) const {
@@ -174,7 +212,8 @@ void Engine::ensure_inv() {
   be_->memset(inv_ + scratch_.cap, 0xFF, 16 * sizeof(u32));
 }
 
-void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want_inv) {
+void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want_inv,
+                    int64_t* n_copy) {
   if (b.nnz > cfg_.max_nnz) throw std::invalid_argument("batch nnz exceeds max_nnz");
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
   if (b.col_stride > 0 && (b.row_ptr || b.col_stride < b.rows || b.nnz != b.rows * b.nnz_per_row))
@@ -195,6 +234,7 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
   o.overflow = overflow_;
   o.block_counts = block_counts_;
   o.inv = want_inv ? inv_ : nullptr;
+  o.n_uniq_copy = n_copy;
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 
@@ -207,6 +247,7 @@ static bool lr16_disabled() {
 
 void Engine::train_step(const BatchView& b) {
   srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
+  use_worker_set(0);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
   const int ps = pstride();
@@ -297,6 +338,7 @@ void Engine::train_step(const BatchView& b) {
 }
 
 void Engine::eval_step(const BatchView& b, float* pctr) {
+  use_worker_set(0);
   dedup_(b);
   PullArgs pa;
   pa.table = table_;
@@ -403,20 +445,26 @@ std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
 // ---------------------------------------------------------------------------
 // multi-rank phases
 // ---------------------------------------------------------------------------
-void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out) {
+void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out,
+                       int wb) {
+  use_worker_set(wb);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  if (b.nnz == 0) {  // a rank without data this step: nothing to send
+    be_->memset(counts_out, 0, sizeof(int64_t) * (world > 0 ? world : 1));
+    be_->memset(n_uniq_, 0, sizeof(int64_t));
+    inv_valid_ = false;
+    send_map_ = uniq_pos_;
+    return;
+  }
   if (world >= 1 && world <= kMaxParts && be_->partitioned_dedup()) {
     // owner-partitioned scratch: the slot-ordered unique list is the send
     // order already; counts are range counts (one range at world 1).  inv_
     // (slot -> send index) lets the LR backward write the send buffer directly.
     if (red_pairs_ && cfg_.model.kind == kLR) ensure_inv();
-    dedup_(b, world, send_keys_out, true);
+    dedup_(b, world, send_keys_out, true, world == 1 ? counts_out : nullptr);
     inv_valid_ = inv_ != nullptr;
-    if (world > 1)
-      be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
-    else
-      be_->copy_d2d(counts_out, n_uniq_, sizeof(int64_t));
+    if (world > 1) be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
     send_map_ = uniq_pos_;
     return;
   }
@@ -455,7 +503,9 @@ bool Engine::lr16_layout() const {
          !lr16_disabled();
 }
 
-void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr) {
+void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr,
+                       int wb) {
+  use_worker_set(wb);
   be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, pstride());
   FwdArgs fa;
   fa.batch = b;
@@ -469,11 +519,14 @@ void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, 
   be_->forward_backward(fa);
 }
 
-void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert, int buf) {
+void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert, int buf,
+                    const std::vector<int64_t>& src_offsets) {
   ensure_server_capacity(n, buf);
   srv_n_[buf] = n;
   srv_vals_[buf] = out_vals;
+  grp_[buf] = SrcGroups();
   if (n == 0) return;
+  if (insert) group_entries(recv_keys, n, buf, src_offsets);
   PullArgs pa;
   pa.table = table_;
   pa.opt = cfg_.opt;
@@ -489,8 +542,78 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
   be_->table_pull(pa);
 }
 
+// Owner grouping of the received entries (several sources with keys this
+// step, GPU backend): one registration per (key, source) in an owner scratch
+// table, so that s_apply runs once over all sources.  The scratch keeps keys
+// across steps and is cleared once the entries registered since the last
+// clear (an upper bound of its keys) could exceed half of it; it is sized to
+// 4x the step's entries, so the load stays below 0.75.
+bool Engine::group_entries(const u64* recv_keys, int64_t n, int buf,
+                           const std::vector<int64_t>& offs) {
+  const int nsrc = (int)offs.size() - 1;
+  if (!be_->owner_grouping() || nsrc < 2 || nsrc > kMaxGroupSources) return false;
+  if (offs.front() != 0 || offs.back() != n) throw std::invalid_argument("s_pull: source offsets");
+  int active = 0;
+  for (int s = 0; s < nsrc; ++s) {
+    if (offs[s + 1] < offs[s]) throw std::invalid_argument("s_pull: source offsets");
+    active += offs[s + 1] > offs[s];
+  }
+  if (active < 2) return false;  // one source: the per-source apply is one launch already
+  const u64 want = next_pow2((uint64_t)n * 4);
+  if (want > (1ull << 32)) throw std::invalid_argument("s_pull: too many received keys to group");
+  if (want > own_cap_ || nsrc != own_nsrc_) {
+    // (re)size: the other buffer's registrations are dropped with the arrays
+    // (its apply then runs source by source)
+    be_->synchronize();
+    const u64 cap = want > own_cap_ ? want : own_cap_;
+    be_->free(own_keys_);
+    be_->free(own_idx_[0]);
+    be_->free(own_idx_[1]);
+    own_idx_[0] = own_idx_[1] = nullptr;
+    grp_[0] = grp_[1] = SrcGroups();
+    own_cap_ = cap;
+    own_nsrc_ = nsrc;
+    own_keys_ = balloc<u64>(*be_, cap);
+    be_->fill_u64(own_keys_, kEmptyKey, cap);
+    own_fill_ = 0;
+  }
+  if (!own_idx_[buf]) {
+    own_idx_[buf] = balloc<u64>(*be_, own_cap_ * (u64)own_nsrc_);
+    be_->memset(own_idx_[buf], 0, sizeof(u64) * own_cap_ * own_nsrc_);  // epoch 0: never valid
+  }
+  if (n > own_pos_cap_[buf]) {
+    be_->synchronize();
+    be_->free(own_pos_[buf]);
+    own_pos_cap_[buf] = n + n / 4 + 1024;
+    own_pos_[buf] = balloc<u32>(*be_, own_pos_cap_[buf]);
+  }
+  if (own_fill_ + n > (int64_t)(own_cap_ / 2)) {
+    be_->fill_u64(own_keys_, kEmptyKey, own_cap_);
+    own_fill_ = 0;
+  }
+  own_fill_ += n;
+  if (++own_epoch_ == 0) own_epoch_ = 1;
+  OwnerGroupArgs ga;
+  ga.keys = recv_keys;
+  ga.n = n;
+  ga.okeys = own_keys_;
+  ga.ocap = own_cap_;
+  ga.opos = own_pos_[buf];
+  ga.oidx = own_idx_[buf];
+  ga.g.nsrc = nsrc;
+  ga.g.epoch = own_epoch_;
+  for (int s = 0; s <= nsrc; ++s) ga.g.offs[s] = offs[s];
+  ga.overflow = overflow_;
+  be_->owner_group(ga);
+  grp_[buf] = ga.g;
+  grp_[buf].opos = own_pos_[buf];
+  grp_[buf].oidx = own_idx_[buf];
+  return true;
+}
+
 void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
-                                float* grads_out, u32* masks_out, int S_global) {
+                                float* grads_out, u32* masks_out, int S_global, int wb) {
+  use_worker_set(wb);
   // All ranks of a step must agree on the gradient row width (S*pstride):
   // S_global (>= this batch's slices) lets a rank with a short or empty batch
   // emit the same layout; its extra slices carry no rows and no mask bits.
@@ -550,39 +673,61 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
                      const std::vector<int64_t>& src_offsets, int S, int buf) {
   if (buf < 0 || buf > 1) throw std::invalid_argument("server buffer must be 0 or 1");
   const int ps = pstride();
+  const int gw = grad_width();
   // the first source applied sees the state its pull saw; a key sent by
   // several sources is updated by the earlier ones, so later sources re-read
+  // (the grouped apply pushes every source of a key at once: its stash stays valid)
   bool stash = srv_nz_fresh_[buf];
   srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;
+  ApplyArgs base;
+  base.table = table_;
+  base.opt = cfg_.opt;
+  base.gstride = gw;
+  if (sharded_fm_compact()) {
+    base.fm_compact = true;
+    base.fm_D = cfg_.model.v_dim;
+  }
+  base.zero_after = false;
+  base.S = S;
+  base.pstride = ps;
+  base.P = cfg_.model.P();
+  base.sum_slices = cfg_.sum_slices;
+  base.slice_rows = nullptr;
+  const SrcGroups& g = grp_[buf];
+  if (g.oidx && (int)src_offsets.size() == g.nsrc + 1) {
+    bool same = true;
+    for (int s = 0; s <= g.nsrc; ++s) same = same && src_offsets[s] == g.offs[s];
+    if (!same) throw std::invalid_argument("s_apply: source offsets differ from the pull's");
+    const int64_t n = g.offs[g.nsrc];
+    if (n > srv_n_[buf]) throw std::invalid_argument("s_apply: offsets beyond pull");
+    ApplyArgs aa = base;
+    aa.keys = recv_keys;
+    aa.slots = srv_slots_[buf];
+    aa.n_host = n;
+    aa.n_max = n;
+    aa.grads = const_cast<float*>(recv_grads);
+    if (aa.fm_compact) aa.pulled = srv_vals_[buf];
+    aa.masks = recv_masks;
+    if (stash) aa.nz_stash = srv_nz_[buf];
+    aa.grp = g;
+    be_->table_apply(aa);
+    return;
+  }
   for (size_t src = 0; src + 1 < src_offsets.size(); ++src) {
     int64_t off = src_offsets[src];
     int64_t cnt = src_offsets[src + 1] - off;
     if (cnt <= 0) continue;
     if (src_offsets[src + 1] > srv_n_[buf]) throw std::invalid_argument("s_apply: offsets beyond pull");
-    ApplyArgs aa;
-    aa.table = table_;
-    aa.opt = cfg_.opt;
+    ApplyArgs aa = base;
     aa.keys = recv_keys + off;
     aa.slots = srv_slots_[buf] + off;
     aa.n_host = cnt;
     aa.n_max = cnt;
-    const int gw = grad_width();
     aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * gw;
-    aa.gstride = gw;
-    if (sharded_fm_compact()) {
-      aa.fm_compact = true;
-      aa.fm_D = cfg_.model.v_dim;
-      aa.pulled = srv_vals_[buf] + off * (int64_t)ps;
-    }
+    if (aa.fm_compact) aa.pulled = srv_vals_[buf] + off * (int64_t)ps;
     aa.masks = recv_masks ? recv_masks + off : nullptr;
     if (stash) aa.nz_stash = srv_nz_[buf] + 2 * off;
     stash = false;
-    aa.zero_after = false;
-    aa.S = S;
-    aa.pstride = ps;
-    aa.P = cfg_.model.P();
-    aa.sum_slices = cfg_.sum_slices;
-    aa.slice_rows = nullptr;
     be_->table_apply(aa);
   }
 }

@@ -83,6 +83,8 @@ class HipBackend final : public Backend {
                         int64_t* counts) override {
     hip::launch_partition_counts(s, chunk_offsets, n_uniq, counts, stream_);
   }
+  bool owner_grouping() const override { return true; }
+  void owner_group(const OwnerGroupArgs& a) override { hip::launch_owner_group(a, stream_); }
   void gather_grads(const GatherGradArgs& a) override { hip::launch_gather_grads(a, stream_); }
   void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                     int64_t n_max, int width, float* zero_out) override {

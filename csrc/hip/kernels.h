@@ -15,6 +15,7 @@ void launch_scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, i
 void launch_table_pull(const PullArgs& a, hipStream_t st);
 void launch_table_apply(const ApplyArgs& a, hipStream_t st);
 void launch_gather_grads(const GatherGradArgs& a, hipStream_t st);
+void launch_owner_group(const OwnerGroupArgs& a, hipStream_t st);
 void launch_bucket(const BucketArgs& a, hipStream_t st);
 void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
                              const int64_t* n_uniq, int64_t* counts, hipStream_t st);

@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
 __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
     unsigned int* __restrict__ counts, int nb, unsigned long long* __restrict__ n_out,
     unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
-    u64 cap_alloc) {
+    u64 cap_alloc, unsigned long long* __restrict__ n_copy) {
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
     int i = c0 + (int)threadIdx.x;
@@ -259,6 +259,7 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
   }
   if (threadIdx.x == 0) {
     *n_out = carry;
+    if (n_copy) *n_copy = carry;  // e.g. the one-owner counts of a world-1 sharded step
     if (ctl) {
       const u64 mx = ctl[1] > carry ? ctl[1] : carry;
       ctl[1] = mx;
@@ -374,7 +375,8 @@ void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipSt
   int g2 = (int)((s.cap + kCompactChunk - 1) / kCompactChunk);
   hipLaunchKernelGGL(k_compact_count, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts);
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanBlock), 0, st, o.block_counts, g2,
-                     reinterpret_cast<unsigned long long*>(o.n_uniq), s.claims, s.ctl, s.cap);
+                     reinterpret_cast<unsigned long long*>(o.n_uniq), s.claims, s.ctl, s.cap,
+                     reinterpret_cast<unsigned long long*>(o.n_uniq_copy));
   hipLaunchKernelGGL(k_compact_write, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts,
                      o.uniq_keys, o.uniq_pos, o.inv);
   XF_HIP_CHECK(hipGetLastError());
@@ -712,11 +714,103 @@ __global__ void __launch_bounds__(kBlock) k_apply_generic(ApplyArgs a) {
   }
 }
 
+// ---- one-launch multi-source apply (ApplyArgs::grp) ------------------------
+__device__ __forceinline__ int group_src(const SrcGroups& g, int64_t i) {
+  int s = 0;
+  while (s + 1 < g.nsrc && i >= g.offs[s + 1]) ++s;
+  return s;
+}
+
+// Entry i leads its key when no earlier source sent the key this step; then
+// row = the key's (slot, source) registrations and src0 = i's source.
+__device__ __forceinline__ bool group_leader(const SrcGroups& g, int64_t i, const u64*& row,
+                                             int& src0) {
+  const u32 so = g.opos[i];
+  if (so == kNoSlot) return false;  // owner scratch overflow (flagged by k_owner_group)
+  row = g.oidx + (u64)so * (u64)g.nsrc;
+  src0 = group_src(g, i);
+  for (int s = 0; s < src0; ++s)
+    if ((u32)(row[s] >> 32) == g.epoch) return false;
+  return true;
+}
+
+// Registration of every received entry under (owner-scratch slot of its key,
+// source).  The owner scratch persists across steps (hot keys keep their
+// slot); stale registrations carry older epochs.
+__global__ void __launch_bounds__(kBlock) k_owner_group(OwnerGroupArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.n) return;
+  const u64 key = sanitize_key(a.keys[i]);
+  const u64 mask = a.ocap - 1;
+  u64 s = fmix64(key) & mask;
+  u32 slot = kNoSlot;
+  for (u64 c = 0; c < a.ocap; ++c) {
+    const u64 cur = a.okeys[s];
+    if (cur == key) {
+      slot = (u32)s;
+      break;
+    }
+    if (cur == kEmptyKey) {
+      const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&a.okeys[s]),
+                                 (unsigned long long)kEmptyKey, (unsigned long long)key);
+      if (prev == kEmptyKey || prev == key) {
+        slot = (u32)s;
+        break;
+      }
+    }
+    s = (s + 1) & mask;
+  }
+  a.opos[i] = slot;
+  if (slot == kNoSlot) {
+    *a.overflow = 1u;
+    return;
+  }
+  a.oidx[(u64)slot * (u64)a.g.nsrc + (u64)group_src(a.g, i)] = ((u64)a.g.epoch << 32) | (u32)i;
+}
+
+void launch_owner_group(const OwnerGroupArgs& a, hipStream_t st) {
+  if (a.n <= 0) return;
+  if (a.g.nsrc < 1 || a.g.nsrc > kMaxGroupSources) throw std::runtime_error("owner_group: nsrc");
+  if (a.ocap == 0 || (a.ocap & (a.ocap - 1))) throw std::runtime_error("owner_group: ocap");
+  hipLaunchKernelGGL(k_owner_group, dim3((unsigned)((a.n + kBlock - 1) / kBlock)), dim3(kBlock),
+                     0, st, a);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// LR-FTRL, one slice, 16-byte slots, all sources in one launch: the leader
+// entry of a key takes (n, z) from its pull stash (or the table), pushes each
+// source's gradient in source order and writes the slot once.
+__global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
+  const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const FtrlParams fp = a.opt.ftrl;
+  const SrcGroups& g = a.grp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64* row;
+    int src0;
+    if (!group_leader(g, i, row, src0)) continue;
+    const u32 slot = a.slots[i];
+    if (slot == kNoSlot) continue;
+    float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
+    float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
+    for (int s = src0; s < g.nsrc; ++s) {
+      const u64 v = row[s];
+      if ((u32)(v >> 32) != g.epoch) continue;
+      const float gr = a.grads[(u32)v];
+      const float w = ftrl_weight(nz.y, nz.x, fp);
+      ftrl_push(nz.x, nz.y, w, gr, fp);
+    }
+    *st = nz;
+  }
+}
+
 // Multi-parameter apply: a group of G lanes per key (G = pow2 >= pstride),
 // lane p owns parameter p's optimizer state, so a wave touches a few
 // contiguous slots instead of 64 scattered ones.  Every lane reads the
 // "pushed" flag before lane 0 of the group writes it (same wave, program
 // order); latent params use their lazy init value until the key's first push.
+// With a.grp (several sources) the group of a key's leader entry applies the
+// (source, slice) contributions in that order; other entries skip.
 template <int G>
 __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   static_assert(G <= kWave, "a key's lanes must share a wave");
@@ -725,13 +819,17 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   const int S = a.S, ps = a.pstride, gs = a.gstride ? a.gstride : ps;
   const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
   const int p = threadIdx.x % G;
+  const bool multi = a.grp.oidx != nullptr;
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; i < n; i += stride) {
+    const u64* grow = nullptr;
+    int src0 = 0, nsrc = 1;
+    if (multi) {
+      if (!group_leader(a.grp, i, grow, src0)) continue;  // uniform over the key's lanes
+      nsrc = a.grp.nsrc;
+    }
     const u32 slot = a.slots[i];
     XF_DASSERT(slot == kNoSlot || slot < a.table.cap);
-    const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
-    float* g = a.grads + (size_t)row * S * gs;
-    const u32 m = a.masks ? a.masks[row] : all;
     if (slot != kNoSlot && p < L.P) {
       u32* sp = a.table.words + (u64)slot * L.stride;
       const u64 key = *reinterpret_cast<const u64*>(sp);
@@ -741,7 +839,8 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
       const bool ftrl = L.opt == kFTRL;
       float n0 = 0.0f, z0 = 0.0f, w0 = 0.0f;
       if (ftrl) {
-        float2 nz = *reinterpret_cast<float2*>(st + 2 * p);
+        float2 nz = (a.nz_stash && L.P == 1) ? reinterpret_cast<const float2*>(a.nz_stash)[i]
+                                             : *reinterpret_cast<float2*>(st + 2 * p);
         n0 = nz.x;
         z0 = nz.y;
       } else {
@@ -763,25 +862,40 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
       // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
       const float w_pre =
           a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : weight()) : 0.0f;
-      auto raw_of = [&](int s) -> float {
-        if (!a.fm_compact) return g[s * gs + p];
-        const float Bv = g[s * gs], Cv = g[s * gs + 1];
-        return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
-      };
-      if (a.sum_slices) {
-        float acc = 0.0f;
-        for (int s = 0; s < S; ++s)
-          if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
-        if (m) push(acc);
-      } else {
-        for (int s = 0; s < S; ++s)
-          if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
+      u32 any = 0;
+      for (int sc = src0; sc < nsrc; ++sc) {
+        u32 e = (u32)i;
+        if (multi) {
+          const u64 v = grow[sc];
+          if ((u32)(v >> 32) != a.grp.epoch) continue;
+          e = (u32)v;
+        }
+        const u32 row = a.grad_map ? a.grad_map[e] : e;
+        const float* g = a.grads + (size_t)row * S * gs;
+        const u32 m = a.masks ? a.masks[row] : all;
+        any |= m;
+        auto raw_of = [&](int s) -> float {
+          if (!a.fm_compact) return g[s * gs + p];
+          const float Bv = g[s * gs], Cv = g[s * gs + 1];
+          return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
+        };
+        if (a.sum_slices) {
+          float acc = 0.0f;
+          for (int s = 0; s < S; ++s)
+            if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
+          if (m) push(acc);
+        } else {
+          for (int s = 0; s < S; ++s)
+            if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
+        }
       }
       if (ftrl) *reinterpret_cast<float2*>(st + 2 * p) = make_float2(n0, z0);
       else st[p] = w0;
-      if (L.has_flag && p == 0 && m) sp[L.flag_word] = 1u;
+      if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
     }
-    if (a.zero_after && p < (a.fm_compact ? 2 : ps)) {
+    if (!multi && a.zero_after && p < (a.fm_compact ? 2 : ps)) {
+      const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+      float* g = a.grads + (size_t)row * S * gs;
       for (int s = 0; s < S; ++s) g[s * gs + p] = 0.0f;
       if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }
@@ -797,8 +911,28 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   const TableLayout& L = a.table.L;
   int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
-  if (L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag && a.S == 1 && !a.masks &&
-      a.pstride == 1) {
+  const bool lr16 = L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag && a.S == 1 &&
+                    !a.masks && a.pstride == 1;
+  if (a.grp.oidx) {
+    if (a.zero_after || a.reset_pos || a.pstride > 64)
+      throw std::runtime_error("multi-source apply: unsupported arguments");
+    if (lr16) {
+      hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);
+    } else {
+      int64_t nm = a.n_dev ? a.n_max : a.n_host;
+      const int G = group_for(a.pstride);
+      const int g2 = grid_for(nm * G, kBlock, kGroupGridCap);
+      switch (G) {
+        case 1: launch_apply_group<1>(a, g2, st); break;
+        case 2: launch_apply_group<2>(a, g2, st); break;
+        case 4: launch_apply_group<4>(a, g2, st); break;
+        case 8: launch_apply_group<8>(a, g2, st); break;
+        case 16: launch_apply_group<16>(a, g2, st); break;
+        case 32: launch_apply_group<32>(a, g2, st); break;
+        default: launch_apply_group<64>(a, g2, st); break;
+      }
+    }
+  } else if (lr16) {
     hipLaunchKernelGGL(k_apply_lr16, dim3(grid), dim3(kBlock), 0, st, a);
   } else if (a.pstride >= 2 && a.pstride <= 64 && !a.reset_pos) {
     int64_t nm = a.n_dev ? a.n_max : a.n_host;

@@ -72,6 +72,7 @@ struct DedupOut {
   u32* overflow = nullptr;
   u32* block_counts = nullptr; // [cap/4096 + 1] compaction workspace (HIP backend)
   u32* inv = nullptr;          // optional [cap]: unique-list index of each slot of the batch (HIP)
+  int64_t* n_uniq_copy = nullptr;  // optional second destination of the unique count
 };
 
 struct FwdArgs {
@@ -136,6 +137,33 @@ struct PullArgs {
   float* zero_out = nullptr;       // [n]
 };
 
+// Owner-side grouping of the keys a rank received from several sources in
+// one sharded step (HIP): every received entry finds its key's slot in an
+// owner scratch table and registers itself under (slot, source).  The apply
+// then runs once over all entries: the entry of a key's first source is its
+// leader and pushes every source's contributions in source order -- one
+// launch per step instead of one per source, and the key's state is read and
+// written once (from the pull's stash when nothing touched the table since).
+constexpr int kMaxGroupSources = 16;
+struct SrcGroups {
+  const u32* opos = nullptr;   // [n] owner-scratch slot of each received entry
+  const u64* oidx = nullptr;   // [ocap][nsrc]: (epoch << 32) | entry, per (slot, source)
+  int nsrc = 0;
+  u32 epoch = 0;               // entries of other steps carry other epochs
+  int64_t offs[kMaxGroupSources + 1] = {};  // entries of source s: [offs[s], offs[s+1])
+};
+
+struct OwnerGroupArgs {
+  const u64* keys = nullptr;   // received keys, grouped by source
+  int64_t n = 0;
+  u64* okeys = nullptr;        // owner scratch keys [ocap] (kEmptyKey when free)
+  u64 ocap = 0;                // power of two
+  u32* opos = nullptr;         // out [n]
+  u64* oidx = nullptr;         // out [ocap][nsrc]
+  SrcGroups g;                 // nsrc, epoch, offs
+  u32* overflow = nullptr;
+};
+
 struct ApplyArgs {
   TableView table;
   OptSpec opt;
@@ -173,6 +201,10 @@ struct ApplyArgs {
   // Optional fused reset of the worker dedup scratch (single-device path).
   ScratchView scratch;
   const u32* reset_pos = nullptr;
+  // Several sources in one launch (grp.oidx != null): n counts all received
+  // entries; an entry's gradient row / mask / pulled values / stash are
+  // indexed by the entry, and each key is applied by its first source's entry.
+  SrcGroups grp;
 };
 
 struct GatherGradArgs {           // worker: pos-indexed raw sums -> send order
@@ -255,6 +287,12 @@ class Backend {
                                 const int64_t* n_uniq, int64_t* counts) {
     (void)s, (void)chunk_offsets, (void)n_uniq, (void)counts;
     throw std::runtime_error("partitioned dedup is not supported by this backend");
+  }
+  // Owner grouping for the one-launch multi-source apply (HIP only).
+  virtual bool owner_grouping() const { return false; }
+  virtual void owner_group(const OwnerGroupArgs& a) {
+    (void)a;
+    throw std::runtime_error("owner grouping is not supported by this backend");
   }
   virtual void gather_grads(const GatherGradArgs& a) = 0;
   // rows of `width` floats: dst[map? map[i] : i] = src[i]   (scatter)

@@ -58,20 +58,29 @@ class Engine {
   std::vector<float> pull_host(const std::vector<u64>& keys);
 
   // ---- multi-rank phases --------------------------------------------------
+  // Worker phases take a worker buffer set wb (0/1): the dedup positions, send
+  // map and counts of a prepared batch live there, so the next batch can be
+  // prepared (deduplicated, counts exchanged) while the current one is still
+  // in its forward/backward -- the pipelined sharded step.
   // worker: dedup the batch and group its unique keys by owner rank.
   // counts_out: backend int64[world]; send_keys_out: backend u64[>= n_unique].
-  void w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out);
+  void w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out,
+                 int wb = 0);
   // server: probe/insert n received keys, write pulled rows (pstride floats)
   // into out_vals (backend memory), remember slots for s_apply.
   // buf selects one of two server slot buffers (pipelined steps alternate).
-  void s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert = true, int buf = 0);
+  // src_offsets (world+1 entries, optional): the sources' ranges of the
+  // received keys; with several sources the GPU backend groups the entries by
+  // key here so that s_apply is one launch.
+  void s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert = true, int buf = 0,
+              const std::vector<int64_t>& src_offsets = {});
   // worker: forward only from pulled rows (sharded evaluation); pctr may be null.
-  void w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr);
+  void w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr, int wb = 0);
   // worker: place pulled rows (in send order) into the pos-indexed buffer,
   // run forward/backward, then emit normalised gradients in send order.
   // grads_out: [n_send][S*pstride]; masks_out: [n_send] (used when S>1).
   void w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
-                          float* grads_out, u32* masks_out, int S_global = 0);
+                          float* grads_out, u32* masks_out, int S_global = 0, int wb = 0);
   // server: apply received gradients source by source (deterministic order).
   // src_offsets has world+1 entries delimiting each source's rows.
   void s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
@@ -114,11 +123,37 @@ class Engine {
 
  private:
   void ensure_server_capacity(int64_t n, int buf = 0);
+  // worker buffer sets (see w_prepare): the members pos_, uniq_pos_, inv_,
+  // n_uniq_, send_pos_, send_map_, inv_valid_ describe set cur_wb_
+  struct WorkerSet {
+    u32* pos = nullptr;
+    u32* uniq_pos = nullptr;
+    u32* inv = nullptr;
+    int64_t* n_uniq = nullptr;
+    u32* send_pos = nullptr;
+    const u32* send_map = nullptr;
+    bool inv_valid = false;
+  };
+  WorkerSet wset_[2];
+  int cur_wb_ = 0;
+  void use_worker_set(int wb);
+  // owner grouping for the one-launch multi-source apply (Backend::owner_group)
+  u64* own_keys_ = nullptr;      // owner scratch [own_cap_]
+  u64 own_cap_ = 0;
+  int64_t own_fill_ = 0;         // entries registered since the last clear (upper bound of keys)
+  int own_nsrc_ = 0;             // row stride of own_idx_
+  u32* own_pos_[2] = {nullptr, nullptr};
+  int64_t own_pos_cap_[2] = {0, 0};
+  u64* own_idx_[2] = {nullptr, nullptr};
+  u32 own_epoch_ = 0;
+  SrcGroups grp_[2];             // grp_[buf].oidx != null: s_pull grouped this buffer
+  bool group_entries(const u64* recv_keys, int64_t n, int buf,
+                     const std::vector<int64_t>& src_offsets);
   const int32_t* slice_rows_dev(const BatchView& b, int S);
   // parts > 1: owner-partitioned scratch (ScratchView::parts); uniq_keys_out
   // redirects the unique-key list (the sharded step's send buffer)
   void dedup_(const BatchView& b, int parts = 1, u64* uniq_keys_out = nullptr,
-              bool want_inv = false);
+              bool want_inv = false, int64_t* n_copy = nullptr);
   const u32* send_map_ = nullptr;  // send order -> scratch slot (send_pos_ or uniq_pos_)
   bool sharded_fm_compact() const {
     return red_pairs_ && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference &&

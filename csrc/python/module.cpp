@@ -147,6 +147,25 @@ PYBIND11_MODULE(_xflow_native, m) {
            [](RcclComm& c, uintptr_t send, uintptr_t recv, int64_t count, int elem_bytes,
               uintptr_t stream) { c.alltoall(P<const void>(send), P<void>(recv), count,
                                              elem_bytes, stream); })
+      .def("alltoallv_group",
+           [](RcclComm& c, std::vector<uintptr_t> sends, std::vector<uintptr_t> recvs,
+              std::vector<int> elem_bytes, std::vector<std::vector<int64_t>> sc,
+              std::vector<std::vector<int64_t>> rc, uintptr_t stream) {
+             std::vector<RcclComm::A2AOp> ops;
+             const size_t n = sends.size();
+             if (recvs.size() != n || elem_bytes.size() != n || sc.size() != n || rc.size() != n)
+               throw std::invalid_argument("alltoallv_group: list lengths differ");
+             for (size_t i = 0; i < n; ++i)
+               ops.push_back({P<const void>(sends[i]), sc[i], P<void>(recvs[i]), rc[i],
+                              elem_bytes[i]});
+             c.alltoallv_group(ops, stream);
+           })
+      .def("send_recv",
+           [](RcclComm& c, std::vector<int> peers, std::vector<uintptr_t> sends,
+              std::vector<int64_t> send_bytes, std::vector<uintptr_t> recvs,
+              std::vector<int64_t> recv_bytes, uintptr_t stream) {
+             c.send_recv(peers, sends, send_bytes, recvs, recv_bytes, stream);
+           })
       .def("abort", &RcclComm::abort);
 
   py::class_<Engine>(m, "Engine")
@@ -205,30 +224,31 @@ PYBIND11_MODULE(_xflow_native, m) {
              return to_np(e.pull_host(k));
            })
       .def("w_prepare",
-           [](Engine& e, const BatchView& b, int world, uintptr_t counts, uintptr_t send_keys) {
-             e.w_prepare(b, world, P<int64_t>(counts), P<u64>(send_keys));
-           },
-           py::call_guard<py::gil_scoped_release>())
+           [](Engine& e, const BatchView& b, int world, uintptr_t counts, uintptr_t send_keys,
+              int wb) { e.w_prepare(b, world, P<int64_t>(counts), P<u64>(send_keys), wb); },
+           py::arg("batch"), py::arg("world"), py::arg("counts"), py::arg("send_keys"),
+           py::arg("wb") = 0, py::call_guard<py::gil_scoped_release>())
       .def("s_pull",
-           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert, int buf) {
-             e.s_pull(P<const u64>(keys), n, P<float>(out), insert, buf);
+           [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert, int buf,
+              std::vector<int64_t> offsets) {
+             e.s_pull(P<const u64>(keys), n, P<float>(out), insert, buf, offsets);
            },
            py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("insert") = true,
-           py::arg("buf") = 0,
+           py::arg("buf") = 0, py::arg("offsets") = std::vector<int64_t>(),
            py::call_guard<py::gil_scoped_release>())
       .def("w_forward",
-           [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t pctr) {
-             e.w_forward(b, P<const float>(pulled), n_send, P<float>(pctr));
-           },
-           py::call_guard<py::gil_scoped_release>())
+           [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t pctr,
+              int wb) { e.w_forward(b, P<const float>(pulled), n_send, P<float>(pctr), wb); },
+           py::arg("batch"), py::arg("pulled"), py::arg("n_send"), py::arg("pctr"),
+           py::arg("wb") = 0, py::call_guard<py::gil_scoped_release>())
       .def("w_forward_backward",
            [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t grads,
-              uintptr_t masks, int S) {
+              uintptr_t masks, int S, int wb) {
              e.w_forward_backward(b, P<const float>(pulled), n_send, P<float>(grads),
-                                  P<u32>(masks), S);
+                                  P<u32>(masks), S, wb);
            },
            py::arg("batch"), py::arg("pulled"), py::arg("n_send"), py::arg("grads"),
-           py::arg("masks"), py::arg("S") = 0,
+           py::arg("masks"), py::arg("S") = 0, py::arg("wb") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("s_apply",
            [](Engine& e, uintptr_t keys, uintptr_t grads, uintptr_t masks,

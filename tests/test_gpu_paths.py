@@ -111,12 +111,17 @@ def _local_sharded(bus, rank, engine):
     return LocalSharded(engine, world=bus.world, rank=rank)
 
 
-@pytest.mark.parametrize("world,kind", [(2, "lr"), (3, "lr"), (2, "fm")])
-def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind):
+@pytest.mark.parametrize("world,kind,S,pipelined",
+                         [(2, "lr", 1, False), (3, "lr", 1, False), (2, "fm", 1, False),
+                          (8, "lr", 1, True), (8, "lr", 2, True), (4, "fm", 2, True),
+                          (4, "mvm", 1, True), (8, "fm", 1, False)])
+def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind, S, pipelined):
     """W in-process ranks on one GPU (threads + a local all-to-all) train the
     owner-partitioned sharded step; the union of their shards equals one
     engine trained on the concatenated batches (same check as the gloo
-    multi-rank test, here through the HIP partitioned dedup)."""
+    multi-rank test, here through the HIP partitioned dedup, the owner
+    grouping and the one-launch multi-source apply; pipelined: each step
+    prepares the next batch into the other worker buffer set)."""
     import threading
 
     from xflow_amd.testing.hashing import owner_of
@@ -126,7 +131,7 @@ def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind):
     def mk():
         return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
                       EngineConfig(table_log2_cap=16, max_rows=world * rows,
-                                   max_nnz=world * rows * 16, max_slices=world),
+                                   max_nnz=world * rows * 16, max_slices=world * S),
                       device=gpu_device)
 
     def data(r, s):
@@ -139,9 +144,10 @@ def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind):
     def run(r):
         try:
             sh = _local_sharded(bus, r, engines[r])
+            bs = [to_batch(*data(r, s), gpu_device, slice_rows=rows // S) for s in range(steps)]
             for s in range(steps):
-                k, rp, fg, lab = data(r, s)
-                sh.train_step(to_batch(k, rp, fg, lab, gpu_device), S=1)
+                nxt = bs[s + 1] if pipelined and s + 1 < steps else None
+                sh.train_step(bs[s], S=S, next_batch=nxt)
             torch.cuda.synchronize()
         except BaseException as e:  # surfaced below
             errors.append(e)
@@ -162,9 +168,10 @@ def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind):
         rp = np.concatenate([parts[0][1]] + [p[1][1:] + sum(len(q[0]) for q in parts[:i + 1])
                                              for i, p in enumerate(parts[1:])])
         ref.train_step(to_batch(keys, rp.astype(np.int32), fg, lab, gpu_device,
-                                slice_rows=rows))
+                                slice_rows=rows // S))
     allk, allv = [], []
     for r, e in enumerate(engines):
+        assert not e.overflowed()
         k, _ = e.export_table()
         assert (owner_of(k, world) == r).all()
         allk.append(k)

@@ -29,15 +29,18 @@ def _make_engine(kind, slices):
                                max_slices=4 * slices))
 
 
-def _sharded_worker(rank, world, kind, slices, out_dir):
+def _sharded_worker(rank, world, kind, slices, out_dir, pipelined=False):
     from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
     eng = _make_engine(kind, slices)
     sh = ShardedEngine(eng)
+    batches = [to_batch(*_batches(rank, step), torch.device("cpu"), slice_rows=ROWS // slices)
+               for step in range(STEPS)]
     for step in range(STEPS):
-        k, rp, fg, lab = _batches(rank, step)
-        sh.train_step(to_batch(k, rp, fg, lab, torch.device("cpu"), slice_rows=ROWS // slices),
-                      S=slices)
+        # pipelined: the next batch is prepared (dedup, counts exchange) inside
+        # this step, into the other worker buffer set
+        nxt = batches[step + 1] if pipelined and step + 1 < STEPS else None
+        sh.train_step(batches[step], S=slices, next_batch=nxt)
     keys, words = eng.export_table()
     np.save(os.path.join(out_dir, f"keys{rank}.npy"), keys)
     vals = eng.pull(keys) if len(keys) else np.zeros((0, eng.params_per_key), np.float32)
@@ -46,10 +49,11 @@ def _sharded_worker(rank, world, kind, slices, out_dir):
     np.save(os.path.join(out_dir, f"stats{rank}.npy"), np.array([st["rows"], st["ln_loss"]]))
 
 
-@pytest.mark.parametrize("kind,slices", [("lr", 1), ("lr", 2), ("fm", 2), ("mvm", 1)])
-def test_sharded_equals_single_rank(tmp_path, kind, slices):
-    world = 2
-    run_world(_sharded_worker, world, kind, slices, str(tmp_path))
+@pytest.mark.parametrize("kind,slices,pipelined,world",
+                         [("lr", 1, False, 2), ("lr", 2, False, 2), ("fm", 2, False, 2),
+                          ("mvm", 1, False, 2), ("lr", 2, True, 3), ("fm", 1, True, 2)])
+def test_sharded_equals_single_rank(tmp_path, kind, slices, pipelined, world):
+    run_world(_sharded_worker, world, kind, slices, str(tmp_path), pipelined)
     # single-rank replay: concatenated batches, world*slices ordered slices
     ref = _make_engine(kind, slices)
     for step in range(STEPS):
@@ -57,7 +61,8 @@ def test_sharded_equals_single_rank(tmp_path, kind, slices):
         keys = np.concatenate([p[0] for p in parts])
         fg = np.concatenate([p[2] for p in parts])
         lab = np.concatenate([p[3] for p in parts])
-        rp = np.concatenate([parts[0][1]] + [p[1][1:] + len(parts[0][0]) for p in parts[1:]])
+        rp = np.concatenate([parts[0][1]] + [p[1][1:] + sum(len(q[0]) for q in parts[:i + 1])
+                                             for i, p in enumerate(parts[1:])])
         ref.train_step(to_batch(keys, rp.astype(np.int32), fg, lab, torch.device("cpu"),
                                 slice_rows=ROWS // slices))
     allk, allv = [], []

@@ -199,29 +199,36 @@ class Engine:
         return self._e.pull_host(k).reshape(len(k), self.params_per_key)
 
     # ---- multi-rank phases (driven by parallel.sparse_a2a) ----------------------
-    def w_prepare(self, batch: Batch, world: int, counts: torch.Tensor, send_keys: torch.Tensor):
+    # wb: worker buffer set (0/1) holding a prepared batch's dedup state, so the
+    # next batch can be prepared while the current one is still in flight.
+    def w_prepare(self, batch: Batch, world: int, counts: torch.Tensor, send_keys: torch.Tensor,
+                  wb: int = 0):
         batch.check(self.device)
         self._sync_stream()
-        self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr())
+        self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr(), int(wb))
 
     def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor,
-               insert: bool = True, buf: int = 0) -> None:
+               insert: bool = True, buf: int = 0, offsets=None) -> None:
+        """Owner pull of n received keys; ``offsets`` (world+1 source
+        boundaries) lets the GPU backend group the sources for a one-launch apply."""
         self._sync_stream()
-        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr(), insert, int(buf))
+        self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr(), insert, int(buf),
+                       [int(o) for o in offsets] if offsets is not None else [])
 
     def w_forward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
-                  pctr: torch.Tensor | None) -> None:
+                  pctr: torch.Tensor | None, wb: int = 0) -> None:
         self._sync_stream()
         self._e.w_forward(batch.view(), pulled.data_ptr(), int(n_send),
-                          pctr.data_ptr() if pctr is not None else 0)
+                          pctr.data_ptr() if pctr is not None else 0, int(wb))
 
     def w_forward_backward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
                            grads_out: torch.Tensor, masks_out: torch.Tensor | None,
-                           S: int = 0) -> None:
+                           S: int = 0, wb: int = 0) -> None:
         self._sync_stream()
         self._e.w_forward_backward(batch.view(), pulled.data_ptr(), int(n_send),
                                    grads_out.data_ptr(),
-                                   masks_out.data_ptr() if masks_out is not None else 0, int(S))
+                                   masks_out.data_ptr() if masks_out is not None else 0, int(S),
+                                   int(wb))
 
     def s_apply(self, recv_keys: torch.Tensor, recv_grads: torch.Tensor,
                 recv_masks: torch.Tensor | None, offsets, S: int, buf: int = 0) -> None:

@@ -7,16 +7,19 @@ fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
 
   1. w_prepare    dedup the batch's keys grouped by owner (owner-partitioned
                   scratch on the GPU, a bucket pass on the CPU backend)
-  2. a2a counts   (int64 x world), one host sync for the split sizes (hidden
-                  behind the next batch's generation, see _exchange_keys)
+  2. a2a counts   (int64 x world); the split sizes return through pinned
+                  memory and are read when the batch's step starts -- with
+                  next_batch, one step after they were produced (see prepare)
   3. a2a keys     -> each owner receives the keys it serves
   4. s_pull       owner probes/inserts its shard, evaluates pull values
   5. a2a values   -> back to the requesting workers (send order)
   6. w_forward_backward  fused fwd/bwd on the rank's rows, per-(key,slice)
                   gradient sums normalised by slice rows, in send order
   7. a2a grads    (+ slice masks when slices are applied in order)
-  8. s_apply      owner applies contributions source by source (fixed order:
-                  deterministic, the analogue of ps-lite's serialized handler)
+  8. s_apply      owner applies every (source, slice) contribution of a key in
+                  source order (deterministic, the analogue of ps-lite's
+                  serialized handler) -- one launch for all sources on the GPU,
+                  grouped by key during the pull
 
 On GPUs the all-to-alls go through the native RCCL communicator on the
 engine's stream (csrc/comm/rccl_comm.h; xGMI peer links between the node's
@@ -59,7 +62,17 @@ class _Buf:
 
 
 class ShardedEngine:
-    """Runs Engine phases with sparse all-to-alls between them."""
+    """Runs Engine phases with sparse all-to-alls between them.
+
+    Pipelined step: ``train_step(batch, next_batch=...)`` prepares the next
+    batch (dedup + owner counts + counts exchange into the other worker buffer
+    set, split sizes copied to pinned host memory) in the middle of the current
+    step, before its forward/backward.  The host reads those split sizes only
+    when it starts the next step, by which time the device copy finished long
+    ago (it sits ahead of the current step's forward/backward, gradient
+    exchange and apply in the queue): the host never waits on an in-flight
+    exchange and stays about one step ahead of the device.  Without
+    next_batch a step prepares its own batch first (one host wait per step)."""
 
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
                  world: Optional[int] = None, rank: Optional[int] = None,
@@ -73,11 +86,12 @@ class ShardedEngine:
         self.world = int(world) if world is not None else dist.get_world_size(group)
         self.rank = int(rank) if rank is not None else dist.get_rank(group)
         dev = engine.device
-        # send and receive counts side by side: one D2H copy returns both
-        self._counts_both = torch.zeros(2 * self.world, dtype=torch.int64, device=dev)
-        self.counts = self._counts_both[: self.world]
-        self.recv_counts = self._counts_both[self.world:]
-        self.send_keys = torch.empty(max(engine.cfg.max_nnz, 1), dtype=torch.int64, device=dev)
+        W = self.world
+        # per worker buffer set: send and receive counts side by side (one D2H
+        # copy returns both), the owner-grouped send keys
+        self._counts_both = [torch.zeros(2 * W, dtype=torch.int64, device=dev) for _ in range(2)]
+        self._send_keys = [torch.empty(max(engine.cfg.max_nnz, 1), dtype=torch.int64, device=dev)
+                           for _ in range(2)]
         self._recv_keys = _Buf(torch.int64, dev)
         # one per server buffer: compact-FM applies read the values served
         # by their step's pull (the async step applies after the next pull)
@@ -90,8 +104,11 @@ class ShardedEngine:
         self.last_send = 0
         self.last_recv = 0
         self.bytes_moved = 0
+        self.host_waits = 0        # split-size reads that found the copy still in flight
         self._counts_host = None
         self._counts_ready = None
+        self._prep = None          # (batch, worker buffer set) prepared ahead
+        self._next_wb = 0
         self._comm = None
         self.transport = "custom"
         if not custom:
@@ -110,6 +127,16 @@ class ShardedEngine:
         if transport == "torch" or not self.engine.is_gpu or self.group is not None:
             self.transport = "torch"
             return
+        comm = self._new_comm()
+        if comm is not None:
+            self._comm = comm
+            self.transport = "rccl"
+        else:
+            self.transport = "torch"
+
+    def _new_comm(self):
+        """A verified native RCCL communicator over the job's ranks, or None
+        on every rank when any rank failed to create or self-test it."""
         from xflow_amd import native
 
         n = native.load()
@@ -126,12 +153,10 @@ class ShardedEngine:
         flag = torch.tensor([ok], dtype=torch.int32, device=self.engine.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if int(flag.item()) == 1:
-            self._comm = comm
-            self.transport = "rccl"
-        else:
-            if comm is not None:
-                comm.abort()
-            self.transport = "torch"
+            return comm
+        if comm is not None:
+            comm.abort()
+        return None
 
     def _selftest(self, comm, timeout_s: float = 60.0) -> bool:
         W = self.world
@@ -149,91 +174,150 @@ class ShardedEngine:
             time.sleep(0.001)
         return recv.cpu().tolist() == list(range(W))
 
+    @staticmethod
+    def _row_bytes(t: torch.Tensor) -> int:
+        return math.prod(t.shape[1:]) * t.element_size()  # bytes per split unit
+
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
         if self._comm is None:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
             return
-        row = math.prod(inp.shape[1:]) * inp.element_size()  # bytes per split unit
         stream = torch.cuda.current_stream(self.engine.device).cuda_stream
         if out_splits is None:
-            self._comm.alltoall(inp.data_ptr(), out.data_ptr(), inp.shape[0] // self.world, row,
-                                stream)
+            self._comm.alltoall(inp.data_ptr(), out.data_ptr(), inp.shape[0] // self.world,
+                                self._row_bytes(inp), stream)
         else:
             self._comm.alltoallv(inp.data_ptr(), [int(x) for x in in_splits], out.data_ptr(),
-                                 [int(x) for x in out_splits], row, stream)
+                                 [int(x) for x in out_splits], self._row_bytes(inp), stream)
 
-    def _exchange_keys(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
-        """Dedup + bucket + key all-to-all.  Returns (send, recv splits, recv keys).
+    def _a2a_ops(self, ops) -> None:
+        """Several all-to-alls, each (out, inp, out_splits, in_splits) with
+        None splits meaning equal parts: ONE RCCL group call (one kernel)
+        natively, one call each (in list order on every rank) otherwise."""
+        if self._comm is None or len(ops) == 1:
+            for out, inp, osp, isp in ops:
+                self._a2a(out, inp, osp, isp)
+            return
+        W = self.world
+        stream = torch.cuda.current_stream(self.engine.device).cuda_stream
+        sc, rc = [], []
+        for out, inp, osp, isp in ops:
+            sc.append([inp.shape[0] // W] * W if isp is None else [int(x) for x in isp])
+            rc.append([out.shape[0] // W] * W if osp is None else [int(x) for x in osp])
+        self._comm.alltoallv_group([inp.data_ptr() for _, inp, _, _ in ops],
+                                   [out.data_ptr() for out, _, _, _ in ops],
+                                   [self._row_bytes(inp) for _, inp, _, _ in ops], sc, rc, stream)
 
-        ``prefetch`` (e.g. generating or staging the next batch) is enqueued on
-        the device after the counts exchange and before the host waits for
-        the split sizes, so the device works through that round trip."""
+    # ---- phases ---------------------------------------------------------------
+    def prepare(self, batch: Batch, exchange: bool = True) -> None:
+        """Dedup + owner grouping + counts exchange of ``batch`` into the next
+        worker buffer set.  Collective: every rank prepares at the same point.
+        exchange=False leaves the counts exchange to the caller, which joins it
+        to another exchange's group call (_counts_op) and then calls
+        _counts_sent."""
         e = self.engine
-        e.w_prepare(batch, self.world, self.counts, self.send_keys)
-        self._a2a(self.recv_counts, self.counts, None, None)
-        both = self._counts_both
+        W = self.world
+        wb = self._next_wb
+        self._next_wb ^= 1
+        both = self._counts_both[wb]
+        e.w_prepare(batch, W, both[:W], self._send_keys[wb], wb)
+        self._prep = (batch, wb)
+        if exchange:
+            self._a2a(both[W:], both[:W], None, None)
+            self._counts_sent(wb)
+
+    def _counts_op(self, wb: int):
+        both = self._counts_both[wb]
+        return (both[self.world:], both[:self.world], None, None)
+
+    def _counts_sent(self, wb: int) -> None:
+        both = self._counts_both[wb]
         if both.is_cuda:
             # the split sizes come back through pinned memory right behind the
-            # counts exchange; the prefetch queues after that copy, so the
-            # device generates the next batch while the host waits and then
-            # launches the key exchange
+            # counts exchange; read by the step that uses this batch
             if self._counts_host is None:
-                self._counts_host = torch.empty(2 * self.world, dtype=torch.int64,
-                                                pin_memory=True)
-                self._counts_ready = torch.cuda.Event()
-            self._counts_host.copy_(both, non_blocking=True)
-            self._counts_ready.record()
-            if prefetch is not None:
-                prefetch()
-            self._counts_ready.synchronize()
-            both = self._counts_host.tolist()
-        else:
-            if prefetch is not None:
-                prefetch()
-            both = both.tolist()
-        send_splits, recv_splits = both[: self.world], both[self.world:]
-        n_send, n_recv = int(sum(send_splits)), int(sum(recv_splits))
-        self.last_send, self.last_recv = n_send, n_recv
-        recv_keys = self._recv_keys.get(n_recv)
-        self._a2a(recv_keys, self.send_keys[:n_send], recv_splits, send_splits)
-        return send_splits, recv_splits, recv_keys
+                self._counts_host = [torch.empty(2 * self.world, dtype=torch.int64,
+                                                 pin_memory=True) for _ in range(2)]
+                self._counts_ready = [torch.cuda.Event(), torch.cuda.Event()]
+            self._counts_host[wb].copy_(both, non_blocking=True)
+            self._counts_ready[wb].record()
 
-    def _pull(self, recv_keys, send_splits, recv_splits, insert: bool, buf: int = 0) -> torch.Tensor:
-        e = self.engine
-        ps = e.pstride
-        n_send, n_recv = sum(send_splits), sum(recv_splits)
-        vals = self._vals_out[buf].get(n_recv * ps).view(n_recv, ps)
-        e.s_pull(recv_keys, n_recv, vals, insert=insert, buf=buf)
-        pulled = self._pulled.get(n_send * ps).view(n_send, ps)
-        self._a2a(pulled, vals, send_splits, recv_splits)
-        return pulled
+    def _take(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
+        """(worker buffer set, send splits, recv splits) of ``batch``, preparing
+        it now unless it is the batch prepared ahead."""
+        if self._prep is None or self._prep[0] is not batch:
+            self.prepare(batch)
+            if prefetch is not None:  # device work to overlap the split-size round trip
+                prefetch()
+                prefetch = None
+        _, wb = self._prep
+        self._prep = None
+        W = self.world
+        both = self._counts_both[wb]
+        if both.is_cuda:
+            ev = self._counts_ready[wb]
+            if not ev.query():
+                self.host_waits += 1
+                ev.synchronize()
+            both = self._counts_host[wb].tolist()
+        else:
+            both = both.tolist()
+        send_splits, recv_splits = both[:W], both[W:]
+        self.last_send, self.last_recv = int(sum(send_splits)), int(sum(recv_splits))
+        return wb, send_splits, recv_splits, prefetch
+
+    def _exchange_keys(self, wb: int, send_splits, recv_splits) -> torch.Tensor:
+        recv_keys = self._recv_keys.get(self.last_recv)
+        self._a2a(recv_keys, self._send_keys[wb][:self.last_send], recv_splits, send_splits)
+        return recv_keys
+
+    @staticmethod
+    def _offsets(splits):
+        offs = [0]
+        for c in splits:
+            offs.append(offs[-1] + int(c))
+        return offs
 
     def train_step(self, batch: Batch, S: Optional[int] = None,
-                   prefetch: Optional[Callable[[], None]] = None) -> None:
+                   prefetch: Optional[Callable[[], None]] = None,
+                   next_batch: Optional[Batch] = None) -> None:
         """One lock-step training step.  S = slices per step, identical on every
         rank (defaults to this batch's slice count, fine when all ranks use the
-        same batch shape).  ``prefetch``: see _exchange_keys."""
+        same batch shape).  ``prefetch``: device work producing the next batch
+        (e.g. the synthetic generator), queued before ``next_batch`` is
+        prepared.  Every rank must pass next_batch (or not) alike."""
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.pstride
         ordered_masks = S > 1 and not e.cfg.sum_slices
-        send_splits, recv_splits, recv_keys = self._exchange_keys(batch, prefetch)
+        wb, send_splits, recv_splits, prefetch = self._take(batch, prefetch)
         n_send, n_recv = self.last_send, self.last_recv
-        pulled = self._pull(recv_keys, send_splits, recv_splits, insert=True)
+        recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
+        offsets = self._offsets(recv_splits)
+        vals = self._vals_out[0].get(n_recv * ps).view(n_recv, ps)
+        e.s_pull(recv_keys, n_recv, vals, insert=True, buf=0, offsets=offsets)
+        if prefetch is not None:
+            prefetch()
+        pulled = self._pulled.get(n_send * ps).view(n_send, ps)
+        ops = [(pulled, vals, send_splits, recv_splits)]
+        if next_batch is not None:
+            # the next batch's counts travel in the same group call as the values
+            self.prepare(next_batch, exchange=False)
+            ops.append(self._counts_op(self._prep[1]))
+        self._a2a_ops(ops)
+        if next_batch is not None:
+            self._counts_sent(self._prep[1])
 
         W = S * e.grad_width  # (B, C) per slice for reference-math FM on the GPU
         grads_out = self._grads_out.get(n_send * W).view(n_send, W)
         masks_out = self._masks_out.get(n_send) if ordered_masks else None
-        e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S)
+        e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S, wb=wb)
         grads_in = self._grads_in.get(n_recv * W).view(n_recv, W)
-        self._a2a(grads_in, grads_out, recv_splits, send_splits)
-        masks_in = None
-        if ordered_masks:
-            masks_in = self._masks_in.get(n_recv)
-            self._a2a(masks_in, masks_out, recv_splits, send_splits)
-        offsets = [0]
-        for c in recv_splits:
-            offsets.append(offsets[-1] + int(c))
+        masks_in = self._masks_in.get(n_recv) if ordered_masks else None
+        ops = [(grads_in, grads_out, recv_splits, send_splits)]
+        if ordered_masks:  # slice masks in the same group call
+            ops.append((masks_in, masks_out, recv_splits, send_splits))
+        self._a2a_ops(ops)
         e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
         e.w_finish()
         self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)  # W = S * grad_width
@@ -244,9 +328,14 @@ class ShardedEngine:
         e = self.engine
         if pctr is None:
             pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
-        send_splits, recv_splits, recv_keys = self._exchange_keys(batch)
-        pulled = self._pull(recv_keys, send_splits, recv_splits, insert=False)
-        e.w_forward(batch, pulled, self.last_send, pctr if batch.rows else None)
+        wb, send_splits, recv_splits, _ = self._take(batch)
+        recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
+        ps = e.pstride
+        vals = self._vals_out[0].get(self.last_recv * ps).view(self.last_recv, ps)
+        e.s_pull(recv_keys, self.last_recv, vals, insert=False, buf=0)
+        pulled = self._pulled.get(self.last_send * ps).view(self.last_send, ps)
+        self._a2a(pulled, vals, send_splits, recv_splits)
+        e.w_forward(batch, pulled, self.last_send, pctr if batch.rows else None, wb=wb)
         return pctr
 
     def close(self) -> None:
