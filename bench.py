@@ -45,6 +45,12 @@ def parse():
     ap.add_argument("--log2-cap", type=int, default=0,
                     help="table slots per GPU = 2^N (default: 2^31 across the node)")
     ap.add_argument("--features", type=int, default=1_000_000_000)
+    ap.add_argument("--table-load", type=float, default=-1.0,
+                    help="before training (untimed), fill this fraction of every table shard's "
+                         "slots with keys no batch touches -- the occupancy a long run reaches "
+                         "(the reference store keeps every key ever pushed, ftrl.h:54-56,84).  "
+                         "Default (-1): the whole --features model, i.e. features/N keys per "
+                         "GPU (load 0.47 of 2^31/N slots for 1e9 features); 0 = empty table")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (smoke only)")
     ap.add_argument("--sharded", action="store_true",
@@ -104,6 +110,14 @@ def main():
                                  max_slices=1),
                     device=device)
     gen = SyntheticCriteo(engine, a.batch, synth, rank=rank)
+    if a.table_load < 0:  # (the CPU smoke path runs on a small table: no default prefill)
+        n_prefill = a.features // world if use_gpu else 0
+    else:
+        n_prefill = int(a.table_load * 2 ** log2_cap)
+    n_prefill = min(n_prefill, int(0.9 * 2 ** log2_cap))
+    if n_prefill > 0:
+        engine.prefill(n_prefill, seed=0x5eed + rank)
+    prefilled = engine.table_size()
 
     sharded = None
     if world > 1 or a.sharded or a.async_p2p:
@@ -171,7 +185,8 @@ def main():
     tbl = engine.table_size()
     nnzw = engine.nonzero_weights() if a.async_p2p else 0
     ovf = float(engine.overflowed())  # table probe wrap / dedup scratch overflow
-    red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw), ovf],
+    red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw), ovf,
+                        float(prefilled)],
                        dtype=torch.float64, device=device)
     if world > 1:
         mx = red[:1].clone()
@@ -180,6 +195,7 @@ def main():
         elapsed = float(mx.item())
     vals = red.tolist()
     ln_loss, rows, table_keys, nonzero = vals[1], vals[2], vals[3], vals[4]
+    prefill_tot = vals[6]
     if vals[5] > 0:
         raise SystemExit("bench: a table or dedup-scratch overflow was flagged (keys would be "
                          "dropped or isolated): the result is invalid")
@@ -198,8 +214,9 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic Criteo-1TB-shaped (39 fields: 13 log-binned int + 26 categorical, "
-                    "power-law values, 1e9 hashed features, planted-logistic labels); "
-                    "zero-init FTRL table",
+                    "power-law values, 1e9 hashed features, planted-logistic labels); FTRL table "
+                    "prefilled (untimed) with %d keys the batches never touch (a long run's "
+                    "table occupancy), trained keys zero-init" % int(prefill_tot),
             "config": {"model": f"{a.model.upper()}-{a.optimizer.upper()}",
                        "global_batch": a.batch * world, "seq_len": synth.fields,
                        "parallelism": f"dp{world}+table-shard{world}",
@@ -211,6 +228,7 @@ def main():
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
             "table_load": table_keys / float(world * 2 ** log2_cap),
+            "prefilled_keys": int(prefill_tot),
             "host_waits": int(sharded.host_waits) if sharded is not None else 0,
         }
         if a.async_p2p:

@@ -391,6 +391,14 @@ class CpuBackend final : public Backend {
       std::memcpy(t.words + (u64)slot * t.L.stride + 2, words + i * W, sizeof(u32) * W);
     }
   }
+  void table_prefill(const TableView& t, int64_t n, u64 seed) override {
+    for (int64_t i = 0; i < n; ++i) {
+      bool claimed = false;
+      const u32 slot = probe(t, prefill_key(seed, (u64)i), true, claimed);
+      if (claimed) ++*t.size;
+      if (slot != kNoSlot && t.L.has_flag) t.words[(u64)slot * t.L.stride + t.L.flag_word] = 1u;
+    }
+  }
   int64_t table_nonzero(const TableView& t, const OptSpec& o) override {
     int64_t n = 0;
     for (u64 s = 0; s < t.cap; ++s) {

@@ -411,6 +411,14 @@ void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& g
   be_->synchronize();
 }
 
+void Engine::prefill(int64_t n, uint64_t seed) {
+  if (n < 0 || (uint64_t)n > table_.cap - table_.cap / 16)
+    throw std::invalid_argument("prefill: at most 15/16 of the table's slots");
+  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;
+  be_->table_prefill(table_, n, seed);
+  be_->synchronize();
+}
+
 std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
   const int64_t n = (int64_t)keys.size();
   const int P = cfg_.model.P();

@@ -113,6 +113,9 @@ class HipBackend final : public Backend {
   void table_import(const TableView& t, const u64* keys, const u32* words, int64_t n) override {
     hip::launch_table_import(t, keys, words, n, stream_);
   }
+  void table_prefill(const TableView& t, int64_t n, u64 seed) override {
+    hip::launch_table_prefill(t, n, seed, stream_);
+  }
   int64_t table_nonzero(const TableView& t, const OptSpec& o) override {
     hip::launch_table_nonzero(t, o, counter_, stream_);
     unsigned long long n = 0;

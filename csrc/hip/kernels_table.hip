@@ -456,8 +456,17 @@ __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, b
 // one block apart and issues all first-probe loads before resolving any (the
 // table is tens of GB: every probe is an HBM miss, so memory-level parallelism
 // is what matters).
+//
+// Line-at-a-time probing: the first round loads only the key's home slot (at
+// low load it answers almost every probe); a chain that continues loads the
+// REST of the aligned 64-byte line (up to 3 slots, independent dwordx4
+// loads) in one round trip and resolves those probe positions from
+// registers, then whole lines.  Same table layout and probe order as
+// one-slot linear probing, but at a realistic load (0.47: a 1e9-key model in
+// 2^31 slots) a chain costs one extra round trip per line, not per slot.
 constexpr int kPullItems = 4;
 constexpr int kPullChunk = kBlock * kPullItems;
+constexpr int kLineSlots = 4;  // 16-byte slots per 64-byte line
 
 __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp,
                                                       const u64* __restrict__ keys,
@@ -494,28 +503,55 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
     float w = 0.0f;
     float2 nz = make_float2(0.0f, 0.0f);  // fresh slot: zero state
     u64 sj = s[j];
-    uint4 vj = v[j];
-    for (u64 c = 0; c < t.cap; ++c) {
-      u64 cur = (u64)vj.x | ((u64)vj.y << 32);
-      if (cur == key[j]) {
-        slot = (u32)sj;
-        nz = make_float2(__uint_as_float(vj.z), __uint_as_float(vj.w));
-        w = ftrl_weight(nz.y, nz.x, fp);
-        break;
-      }
-      if (cur == kEmptyKey) {
-        if (!insert) break;
-        u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[sj]),
-                             (unsigned long long)kEmptyKey, (unsigned long long)key[j]);
-        // fresh slot, or claimed by another lane this launch: state is zero -> w = 0
-        if (prev == kEmptyKey || prev == key[j]) {
-          claims += prev == kEmptyKey;
-          slot = (u32)sj;
-          break;
+    int q0 = (int)(sj & (kLineSlots - 1)), q1 = q0 + 1;  // registers hold [q0, q1) of the line
+    uint4 ln[kLineSlots];
+#pragma unroll
+    for (int q = 0; q < kLineSlots; ++q) ln[q] = v[j];  // (only ln[q0] is read in round one)
+    bool done = false;
+    for (u64 c = 0; c < t.cap && !done;) {
+#pragma unroll
+      for (int q = 0; q < kLineSlots; ++q) {
+        if (q < q0 || q >= q1 || done) continue;
+        const u64 cur = (u64)ln[q].x | ((u64)ln[q].y << 32);
+        const u64 sq = (sj & ~(u64)(kLineSlots - 1)) + (u64)q;
+        if (cur == key[j]) {
+          slot = (u32)sq;
+          nz = make_float2(__uint_as_float(ln[q].z), __uint_as_float(ln[q].w));
+          w = ftrl_weight(nz.y, nz.x, fp);
+          done = true;
+        } else if (cur == kEmptyKey) {
+          if (!insert) {
+            done = true;
+          } else {
+            const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(&slots[sq]),
+                                       (unsigned long long)kEmptyKey, (unsigned long long)key[j]);
+            if (prev == kEmptyKey) {  // fresh slot: state is zero -> w = 0
+              ++claims;
+              slot = (u32)sq;
+              done = true;
+            } else if (prev == key[j]) {  // claimed by another lane this launch
+              slot = (u32)sq;
+              done = true;
+            }
+            // else: taken by another key meanwhile -- keep probing
+          }
         }
       }
-      sj = (sj + 1) & mask;
-      vj = slots[sj];
+      if (done) break;
+      c += (u64)(q1 - q0);
+      // next: the rest of this line after the home slot, then whole lines --
+      // every slot of a round is loaded at once (one dependent round trip)
+      if (q1 < kLineSlots) {
+        q0 = q1;
+      } else {
+        sj = ((sj | (u64)(kLineSlots - 1)) + 1) & mask;
+        q0 = 0;
+      }
+      q1 = kLineSlots;
+      const uint4* line = slots + (sj & ~(u64)(kLineSlots - 1));
+#pragma unroll
+      for (int q = 0; q < kLineSlots; ++q)
+        if (q >= q0) ln[q] = line[q];
     }
     if (insert && slot == kNoSlot) *t.overflow = 1u;
     if (out_slot) out_slot[i] = slot;
@@ -1192,6 +1228,26 @@ __global__ void __launch_bounds__(kBlock) k_table_import(TableView t, const u64*
     for (int w = 0; w < W; ++w) sp[2 + w] = words[i * W + w];
   }
   block_count_add<kBlock>(t.size, claims);
+}
+
+__global__ void __launch_bounds__(kBlock) k_table_prefill(TableView t, int64_t n, u64 seed) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned int claims = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u64 key = prefill_key(seed, (u64)i);
+    bool claimed = false;
+    const u32 slot = probe(t, key, true, claimed);
+    claims += claimed;
+    if (slot != kNoSlot && t.L.has_flag) t.words[(u64)slot * t.L.stride + t.L.flag_word] = 1u;
+  }
+  block_count_add<kBlock>(t.size, claims);
+}
+
+void launch_table_prefill(const TableView& t, int64_t n, u64 seed, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_table_prefill, dim3(grid_for(n, kBlock, 16384)), dim3(kBlock), 0, st, t, n,
+                     seed);
+  XF_HIP_CHECK(hipGetLastError());
 }
 
 void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,

@@ -317,6 +317,11 @@ class Backend {
   virtual int64_t table_nonzero(const TableView& t, const OptSpec& o) = 0;
   virtual void table_import(const TableView& t, const u64* keys, const u32* words,
                             int64_t n) = 0;
+  // Insert n synthetic keys (1 << 62 | hash(seed, i) >> 2: disjoint from any
+  // key below 2^62, e.g. hashed features) with zero state, marked pushed --
+  // keys a long run has accumulated but the current batches do not touch
+  // (occupancy-realistic benchmarks).
+  virtual void table_prefill(const TableView& t, int64_t n, u64 seed) = 0;
 };
 
 std::unique_ptr<Backend> make_cpu_backend();

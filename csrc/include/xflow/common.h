@@ -43,6 +43,12 @@ XF_HD u64 fmix64(u64 h) {
   return h;
 }
 
+// Synthetic "historic" key i of a prefilled table (Backend::table_prefill):
+// bit 62 set, so it never equals a hashed feature below 2^62.
+XF_HD u64 prefill_key(u64 seed, u64 i) {
+  return (1ull << 62) | (fmix64(seed * 0x9E3779B97F4A7C15ull + i) >> 2);
+}
+
 XF_HD u32 owner_of(u64 key, u32 world) {
   return world <= 1 ? 0u : (u32)((fmix64(key) >> 32) % world);
 }

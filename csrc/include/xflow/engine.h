@@ -54,6 +54,9 @@ class Engine {
   // Push explicit gradients (host arrays) to keys, like the reference's
   // initialisation pushes (lr_worker.cc:180-182, fm_worker.cc:248-252).
   void push_host(const std::vector<u64>& keys, const std::vector<float>& grads);
+  // Insert n synthetic keys no batch touches (Backend::table_prefill):
+  // occupancy-realistic benchmarks of a long run's table.
+  void prefill(int64_t n, uint64_t seed);
   // Pull current values (host) of keys without inserting them.
   std::vector<float> pull_host(const std::vector<u64>& keys);
 

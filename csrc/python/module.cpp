@@ -218,6 +218,8 @@ PYBIND11_MODULE(_xflow_native, m) {
              std::vector<float> g(grads.data(), grads.data() + grads.size());
              e.push_host(k, g);
            })
+      .def("prefill", &Engine::prefill, py::arg("n"), py::arg("seed") = 0x5eedull,
+           py::call_guard<py::gil_scoped_release>())
       .def("pull_host",
            [](Engine& e, py::array_t<uint64_t> keys) {
              std::vector<u64> k(keys.data(), keys.data() + keys.size());

@@ -194,6 +194,12 @@ class Engine:
         self._e.push_host(np.asarray(keys, dtype=np.uint64),
                           np.asarray(grads, dtype=np.float32).reshape(-1))
 
+    def prefill(self, n: int, seed: int = 0x5eed) -> None:
+        """Insert n synthetic keys that no batch touches (bit 62 set): a table
+        at the occupancy a long run reaches (untimed benchmark setup)."""
+        self._sync_stream()
+        self._e.prefill(int(n), int(seed))
+
     def pull(self, keys) -> np.ndarray:
         k = np.asarray(keys, dtype=np.uint64)
         return self._e.pull_host(k).reshape(len(k), self.params_per_key)
