@@ -139,6 +139,27 @@ __device__ __forceinline__ void block_count_add(unsigned long long* counter, uns
   }
 }
 
+// Deterministic gradient sums.  Float atomics add in whatever order the
+// hardware serves them, so a sum's rounding changes run to run.  The LR and
+// reference-FM reductions therefore accumulate fixed-point integers
+// (v * 2^FX, int64 LDS atomics): integer addition is associative, so every
+// partial and final sum is bitwise independent of the order.  2^36 for LR
+// (|loss| <= 1: totals < 2^27 rows fit, resolution 1.5e-11) and 2^32 for FM's
+// loss*vsum.  The value of a partial sum passed between kernels is the float
+// of the exact integer sum, itself order independent.
+template <int FX>
+__device__ __forceinline__ long long fx_from(float v) {
+  return (long long)__builtin_rint((double)v * (double)(1ull << FX));
+}
+template <int FX>
+__device__ __forceinline__ double fx_to_double(long long a) {
+  return (double)a * (1.0 / (double)(1ull << FX));
+}
+template <int NV>
+struct FxBits {
+  static constexpr int kFx = NV == 1 ? 36 : 32;
+};
+
 // Read a device-side element count, clamped to the launch's upper bound.
 __device__ __forceinline__ int64_t dev_count(const int64_t* n_dev, int64_t n_host,
                                              int64_t n_max) {

@@ -157,8 +157,9 @@ template <int LOG2, int NV = 1>
 struct ListAgg {
   static constexpr int kSlots = 1 << LOG2;
   static constexpr int kShift = red_shift(NV);
+  static constexpr int kFx = FxBits<NV>::kFx;
   u64 (*tag)[kSlots];
-  float (*acc)[kSlots * NV];
+  long long (*acc)[kSlots * NV];  // fixed-point sums (deterministic, see fx_from)
   unsigned short (*list)[kSlots / 2];
   u32* nlist;   // [3] list lengths, rotating over columns
   u32* hist;    // [red_nb]
@@ -169,7 +170,7 @@ struct ListAgg {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
       tag[0][i] = tag[1][i] = ~0ull;
 #pragma unroll
-      for (int v = 0; v < NV; ++v) acc[0][i * NV + v] = acc[1][i * NV + v] = 0.0f;
+      for (int v = 0; v < NV; ++v) acc[0][i * NV + v] = acc[1][i * NV + v] = 0ll;
     }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0u;
     if (threadIdx.x < 3) nlist[threadIdx.x] = 0u;
@@ -203,8 +204,11 @@ struct ListAgg {
     int h = 0;
     if (has) {
       h = insert(t, j, dest, claimed);
-      atomicAdd(&acc[t][h * NV], loss);
-      if constexpr (NV > 1) atomicAdd(&acc[t][h * NV + 1], loss2);
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV]),
+                (unsigned long long)fx_from<kFx>(loss));
+      if constexpr (NV > 1)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV + 1]),
+                  (unsigned long long)fx_from<kFx>(loss2));
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -220,13 +224,13 @@ struct ListAgg {
     for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
       const int hh = list[t][i];
       const u32 d = (u32)tag[t][hh];
-      const float v = acc[t][hh * NV];
-      acc[t][hh * NV] = 0.0f;
+      const float v = (float)fx_to_double<kFx>(acc[t][hh * NV]);
+      acc[t][hh * NV] = 0ll;
       if constexpr (NV == 1) {
         region[written + i] = (u64)d | ((u64)__float_as_uint(v) << 32);
       } else {
-        const float v2 = acc[t][hh * NV + 1];
-        acc[t][hh * NV + 1] = 0.0f;
+        const float v2 = (float)fx_to_double<kFx>(acc[t][hh * NV + 1]);
+        acc[t][hh * NV + 1] = 0ll;
         reinterpret_cast<uint4*>(region)[written + i] =
             make_uint4(d, __float_as_uint(v), __float_as_uint(v2), 0u);
       }
@@ -266,7 +270,8 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   constexpr int C = kLrRegCols;
   constexpr bool kCol = kAgg && !kRed;  // column tables with global atomics
   __shared__ u32 s_tag[kCol ? 2 : 1][kCol ? (1 << LOG2) : 1];
-  __shared__ float s_acc[kAgg ? 2 : 1][1 << LOG2];
+  __shared__ float s_acc[kCol ? 2 : 1][kCol ? (1 << LOG2) : 1];
+  __shared__ long long s_fx[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
   __shared__ int s_wmax[BLOCK / kWave];
   __shared__ u64 s_tag64[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
   __shared__ unsigned short s_list[kRed ? 2 : 1][kRed ? BLOCK : 1];
@@ -281,9 +286,11 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   if (active) rs = row_span(b, r);
   const int len = rs.len;
   // (the unused aggregator of an instantiation points at a 1-element array)
-  ColumnAgg<1, LOG2> agg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag[0][0]), s_acc};
+  ColumnAgg<1, LOG2> agg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag[0][0]),
+                         reinterpret_cast<float(*)[1 << LOG2]>(&s_acc[0][0])};
   if constexpr (kCol) agg.init();
-  ListAgg<LOG2> lagg{reinterpret_cast<u64(*)[1 << LOG2]>(&s_tag64[0][0]), s_acc,
+  ListAgg<LOG2> lagg{reinterpret_cast<u64(*)[1 << LOG2]>(&s_tag64[0][0]),
+                     reinterpret_cast<long long(*)[1 << LOG2]>(&s_fx[0][0]),
                      reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
                      s_nlist, s_hist, nullptr, 0u};
   if constexpr (kRed) {
@@ -622,10 +629,12 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
   using T = typename RedRec<NV>::T;
   constexpr int kShift = red_shift(NV);
   constexpr u32 kR = 1u << kShift;
-  __shared__ float acc[kR * NV];
+  constexpr int kFx = FxBits<NV>::kFx;
+  // fixed-point accumulators: the bucket's sums do not depend on record order
+  __shared__ long long acc[kR * NV];
   const u32 beg = start[blockIdx.x], end = start[blockIdx.x + 1];
   if (beg == end) return;
-  for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0.0f;
+  for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
   __syncthreads();
   const T* src = static_cast<const T*>(sorted);
   for (u32 i0 = beg + threadIdx.x; i0 < end; i0 += kRedUnroll * kRedBlock) {
@@ -639,11 +648,14 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
     for (int q = 0; q < kRedUnroll; ++q) {
       if (i0 + (u32)q * kRedBlock >= end) continue;
       if constexpr (NV == 1) {
-        atomicAdd(&acc[(u32)pr[q] & (kR - 1)], __uint_as_float((u32)(pr[q] >> 32)));
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[(u32)pr[q] & (kR - 1)]),
+                  (unsigned long long)fx_from<kFx>(__uint_as_float((u32)(pr[q] >> 32))));
       } else {
         const u32 l = pr[q].x & (kR - 1);
-        atomicAdd(&acc[l * 2], __uint_as_float(pr[q].y));
-        atomicAdd(&acc[l * 2 + 1], __uint_as_float(pr[q].z));
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2]),
+                  (unsigned long long)fx_from<kFx>(__uint_as_float(pr[q].y)));
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2 + 1]),
+                  (unsigned long long)fx_from<kFx>(__uint_as_float(pr[q].z)));
       }
     }
   }
@@ -654,22 +666,23 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
       // normalised like the gather would (lr_worker.cc:116-118, in double)
       const double rows = (double)f.rows[0];
       for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-        const float v = acc[i];
-        if (v == 0.0f) continue;
+        const long long a = acc[i];
+        if (a == 0) continue;
         const u32 o = f.inv[d0 + i];
-        if (o != 0xFFFFFFFFu) f.out[o] = (float)((double)v / rows);  // (not the trash slot)
+        if (o != 0xFFFFFFFFu) f.out[o] = (float)(fx_to_double<kFx>(a) / rows);  // (not the trash slot)
       }
     } else {
       float* g = f.grad + d0;
       for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-        const float v = acc[i];
-        if (v != 0.0f) g[i] = v;  // grad is zero outside this step's keys
+        const long long a = acc[i];
+        if (a != 0) g[i] = (float)fx_to_double<kFx>(a);  // grad is zero outside this step's keys
       }
     }
   } else {
     for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-      const float B = acc[2 * i], C = acc[2 * i + 1];
-      if (B == 0.0f && C == 0.0f) continue;
+      if (acc[2 * i] == 0 && acc[2 * i + 1] == 0) continue;
+      const float B = (float)fx_to_double<kFx>(acc[2 * i]);
+      const float C = (float)fx_to_double<kFx>(acc[2 * i + 1]);
       const u64 dest = d0 + i;
       if (f.compact) {  // expanded by the apply (k_apply_group)
         *reinterpret_cast<float2*>(f.grad + dest * f.ps) = make_float2(B, C);
@@ -716,7 +729,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int LOG2 = ilog2c(2 * BLOCK);
   __shared__ u64 s_tag64[2][1 << LOG2];
-  __shared__ float s_acc[2][(1 << LOG2) * 2];
+  __shared__ long long s_acc[2][(1 << LOG2) * 2];
   __shared__ unsigned short s_list[2][BLOCK];
   __shared__ u32 s_hist[kRedMaxBuckets];
   __shared__ u32 s_nlist[3];
