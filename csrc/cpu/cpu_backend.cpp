@@ -315,9 +315,9 @@ class CpuBackend final : public Backend {
   }
 
   void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
-                    int64_t n_max, int width, float* zero_out) override {
+                    int64_t n_max, int width, float* zero_out, int zero_width) override {
     int64_t n = count_of(n_dev, n_max, n_max);
-    if (zero_out) std::fill(zero_out, zero_out + n, 0.0f);
+    if (zero_out) std::fill(zero_out, zero_out + n * zero_width, 0.0f);
     for (int64_t i = 0; i < n; ++i) {
       int64_t r = map ? map[i] : i;
       std::memcpy(dst + r * width, src + i * width, sizeof(float) * width);

@@ -85,8 +85,6 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // slot-indexed buffers carry one extra row: the trash slot (index cap) that
   // a dedup probe overflow sends its occurrences to (flagged, never applied)
   const uint64_t rows1 = scratch_.cap + 1;
-  wpull_ = balloc<float>(be, rows1 * ps);
-  be.memset(wpull_ + scratch_.cap * ps, 0, sizeof(float) * ps);
   grad_ = balloc<float>(be, rows1 * cfg_.max_slices * ps);
   be.memset(grad_, 0, sizeof(float) * rows1 * cfg_.max_slices * ps);
   tmask_ = balloc<u32>(be, rows1);
@@ -98,7 +96,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref || mvm)) {
     const int nv = fm_ref ? 2 : 1, shift = red_shift(nv);
     const int group_rows = fm_ref ? kFmGroupRows : (mvm ? kMvmGroupRows : kLrGroupRows);
-    const uint64_t dests = (scratch_.cap + 1) * (uint64_t)cfg_.max_slices;  // + trash slot
+    // (the trash slot's occurrences are never reduced: FwdArgs::trash_pos)
+    const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
     const int nb = (int)((dests + (1ull << shift) - 1) >> shift);
     if (nb <= kRedMaxBuckets) {
       const int64_t groups = (cfg_.max_rows + group_rows - 1) / group_rows;
@@ -111,6 +110,11 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       if (mvm) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
     }
   }
+  // reference-math FM with the GPU reduction: compact (w, Σv, Σv^2, 0) value rows
+  fm_vals_ = red_pairs_ && fm_ref;
+  vstride_ = fm_vals_ ? 4 : ps;
+  wpull_ = balloc<float>(be, rows1 * vstride_);
+  be.memset(wpull_ + scratch_.cap * vstride_, 0, sizeof(float) * vstride_);
   stats_ = balloc<LossStats>(be, 2);
   be.memset(stats_, 0, 2 * sizeof(LossStats));
   bucket_ws_ = balloc<int64_t>(be, 512);
@@ -133,7 +137,7 @@ Engine::~Engine() {
                   srv_slots_[0], srv_slots_[1], srv_nz_[0], srv_nz_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, own_pos_[0],
-                  own_pos_[1], own_idx_[0], own_idx_[1]};
+                  own_pos_[1], own_idx_[0], own_idx_[1], srv_w_[0], srv_w_[1], fm_grad_};
   for (void* p : ptrs) be.free(p);
   for (WorkerSet& w : wset_) {
     void* wp[] = {w.pos, w.uniq_pos, w.inv, w.n_uniq, w.send_pos};
@@ -171,6 +175,7 @@ void Engine::use_worker_set(int wb) {
 }
 
 void Engine::set_reduction(FwdArgs& fa) const {
+  fa.trash_pos = (u32)scratch_.cap;
   if (!red_pairs_) return;
   fa.red_pairs = red_pairs_;
   fa.red_sorted = red_sorted_;
@@ -266,7 +271,13 @@ void Engine::train_step(const BatchView& b) {
     if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz);
     if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   }
-  dedup_(b, 1, nullptr, lr16);
+  // reference FM, one slice: the (B, C) sums land in unique order (dense apply read)
+  const bool fmu = fm_vals_ && S == 1;
+  if (fmu) {
+    ensure_inv();
+    if (!fm_grad_) fm_grad_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
+  }
+  dedup_(b, 1, nullptr, lr16 || fmu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)
 
   PullArgs pa;
@@ -280,9 +291,14 @@ void Engine::train_step(const BatchView& b) {
   pa.out_vals = wpull_;
   pa.out_map = uniq_pos_;
   pa.pstride = ps;
+  pa.fm_vals = fm_vals_;
   if (lr16) {
     pa.out_nz = lr_nz_;
     pa.zero_out = lr_grad_;
+  }
+  if (fmu) {
+    pa.zero_out = fm_grad_;
+    pa.zero_width = 2;
   }
   be_->table_pull(pa);
 
@@ -301,10 +317,16 @@ void Engine::train_step(const BatchView& b) {
   // reference-math FM on the GPU reduction path: (B, C) rows, expanded by the apply
   fa.fm_compact = fa.red_pairs && fa.agg_ok && cfg_.model.kind == kFM &&
                   cfg_.model.fm_math == kFmReference;
+  fa.fm_vals = fm_vals_;
+  if (fm_vals_ && !fa.fm_compact) throw std::logic_error("train_step: compact FM rows need the reduction");
   if (lr16) {
     fa.red_out = lr_grad_;
     fa.red_inv = inv_;
     fa.red_rows = srows;
+  }
+  if (fmu) {
+    fa.red_out = fm_grad_;
+    fa.red_inv = inv_;
   }
   be_->forward_backward(fa);
 
@@ -334,6 +356,12 @@ void Engine::train_step(const BatchView& b) {
     aa.slice_rows = nullptr;
     aa.nz_stash = lr_nz_;
   }
+  if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
+    aa.grads = fm_grad_;
+    aa.grad_map = nullptr;
+    aa.zero_after = false;
+    aa.gstride = 2;
+  }
   be_->table_apply(aa);
 }
 
@@ -351,6 +379,7 @@ void Engine::eval_step(const BatchView& b, float* pctr) {
   pa.out_vals = wpull_;
   pa.out_map = uniq_pos_;
   pa.pstride = pstride();
+  pa.fm_vals = fm_vals_;
   be_->table_pull(pa);
 
   FwdArgs fa;
@@ -362,6 +391,7 @@ void Engine::eval_step(const BatchView& b, float* pctr) {
   fa.stats = stats_ + 1;
   fa.model = cfg_.model;
   fa.S = 1;
+  fa.fm_vals = fm_vals_;
   be_->forward_backward(fa);
 }
 
@@ -469,7 +499,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
     // owner-partitioned scratch: the slot-ordered unique list is the send
     // order already; counts are range counts (one range at world 1).  inv_
     // (slot -> send index) lets the LR backward write the send buffer directly.
-    if (red_pairs_ && cfg_.model.kind == kLR) ensure_inv();
+    if (red_pairs_ && (cfg_.model.kind == kLR || fm_vals_)) ensure_inv();
     dedup_(b, world, send_keys_out, true, world == 1 ? counts_out : nullptr);
     inv_valid_ = inv_ != nullptr;
     if (world > 1) be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
@@ -514,7 +544,7 @@ bool Engine::lr16_layout() const {
 void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr,
                        int wb) {
   use_worker_set(wb);
-  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, pstride());
+  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, vstride_);
   FwdArgs fa;
   fa.batch = b;
   fa.pos = pos_;
@@ -524,14 +554,16 @@ void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, 
   fa.stats = stats_ + 1;
   fa.model = cfg_.model;
   fa.S = 1;
+  fa.fm_vals = fm_vals_;
   be_->forward_backward(fa);
 }
 
 void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert, int buf,
-                    const std::vector<int64_t>& src_offsets) {
+                    const std::vector<int64_t>& src_offsets, bool keep_weights) {
   ensure_server_capacity(n, buf);
   srv_n_[buf] = n;
   srv_vals_[buf] = out_vals;
+  srv_w_valid_[buf] = false;
   grp_[buf] = SrcGroups();
   if (n == 0) return;
   if (insert) group_entries(recv_keys, n, buf, src_offsets);
@@ -545,6 +577,19 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
   pa.out_slot = srv_slots_[buf];
   pa.out_vals = out_vals;
   pa.pstride = pstride();
+  pa.fm_vals = fm_vals_;
+  if (keep_weights && fm_vals_) {
+    // the per-parameter weights the workers' gradients refer to, for an apply
+    // that runs after other table updates (the staleness-1 step)
+    if (srv_w_cap_[buf] < n) {
+      be_->synchronize();
+      be_->free(srv_w_[buf]);
+      srv_w_cap_[buf] = n + n / 4 + 1024;
+      srv_w_[buf] = balloc<float>(*be_, (size_t)srv_w_cap_[buf] * pstride());
+    }
+    pa.out_w = srv_w_[buf];
+    srv_w_valid_[buf] = true;
+  }
   pa.out_nz = srv_nz_[buf];
   srv_nz_fresh_[buf] = srv_nz_[buf] != nullptr;
   be_->table_pull(pa);
@@ -631,10 +676,12 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
-  const bool direct = inv_valid_ && red_pairs_ && S == 1 && cfg_.model.kind == kLR &&
+  const bool direct = inv_valid_ && red_pairs_ && S == 1 &&
+                      (cfg_.model.kind == kLR || fm_vals_) &&
                       (double)scratch_.cap * S * ps < 4294967295.0;
   // the direct path's send buffer is zeroed by the scatter
-  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, ps, direct ? grads_out : nullptr);
+  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, vstride_,
+                    direct ? grads_out : nullptr, grad_width());
   if (masks) be_->slice_masks(b, pos_, tmask_);
   FwdArgs fa;
   fa.batch = b;
@@ -647,6 +694,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
   fa.fm_compact = sharded_fm_compact() && fa.agg_ok;
+  fa.fm_vals = fm_vals_;
   if (sharded_fm_compact() && !fa.fm_compact)
     throw std::logic_error("w_forward_backward: compact FM rows need the reduction path");
   if (direct) {
@@ -714,13 +762,16 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
     aa.n_host = n;
     aa.n_max = n;
     aa.grads = const_cast<float*>(recv_grads);
-    if (aa.fm_compact) aa.pulled = srv_vals_[buf];
+    if (aa.fm_compact) aa.pulled = pulled_weights(buf, 0);
     aa.masks = recv_masks;
     if (stash) aa.nz_stash = srv_nz_[buf];
     aa.grp = g;
     be_->table_apply(aa);
     return;
   }
+  size_t first_src = 0;
+  while (first_src + 1 < src_offsets.size() && src_offsets[first_src + 1] <= src_offsets[first_src])
+    ++first_src;
   for (size_t src = 0; src + 1 < src_offsets.size(); ++src) {
     int64_t off = src_offsets[src];
     int64_t cnt = src_offsets[src + 1] - off;
@@ -732,12 +783,28 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
     aa.n_host = cnt;
     aa.n_max = cnt;
     aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * gw;
-    if (aa.fm_compact) aa.pulled = srv_vals_[buf] + off * (int64_t)ps;
+    if (aa.fm_compact) {
+      aa.pulled = pulled_weights(buf, off);
+      // compact value rows carry no per-parameter weights: a later source
+      // would expand its (B, C) with weights the earlier sources updated
+      if (!aa.pulled && src > first_src)
+        throw std::logic_error("s_apply: compact FM rows of several sources need the grouped "
+                               "apply or s_pull(keep_weights)");
+    }
     aa.masks = recv_masks ? recv_masks + off : nullptr;
     if (stash) aa.nz_stash = srv_nz_[buf] + 2 * off;
     stash = false;
     be_->table_apply(aa);
   }
+}
+
+// Per-parameter pre-step weights of buffer entries from `off` for the compact
+// FM apply: full pulled rows, or the owner's kept weights, or none (the apply
+// then takes the slot's current weights -- valid while no other update ran).
+const float* Engine::pulled_weights(int buf, int64_t off) const {
+  if (!fm_vals_) return srv_vals_[buf] + off * (int64_t)pstride();
+  if (srv_w_valid_[buf]) return srv_w_[buf] + off * (int64_t)pstride();
+  return nullptr;
 }
 
 // The dedup scratch is epoch-stamped and persistent: nothing to release.

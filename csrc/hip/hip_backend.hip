@@ -87,8 +87,8 @@ class HipBackend final : public Backend {
   void owner_group(const OwnerGroupArgs& a) override { hip::launch_owner_group(a, stream_); }
   void gather_grads(const GatherGradArgs& a) override { hip::launch_gather_grads(a, stream_); }
   void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
-                    int64_t n_max, int width, float* zero_out) override {
-    hip::launch_scatter_rows(src, dst, map, n_dev, n_max, width, zero_out, stream_);
+                    int64_t n_max, int width, float* zero_out, int zero_width) override {
+    hip::launch_scatter_rows(src, dst, map, n_dev, n_max, width, zero_out, zero_width, stream_);
   }
   void gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                    int64_t n_max, int width, bool zero_src) override {

@@ -20,7 +20,8 @@ void launch_bucket(const BucketArgs& a, hipStream_t st);
 void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
                              const int64_t* n_uniq, int64_t* counts, hipStream_t st);
 void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
-                         int64_t n_max, int width, float* zero_out, hipStream_t st);
+                         int64_t n_max, int width, float* zero_out, int zero_width,
+                         hipStream_t st);
 void launch_gather_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                         int64_t n_max, int width, bool zero_src, hipStream_t st);
 void launch_gather_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,

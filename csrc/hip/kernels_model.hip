@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < C; ++j) {
           if (j >= maxlen) continue;
-          if constexpr (kRed) lagg.column(j, j < len, pv[j] * S + s, loss);
+          if constexpr (kRed) lagg.column(j, j < len && pv[j] != a.trash_pos, pv[j] * S + s, loss);
           else lr_column<LOG2>(agg, j, j < len, pv[j] * S + s, loss, a.grad);
         }
       }
@@ -375,8 +375,9 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
         for (int j = 0; j < len; ++j) atomicAdd(&a.grad[pos[rs.at(j)] * S + s], loss);
       } else {
         for (int j = 0; j < maxlen; ++j) {
-          const u32 dest = j < len ? pos[rs.at(j)] * S + s : 0u;
-          if constexpr (kRed) lagg.column(j, j < len, dest, loss);
+          const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
+          const u32 dest = pj * S + s;
+          if constexpr (kRed) lagg.column(j, pj != a.trash_pos, dest, loss);
           else lr_column<LOG2>(agg, j, j < len, dest, loss, a.grad);
         }
       }
@@ -685,7 +686,19 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
       const float C = (float)fx_to_double<kFx>(acc[2 * i + 1]);
       const u64 dest = d0 + i;
       if (f.compact) {  // expanded by the apply (k_apply_group)
-        *reinterpret_cast<float2*>(f.grad + dest * f.ps) = make_float2(B, C);
+        if (f.out) {    // one slice: unique (send) order
+          const u32 o = f.inv[dest];
+          if (o == 0xFFFFFFFFu) continue;
+          if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
+            const double rows = (double)f.rows[0];
+            reinterpret_cast<float2*>(f.out)[o] =
+                make_float2((float)((double)B / rows), (float)((double)C / rows));
+          } else {  // normalised by the apply (fused step)
+            reinterpret_cast<float2*>(f.out)[o] = make_float2(B, C);
+          }
+        } else {
+          *reinterpret_cast<float2*>(f.grad + dest * f.ps) = make_float2(B, C);
+        }
         continue;
       }
       // rows are padded to 16 B: dwordx4 loads of v and stores of the row
@@ -713,8 +726,10 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
   hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
                      rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
-  RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim,
-             NV == 1 ? a.red_out : nullptr, a.red_inv, a.red_rows, NV == 2 && a.fm_compact};
+  if (a.red_out && (a.S != 1 || (NV == 2 && !a.fm_compact)))
+    throw std::runtime_error("red_out: one slice (and compact rows for FM) only");
+  RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim, a.red_out, a.red_inv,
+             a.red_rows, NV == 2 && a.fm_compact};
   hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, f);
 }
@@ -797,13 +812,100 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   const u32 S = (u32)a.S;
   const float lv = loss * vsum;
   for (int j = 0; j < maxlen; ++j) {
-    const u32 dest = j < len ? pos[rs.at(j)] * S + s : 0u;
-    lagg.column(j, j < len, dest, loss, lv);
+    const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
+    lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
   }
   __syncthreads();
   if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
   for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
     a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
+  flush_stats<BLOCK>(st, a.stats);
+}
+
+// Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
+// pulled row is (w, Σ_k v_k, Σ_k v_k^2, 0), one dwordx4 -- the reference's
+// y = Σ w + (Σ_f Σ_k v)^2 - Σ_f Σ_k v^2 (fm_worker.cc:159-202) needs nothing
+// else, and its backward only Σ loss and Σ loss*vsum per key (k_fm_red).
+// A third of the gather traffic of the full-row kernel, independent of D.
+template <int BLOCK, bool kGrad>
+__global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
+  constexpr int LOG2 = ilog2c(2 * BLOCK);
+  __shared__ u64 s_tag64[kGrad ? 2 : 1][kGrad ? (1 << LOG2) : 1];
+  __shared__ long long s_acc[kGrad ? 2 : 1][kGrad ? (1 << LOG2) * 2 : 1];
+  __shared__ unsigned short s_list[kGrad ? 2 : 1][kGrad ? BLOCK : 1];
+  __shared__ u32 s_hist[kGrad ? kRedMaxBuckets : 1];
+  __shared__ u32 s_nlist[3];
+  __shared__ int s_wmax[BLOCK / kWave];
+  const BatchView& b = a.batch;
+  const u32* __restrict__ pos = a.pos;
+  const float4* __restrict__ wp4 = reinterpret_cast<const float4*>(a.wpull);
+  const int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool active = r < b.rows;
+  RowSpan rs;
+  if (active) rs = row_span(b, r);
+  const int len = rs.len;
+  const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
+  ListAgg<LOG2, 2> lagg{reinterpret_cast<u64(*)[1 << LOG2]>(&s_tag64[0][0]),
+                        reinterpret_cast<long long(*)[(1 << LOG2) * 2]>(&s_acc[0][0]),
+                        reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
+                        s_nlist, s_hist, nullptr, 0u};
+  int maxlen = 0;
+  if constexpr (kGrad) {
+    lagg.region = reinterpret_cast<u64*>(reinterpret_cast<uint4*>(a.red_pairs) +
+                                         (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row));
+    lagg.init(a.red_nb);
+    if (!b.row_ptr) {
+      maxlen = b.nnz_per_row;
+      __syncthreads();
+    } else {
+      const int m = wave_max(len);
+      if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
+    }
+  }
+  StatAcc st;
+  float loss = 0.0f, vsum = 0.0f;
+  if (active) {
+    float wx = 0.0f, vp = 0.0f;
+    int j = 0;
+    for (; j + 4 <= len; j += 4) {  // four independent row loads in flight
+      float4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = wp4[pos[rs.at(j + u)]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        wx += q[u].x;
+        vsum += q[u].y;
+        vp += q[u].z;
+      }
+    }
+    for (; j < len; ++j) {
+      const float4 q = wp4[pos[rs.at(j)]];
+      wx += q.x;
+      vsum += q.y;
+      vp += q.z;
+    }
+    const float p = sigmoid_ref(wx + (vsum * vsum - vp));
+    const float lab = b.labels[r];
+    loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+  }
+  if constexpr (kGrad) {
+    const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+    const u32 S = (u32)a.S;
+    const float lv = loss * vsum;
+    for (int j = 0; j < maxlen; ++j) {
+      const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
+      lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
+    for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+      a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
+  }
   flush_stats<BLOCK>(st, a.stats);
 }
 
@@ -813,6 +915,19 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool red = agg && a.model.fm_math == kFmReference && a.red_pairs && a.red_nb > 0 &&
                    a.red_nb <= kRedMaxBuckets;
   if (a.fm_compact && !red) throw std::runtime_error("fm_compact needs the FM reduction path");
+  if (a.fm_vals) {
+    if (a.model.fm_math != kFmReference) throw std::runtime_error("fm_vals: reference math only");
+    constexpr int R = kFmGroupRows;
+    const int gr = (int)((a.batch.rows + R - 1) / R);
+    if (kGrad) {
+      if (!red || !a.fm_compact) throw std::runtime_error("fm_vals: needs the compact reduction");
+      hipLaunchKernelGGL((k_fm_vals<R, true>), dim3(gr), dim3(R), 0, st, a);
+      launch_reduction<2>(a, gr, R, st);
+    } else {
+      hipLaunchKernelGGL((k_fm_vals<R, false>), dim3(gr), dim3(R), 0, st, a);
+    }
+    return;
+  }
   switch (a.model.v_dim) {
 #define XF_FM_CASE(DD)                                                                   \
   case DD: {                                                                             \
@@ -1029,8 +1144,9 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
       u64* region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
       const int lane = lane_id();
       for (int j = 0; j < maxlen; ++j) {
-        const bool has = emit && j < len;
-        const u32 dest = has ? pos[rs.at(j)] * S + s : 0u;
+        const u32 pj = emit && j < len ? pos[rs.at(j)] : a.trash_pos;
+        const bool has = pj != a.trash_pos;
+        const u32 dest = has ? pj * S + s : 0u;
         const unsigned long long bm = __ballot(has);
         if (bm) {
           const int leader = __ffsll((long long)bm) - 1;

@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
     if (out_slot) out_slot[i] = slot;
     if (out_vals) out_vals[out_map ? out_map[i] : i] = w;
     if (out_nz) out_nz[i] = nz;
-    if (zero_out) zero_out[i] = 0.0f;
+    if (zero_out) zero_out[i] = 0.0f;  // (width 1: LR)
   }
   block_count_add<kBlock>(t.size, claims);
 }
@@ -609,26 +609,75 @@ __global__ void __launch_bounds__(kBlock) k_pull_probe(TableView t, const u64* _
   block_count_add<kBlock>(t.size, claims);
 }
 
+// Keys per lane group in flight in the lane-group pull/apply: each key is a
+// dependent chain (slot index -> slot state), and with G lanes per key a wave
+// holds only 64/G keys, so the group issues the chains of kGroupKeys keys
+// before resolving any (k_pull_values<16> for FM-8: 130 us -> see profiles).
+constexpr int kGroupKeys = 4;
+
 template <int G>
 __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
+  constexpr int U = kGroupKeys;
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
+  const bool ftrl = L.opt == kFTRL;
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
   const int p = threadIdx.x % G;
-  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; i < n; i += stride) {
-    const u32 slot = a.out_slot[i];
-    float* dst = a.out_vals + (size_t)(a.out_map ? a.out_map[i] : i) * a.pstride;
-    if (p >= a.pstride) continue;
-    float v = 0.0f;
-    if (p < L.P) {
-      if (slot == kNoSlot) {
-        v = absent_weight(sanitize_key(a.keys[i]), p, L, a.opt);
+  const int64_t first = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
+  // (group-uniform trip counts: every lane of a key's group reaches the shuffles)
+  for (int64_t i0 = first; i0 < n; i0 += stride * U) {
+    u32 slot[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * stride;
+      slot[u] = i < n ? a.out_slot[i] : kNoSlot;
+    }
+    u64 key[U];
+    u32 flag[U];
+    float s0[U], s1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      key[u] = 0ull;
+      flag[u] = 1u;
+      s0[u] = s1[u] = 0.0f;
+      if (slot[u] == kNoSlot || p >= L.P) continue;
+      const u32* sp = a.table.words + (u64)slot[u] * L.stride;
+      key[u] = *reinterpret_cast<const u64*>(sp);
+      if (L.has_flag) flag[u] = sp[L.flag_word];
+      if (ftrl) {
+        const float2 nz = *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
+        s0[u] = nz.x;
+        s1[u] = nz.y;
       } else {
-        const u32* sp = a.table.words + (u64)slot * L.stride;
-        v = slot_weight(sp, *reinterpret_cast<const u64*>(sp), p, L, a.opt);
+        s0[u] = __uint_as_float(sp[2 + p]);
       }
     }
-    dst[p] = v;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * stride;
+      if (i >= n) break;
+      float v = 0.0f;
+      if (p < L.P)
+        v = slot[u] == kNoSlot ? absent_weight(sanitize_key(a.keys[i]), p, L, a.opt)
+                               : state_weight(key[u], flag[u] != 0u, s0[u], s1[u], p, L, a.opt);
+      if (a.out_w && p < a.pstride) a.out_w[(size_t)i * a.pstride + p] = v;
+      if (a.zero_out && p < a.zero_width) a.zero_out[(size_t)i * a.zero_width + p] = 0.0f;
+      if (!a.out_vals) continue;
+      const size_t row = a.out_map ? a.out_map[i] : (size_t)i;
+      if (a.fm_vals) {
+        // (w, Σ_k v_k, Σ_k v_k^2) of the key: fixed shuffle tree over the group
+        float sv = (p >= L.p_w && p < L.P) ? v : 0.0f, qv = sv * sv;
+#pragma unroll
+        for (int o = G / 2; o > 0; o >>= 1) {
+          sv += __shfl_xor(sv, o);
+          qv += __shfl_xor(qv, o);
+        }
+        if (p == 0)
+          reinterpret_cast<float4*>(a.out_vals)[row] = make_float4(v, sv, qv, 0.0f);
+      } else if (p < a.pstride) {
+        a.out_vals[row * a.pstride + p] = v;
+      }
+    }
   }
 }
 
@@ -648,17 +697,20 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
   const TableLayout& L = a.table.L;
   int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
   if (L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag) {
+    if (a.zero_out && a.zero_width != 1) throw std::runtime_error("table_pull: zero_width");
     int64_t nm = a.n_dev ? a.n_max : a.n_host;
     int g = (int)((nm + kPullChunk - 1) / kPullChunk);
     hipLaunchKernelGGL(k_pull_lr16, dim3(g > 0 ? g : 1), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map,
                        reinterpret_cast<float2*>(a.out_nz), a.zero_out);
   } else if (a.out_slot && a.pstride >= 2 && a.pstride <= 64) {
+    if (a.fm_vals && group_for(a.pstride) < 2) throw std::runtime_error("fm_vals: bad layout");
     int64_t nm = a.n_dev ? a.n_max : a.n_host;
     int g1 = (int)((nm + kPullChunk - 1) / kPullChunk);
     hipLaunchKernelGGL(k_pull_probe, dim3(g1 > 0 ? g1 : 1), dim3(kBlock), 0, st, a.table, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot);
-    if (a.out_vals) {
+    if (a.zero_width > group_for(a.pstride)) throw std::runtime_error("table_pull: zero_width");
+    if (a.out_vals || a.out_w || a.zero_out) {
       const int G = group_for(a.pstride);
       // one key per lane group where possible: the grid-stride iterations of
       // a group are dependent random-access chains (latency bound)
@@ -673,6 +725,7 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
       }
     }
   } else {
+    if (a.fm_vals || a.out_w) throw std::runtime_error("table_pull: fm_vals/out_w need the group path");
     hipLaunchKernelGGL(k_pull_generic, dim3(grid), dim3(kBlock), 0, st, a);
   }
   XF_HIP_CHECK(hipGetLastError());
@@ -845,9 +898,11 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
 // contiguous slots instead of 64 scattered ones.  Every lane reads the
 // "pushed" flag before lane 0 of the group writes it (same wave, program
 // order); latent params use their lazy init value until the key's first push.
-// With a.grp (several sources) the group of a key's leader entry applies the
-// (source, slice) contributions in that order; other entries skip.
-template <int G>
+// U keys per group are in flight: their slot states are loaded before any is
+// updated (the chains are independent: one key per slot per launch).
+// With a.grp (several sources, U = 1) the group of a key's leader entry
+// applies the (source, slice) contributions in that order; other entries skip.
+template <int G, int U>
 __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   static_assert(G <= kWave, "a key's lanes must share a wave");
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
@@ -856,91 +911,116 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
   const int p = threadIdx.x % G;
   const bool multi = a.grp.oidx != nullptr;
+  const bool ftrl = L.opt == kFTRL;
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
-  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; i < n; i += stride) {
-    const u64* grow = nullptr;
-    int src0 = 0, nsrc = 1;
-    if (multi) {
-      if (!group_leader(a.grp, i, grow, src0)) continue;  // uniform over the key's lanes
-      nsrc = a.grp.nsrc;
+  const int64_t first = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
+  for (int64_t i0 = first; i0 < n; i0 += stride * U) {
+    u32 slot[U];
+    const u64* grow[U];
+    int src0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * stride;
+      slot[u] = kNoSlot;
+      grow[u] = nullptr;
+      src0[u] = 0;
+      if (i >= n) continue;
+      if (multi && !group_leader(a.grp, i, grow[u], src0[u])) continue;  // uniform per key
+      slot[u] = a.slots[i];
+      XF_DASSERT(slot[u] == kNoSlot || slot[u] < a.table.cap);
     }
-    const u32 slot = a.slots[i];
-    XF_DASSERT(slot == kNoSlot || slot < a.table.cap);
-    if (slot != kNoSlot && p < L.P) {
-      u32* sp = a.table.words + (u64)slot * L.stride;
-      const u64 key = *reinterpret_cast<const u64*>(sp);
-      bool pushed = !L.has_flag || sp[L.flag_word] != 0u;
-      float* st = reinterpret_cast<float*>(sp + 2);
-      const bool latent = p >= L.p_w;
-      const bool ftrl = L.opt == kFTRL;
-      float n0 = 0.0f, z0 = 0.0f, w0 = 0.0f;
+    u64 key[U];
+    bool pushed[U];
+    float n0[U], z0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      key[u] = 0ull;
+      pushed[u] = true;
+      n0[u] = z0[u] = 0.0f;
+      if (slot[u] == kNoSlot || p >= L.P) continue;
+      const u32* sp = a.table.words + (u64)slot[u] * L.stride;
+      key[u] = *reinterpret_cast<const u64*>(sp);
+      pushed[u] = !L.has_flag || sp[L.flag_word] != 0u;
       if (ftrl) {
-        float2 nz = (a.nz_stash && L.P == 1) ? reinterpret_cast<const float2*>(a.nz_stash)[i]
-                                             : *reinterpret_cast<float2*>(st + 2 * p);
-        n0 = nz.x;
-        z0 = nz.y;
+        const float2 nz = (a.nz_stash && L.P == 1)
+                              ? reinterpret_cast<const float2*>(a.nz_stash)[i0 + (int64_t)u * stride]
+                              : *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
+        n0[u] = nz.x;
+        z0[u] = nz.y;
       } else {
-        w0 = st[p];
+        n0[u] = __uint_as_float(sp[2 + p]);  // (SGD: w)
       }
-      auto weight = [&]() -> float {
-        if (latent && !pushed)
-          return ftrl ? normal_init(key, (u32)(p - L.p_w), a.opt.seed) * a.opt.v_init_scale
-                      : a.opt.sgd.v_init;
-        return ftrl ? ftrl_weight(z0, n0, a.opt.ftrl) : w0;
-      };
-      auto push = [&](float gv) {
-        float w = weight();
-        if (ftrl) ftrl_push(n0, z0, w, gv, a.opt.ftrl);
-        else w0 = w - a.opt.sgd.lr * gv;
-        pushed = true;
-      };
-      // compact reference-math FM rows (B, C): expand with the pre-step
-      // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
-      const float w_pre =
-          a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : weight()) : 0.0f;
-      u32 any = 0;
-      for (int sc = src0; sc < nsrc; ++sc) {
-        u32 e = (u32)i;
-        if (multi) {
-          const u64 v = grow[sc];
-          if ((u32)(v >> 32) != a.grp.epoch) continue;
-          e = (u32)v;
-        }
-        const u32 row = a.grad_map ? a.grad_map[e] : e;
-        const float* g = a.grads + (size_t)row * S * gs;
-        const u32 m = a.masks ? a.masks[row] : all;
-        any |= m;
-        auto raw_of = [&](int s) -> float {
-          if (!a.fm_compact) return g[s * gs + p];
-          const float Bv = g[s * gs], Cv = g[s * gs + 1];
-          return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
-        };
-        if (a.sum_slices) {
-          float acc = 0.0f;
-          for (int s = 0; s < S; ++s)
-            if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
-          if (m) push(acc);
-        } else {
-          for (int s = 0; s < S; ++s)
-            if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
-        }
-      }
-      if (ftrl) *reinterpret_cast<float2*>(st + 2 * p) = make_float2(n0, z0);
-      else st[p] = w0;
-      if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
     }
-    if (!multi && a.zero_after && p < (a.fm_compact ? 2 : ps)) {
-      const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
-      float* g = a.grads + (size_t)row * S * gs;
-      for (int s = 0; s < S; ++s) g[s * gs + p] = 0.0f;
-      if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * stride;
+      if (i >= n) break;
+      if (slot[u] != kNoSlot && p < L.P) {
+        u32* sp = a.table.words + (u64)slot[u] * L.stride;
+        float nn = n0[u], zz = z0[u];
+        bool pu = pushed[u];
+        auto weight = [&]() -> float {
+          return ftrl ? state_weight(key[u], pu, nn, zz, p, L, a.opt)
+                      : state_weight(key[u], pu, nn, 0.0f, p, L, a.opt);
+        };
+        auto push = [&](float gv) {
+          const float w = weight();
+          if (ftrl) ftrl_push(nn, zz, w, gv, a.opt.ftrl);
+          else nn = w - a.opt.sgd.lr * gv;
+          pu = true;
+        };
+        // compact reference-math FM rows (B, C): expand with the pre-step
+        // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
+        const float w_pre =
+            a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : weight()) : 0.0f;
+        u32 any = 0;
+        const int nsrc = multi ? a.grp.nsrc : 1;
+        for (int sc = src0[u]; sc < nsrc; ++sc) {
+          u32 e = (u32)i;
+          if (multi) {
+            const u64 v = grow[u][sc];
+            if ((u32)(v >> 32) != a.grp.epoch) continue;
+            e = (u32)v;
+          }
+          const u32 row = a.grad_map ? a.grad_map[e] : e;
+          const float* g = a.grads + (size_t)row * S * gs;
+          const u32 m = a.masks ? a.masks[row] : all;
+          any |= m;
+          auto raw_of = [&](int s) -> float {
+            if (!a.fm_compact) return g[s * gs + p];
+            const float Bv = g[s * gs], Cv = g[s * gs + 1];
+            return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
+          };
+          if (a.sum_slices) {
+            float acc = 0.0f;
+            for (int s = 0; s < S; ++s)
+              if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
+            if (m) push(acc);
+          } else {
+            for (int s = 0; s < S; ++s)
+              if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
+          }
+        }
+        if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(nn, zz);
+        else sp[2 + p] = __float_as_uint(nn);
+        if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
+      }
+      if (!multi && a.zero_after && p < (a.fm_compact ? 2 : ps)) {
+        const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+        float* g = a.grads + (size_t)row * S * gs;
+        for (int s = 0; s < S; ++s) g[s * gs + p] = 0.0f;
+        if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
+      }
     }
   }
 }
 
 template <int G>
 static void launch_apply_group(const ApplyArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_apply_group<G>, dim3(grid), dim3(kBlock), 0, st, a);
+  if (a.grp.oidx)
+    hipLaunchKernelGGL((k_apply_group<G, 1>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_apply_group<G, kGroupKeys>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
 void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
@@ -1105,7 +1185,7 @@ void launch_bucket(const BucketArgs& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 __global__ void k_scatter_rows(const float* __restrict__ src, float* __restrict__ dst,
                                const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
-                               int width, float* __restrict__ zero_out) {
+                               int width, float* __restrict__ zero_out, int zero_width) {
   const int64_t rows = dev_count(n_dev, n_max, n_max), n = rows * width;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
@@ -1115,7 +1195,8 @@ __global__ void k_scatter_rows(const float* __restrict__ src, float* __restrict_
     dst[r * width + c] = src[e];
   }
   if (zero_out)  // the send buffer the reduction fills next (saves a memset launch)
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows; i += stride)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * zero_width;
+         i += stride)
       zero_out[i] = 0.0f;
 }
 
@@ -1153,10 +1234,11 @@ __global__ void k_scatter_u32(const u32* __restrict__ src, u32* __restrict__ dst
 }
 
 void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
-                         int64_t n_max, int width, float* zero_out, hipStream_t st) {
+                         int64_t n_max, int width, float* zero_out, int zero_width,
+                         hipStream_t st) {
   if (n_max <= 0) return;
   hipLaunchKernelGGL(k_scatter_rows, dim3(grid_for(n_max * width)), dim3(kBlock), 0, st, src, dst,
-                     map, n_dev, n_max, width, zero_out);
+                     map, n_dev, n_max, width, zero_out, zero_width);
   XF_HIP_CHECK(hipGetLastError());
 }
 

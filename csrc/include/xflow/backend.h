@@ -78,7 +78,15 @@ struct DedupOut {
 struct FwdArgs {
   BatchView batch;
   const u32* pos = nullptr;        // [nnz]
-  const float* wpull = nullptr;    // [scratch_cap][pstride]
+  // dedup slot of overflowed occurrences (the scratch's trash slot, == cap):
+  // read as zero weights, never reduced (none: ~0)
+  u32 trash_pos = 0xFFFFFFFFu;
+  const float* wpull = nullptr;    // [scratch_cap][pstride] (fm_vals: [scratch_cap][4])
+  // Reference-math FM on compact value rows: the pull emits (w, Σ_k v_k,
+  // Σ_k v_k^2, 0) per key -- all the reference forward and its (B, C)
+  // backward need (fm_worker.cc:159-202) -- so a row gathers 16 B per
+  // feature instead of the whole (1+D)-float row (PullArgs::fm_vals).
+  bool fm_vals = false;
   float* grad = nullptr;           // [scratch_cap][S][pstride] (null: forward only)
   u32* tmask = nullptr;            // [scratch_cap] slice-touch bits (null unless S>1)
   float* pctr = nullptr;           // [rows] optional
@@ -95,9 +103,12 @@ struct FwdArgs {
   u32* red_tot = nullptr;          // [red_nb + 1] pairs per bucket, then bucket starts
   u32* red_count = nullptr;        // [workgroups] pairs per workgroup
   int red_nb = 0;                  // buckets = ceil(grad dests / 2^kRedShift)
-  // LR, one slice (multi-rank step): the bucket sums go straight to the send
-  // buffer, red_out[red_inv[dest]] = sum / red_rows[0], instead of grad (no
-  // separate gather).  red_out must be zeroed by the caller.
+  // One slice: the bucket sums go straight to a unique-order (= send order in
+  // the multi-rank step) buffer through the compaction's slot -> unique map,
+  // instead of the slot-indexed grad (no gather, a dense apply read):
+  // LR red_out[red_inv[dest]] = sum / red_rows[0]; compact FM
+  // red_out[2 red_inv[dest] + {0,1}] = (B, C) (normalised by the apply).
+  // red_out must be zeroed by the caller.
   float* red_out = nullptr;
   const u32* red_inv = nullptr;
   const int32_t* red_rows = nullptr;
@@ -134,7 +145,13 @@ struct PullArgs {
   // in unique order (read back by the apply instead of the table), and a
   // unique-order gradient buffer to zero for the reduction's direct writes.
   float* out_nz = nullptr;         // [n][2]
-  float* zero_out = nullptr;       // [n]
+  float* zero_out = nullptr;       // [n][zero_width]
+  int zero_width = 1;
+  // reference-math FM: out_vals rows are (w, Σ v, Σ v^2, 0) (FwdArgs::fm_vals)
+  bool fm_vals = false;
+  // optional per-parameter pulled weights [n][pstride] in entry order (the
+  // owner keeps them for an apply that runs after other table updates)
+  float* out_w = nullptr;
 };
 
 // Owner-side grouping of the keys a rank received from several sources in
@@ -144,7 +161,7 @@ struct PullArgs {
 // leader and pushes every source's contributions in source order -- one
 // launch per step instead of one per source, and the key's state is read and
 // written once (from the pull's stash when nothing touched the table since).
-constexpr int kMaxGroupSources = 16;
+constexpr int kMaxGroupSources = 64;
 struct SrcGroups {
   const u32* opos = nullptr;   // [n] owner-scratch slot of each received entry
   const u64* oidx = nullptr;   // [ocap][nsrc]: (epoch << 32) | entry, per (slot, source)
@@ -296,10 +313,10 @@ class Backend {
   }
   virtual void gather_grads(const GatherGradArgs& a) = 0;
   // rows of `width` floats: dst[map? map[i] : i] = src[i]   (scatter)
-  // (zero_out: also zero zero_out[0..n), the direct send buffer)
+  // (zero_out: also zero zero_out[0..n*zero_width), the direct send buffer)
   virtual void scatter_rows(const float* src, float* dst, const u32* map,
                             const int64_t* n_dev, int64_t n_max, int width,
-                            float* zero_out = nullptr) = 0;
+                            float* zero_out = nullptr, int zero_width = 1) = 0;
   // dst[i] = src[map[i]]; optionally zero the source row   (gather)
   virtual void gather_rows(const float* src, float* dst, const u32* map,
                            const int64_t* n_dev, int64_t n_max, int width,

@@ -75,8 +75,11 @@ class Engine {
   // src_offsets (world+1 entries, optional): the sources' ranges of the
   // received keys; with several sources the GPU backend groups the entries by
   // key here so that s_apply is one launch.
+  // keep_weights: also keep the per-parameter pulled weights for the apply
+  // (needed when other updates reach the table between this pull and its
+  // apply, i.e. the staleness-1 step, with compact FM value rows)
   void s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert = true, int buf = 0,
-              const std::vector<int64_t>& src_offsets = {});
+              const std::vector<int64_t>& src_offsets = {}, bool keep_weights = false);
   // worker: forward only from pulled rows (sharded evaluation); pctr may be null.
   void w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr, int wb = 0);
   // worker: place pulled rows (in send order) into the pos-indexed buffer,
@@ -103,6 +106,10 @@ class Engine {
   // exactly non-zero (key, param) weights of this table shard (L1 sparsity)
   int64_t nonzero_weights() { return be_->table_nonzero(table_, cfg_.opt); }
   int pstride() const { return cfg_.model.pstride(); }
+  // floats per pulled value row (pull outputs, the values exchange, the
+  // forward's gather): pstride, or 4 for reference-math FM on the GPU
+  // reduction path ((w, Σv, Σv^2, 0), FwdArgs::fm_vals)
+  int value_width() const { return vstride_; }
   // floats per (key, slice) in the multi-rank gradient exchange: pstride, or
   // 2 for reference-math FM on the GPU reduction path ((B, C) rows, expanded
   // by the owner with the values it served)
@@ -163,6 +170,12 @@ class Engine {
            (double)scratch_.cap * cfg_.max_slices * pstride() < 4294967295.0;
   }
   const float* srv_vals_[2] = {nullptr, nullptr};  // s_pull outputs (fm_compact apply)
+  float* srv_w_[2] = {nullptr, nullptr};           // s_pull(keep_weights) per-param weights
+  int64_t srv_w_cap_[2] = {0, 0};
+  bool srv_w_valid_[2] = {false, false};
+  bool fm_vals_ = false;
+  int vstride_ = 1;
+  const float* pulled_weights(int buf, int64_t off) const;
 
   EngineConfig cfg_;
   std::unique_ptr<Backend> be_;
@@ -190,6 +203,7 @@ class Engine {
   float* red_rowv_ = nullptr;    // MVM: per-row loss*M (FwdArgs::red_rowv)
   float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz]
   float* lr_nz_ = nullptr;       // LR-FTRL fused step: pulled (n, z) [max_nnz][2]
+  float* fm_grad_ = nullptr;     // reference FM fused step: unique-order (B, C) [max_nnz][2]
   int red_nb_ = 0;
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare

@@ -76,17 +76,25 @@ struct TableLayout {
   }
 };
 
+// Weight of param p from already-loaded slot words: the pushed flag and the
+// param's state (FTRL: s0 = n, s1 = z; SGD: s0 = w).
+XF_HD float state_weight(u64 key, bool pushed, float s0, float s1, int p, const TableLayout& L,
+                         const OptSpec& o) {
+  if (p >= L.p_w && L.has_flag && !pushed) {
+    return L.opt == kFTRL ? normal_init(key, (u32)(p - L.p_w), o.seed) * o.v_init_scale
+                          : o.sgd.v_init;
+  }
+  if (L.opt == kFTRL) return ftrl_weight(s1, s0, o.ftrl);
+  return s0;
+}
+
 // Current weight of param p stored in `slot` (reference pull semantics).
 XF_HD float slot_weight(const u32* slot, u64 key, int p, const TableLayout& L,
                         const OptSpec& o) {
   const float* st = reinterpret_cast<const float*>(slot + 2);
-  bool latent = p >= L.p_w;
-  if (latent && L.has_flag && slot[L.flag_word] == 0u) {
-    return L.opt == kFTRL ? normal_init(key, (u32)(p - L.p_w), o.seed) * o.v_init_scale
-                          : o.sgd.v_init;
-  }
-  if (L.opt == kFTRL) return ftrl_weight(st[2 * p + 1], st[2 * p], o.ftrl);
-  return st[p];
+  const bool pushed = !L.has_flag || slot[L.flag_word] != 0u;
+  return L.opt == kFTRL ? state_weight(key, pushed, st[2 * p], st[2 * p + 1], p, L, o)
+                        : state_weight(key, pushed, st[p], 0.0f, p, L, o);
 }
 
 // Weight of a key that is not in the table (lookup-only pulls at eval time).

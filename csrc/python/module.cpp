@@ -192,6 +192,7 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_property_readonly("backend_name", [](Engine& e) { return e.backend().name(); })
       .def_property_readonly("pstride", &Engine::pstride)
       .def_property_readonly("grad_width", &Engine::grad_width)
+      .def_property_readonly("value_width", &Engine::value_width)
       .def_property_readonly("P", [](Engine& e) { return e.config().model.P(); })
       .def_property_readonly("state_words", &Engine::state_words)
       .def_property_readonly("table_capacity", &Engine::table_capacity)
@@ -232,11 +233,12 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("wb") = 0, py::call_guard<py::gil_scoped_release>())
       .def("s_pull",
            [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert, int buf,
-              std::vector<int64_t> offsets) {
-             e.s_pull(P<const u64>(keys), n, P<float>(out), insert, buf, offsets);
+              std::vector<int64_t> offsets, bool keep_weights) {
+             e.s_pull(P<const u64>(keys), n, P<float>(out), insert, buf, offsets, keep_weights);
            },
            py::arg("keys"), py::arg("n"), py::arg("out"), py::arg("insert") = true,
            py::arg("buf") = 0, py::arg("offsets") = std::vector<int64_t>(),
+           py::arg("keep_weights") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("w_forward",
            [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t pctr,

@@ -138,6 +138,12 @@ class Engine:
         return int(self._e.grad_width)
 
     @property
+    def value_width(self) -> int:
+        """Floats per pulled value row (pull outputs / values exchange): pstride,
+        or 4 for reference-math FM on the GPU ((w, sum v, sum v^2, 0))."""
+        return int(self._e.value_width)
+
+    @property
     def params_per_key(self) -> int:
         return int(self._e.P)
 
@@ -214,12 +220,15 @@ class Engine:
         self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr(), int(wb))
 
     def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor,
-               insert: bool = True, buf: int = 0, offsets=None) -> None:
-        """Owner pull of n received keys; ``offsets`` (world+1 source
-        boundaries) lets the GPU backend group the sources for a one-launch apply."""
+               insert: bool = True, buf: int = 0, offsets=None, keep_weights: bool = False) -> None:
+        """Owner pull of n received keys into out_vals ([n, value_width]);
+        ``offsets`` (world+1 source boundaries) lets the GPU backend group the
+        sources for a one-launch apply; ``keep_weights`` keeps the pulled
+        per-parameter weights for an apply after other updates (async step)."""
         self._sync_stream()
         self._e.s_pull(recv_keys.data_ptr(), int(n), out_vals.data_ptr(), insert, int(buf),
-                       [int(o) for o in offsets] if offsets is not None else [])
+                       [int(o) for o in offsets] if offsets is not None else [],
+                       bool(keep_weights))
 
     def w_forward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
                   pctr: torch.Tensor | None, wb: int = 0) -> None:

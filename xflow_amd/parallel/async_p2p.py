@@ -117,7 +117,7 @@ class AsyncShardedEngine(ShardedEngine):
                    next_batch: Optional[Batch] = None) -> None:
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
-        ps = e.pstride
+        ps = e.value_width  # floats per pulled value row
         W = S * e.grad_width
         ordered_masks = S > 1 and not e.cfg.sum_slices
         buf = self._parity
@@ -128,7 +128,8 @@ class AsyncShardedEngine(ShardedEngine):
         self._a2a(rk, self._send_keys[wb][:n_send], recv_splits, send_splits)
         offsets = self._offsets(recv_splits)
         vals = self._vals_out[buf].get(n_recv * ps).view(n_recv, ps)
-        e.s_pull(rk, n_recv, vals, insert=True, buf=buf, offsets=offsets)
+        # (applied after the next step's pull: keep the pulled weights)
+        e.s_pull(rk, n_recv, vals, insert=True, buf=buf, offsets=offsets, keep_weights=True)
         if prefetch is not None:
             prefetch()
         pulled = self._pulled.get(n_send * ps).view(n_send, ps)

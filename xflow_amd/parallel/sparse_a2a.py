@@ -288,7 +288,7 @@ class ShardedEngine:
         prepared.  Every rank must pass next_batch (or not) alike."""
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
-        ps = e.pstride
+        ps = e.value_width  # floats per pulled value row
         ordered_masks = S > 1 and not e.cfg.sum_slices
         wb, send_splits, recv_splits, prefetch = self._take(batch, prefetch)
         n_send, n_recv = self.last_send, self.last_recv
@@ -330,7 +330,7 @@ class ShardedEngine:
             pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
         wb, send_splits, recv_splits, _ = self._take(batch)
         recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
-        ps = e.pstride
+        ps = e.value_width  # floats per pulled value row
         vals = self._vals_out[0].get(self.last_recv * ps).view(self.last_recv, ps)
         e.s_pull(recv_keys, self.last_recv, vals, insert=False, buf=0)
         pulled = self._pulled.get(self.last_send * ps).view(self.last_send, ps)
