@@ -399,6 +399,29 @@ class CpuBackend final : public Backend {
       if (slot != kNoSlot && t.L.has_flag) t.words[(u64)slot * t.L.stride + t.L.flag_word] = 1u;
     }
   }
+  EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {
+    // same definition as the HIP kernels: stable order by pctr descending
+    EvalMetrics m;
+    m.n = n;
+    std::vector<int64_t> idx((size_t)n);
+    for (int64_t i = 0; i < n; ++i) idx[(size_t)i] = i;
+    std::stable_sort(idx.begin(), idx.end(),
+                     [&](int64_t a, int64_t b) { return pctr[a] > pctr[b]; });
+    uint64_t tp = 0;
+    for (int64_t i : idx) {
+      if (labels[i] > 0.5f) ++tp;
+      else m.area += tp;
+    }
+    m.tp = (int64_t)tp;
+    for (int64_t i = 0; i < n; ++i) {
+      const float p = pctr[i];
+      const int y = labels[i] > 0.5f ? 1 : 0;
+      m.log2_sum += (double)((float)y * std::log2(p)) + (1.0 - y) * std::log2(1.0 - (double)p);
+      const float pc = std::fmin(std::fmax(p, 1e-7f), 1.0f - 1e-7f);
+      m.ln_sum += y ? -std::log((double)pc) : -std::log(1.0 - (double)pc);
+    }
+    return m;
+  }
   int64_t table_nonzero(const TableView& t, const OptSpec& o) override {
     int64_t n = 0;
     for (u64 s = 0; s < t.cap; ++s) {

@@ -52,6 +52,29 @@ EvalResult reference_auc(std::vector<std::pair<int, float>>& v) {
   return r;
 }
 
+EvalResult eval_result(const EvalMetrics& m) {
+  EvalResult r;
+  r.n = m.n;
+  r.tp = m.tp;
+  float logloss = (float)m.log2_sum;
+  if (m.n > 0) logloss /= (float)m.n;  // (base.h:100: float /= size_t)
+  r.logloss_printed = logloss;
+  r.ln_logloss = m.n > 0 ? m.ln_sum / (double)m.n : 0.0;
+  std::ostringstream os;
+  os << "logloss: " << logloss << "\t";
+  if (m.tp == 0 || m.tp == m.n) {
+    os << "tp_n = " << m.tp;
+    r.auc = std::nan("");
+  } else {
+    float area = (float)m.area;
+    area /= 1.0 * ((uint64_t)m.tp * (uint64_t)(m.n - m.tp));
+    r.auc = area;
+    os << "auc = " << area << "\ttp = " << m.tp << " fp = " << m.n - m.tp;
+  }
+  r.line = os.str();
+  return r;
+}
+
 Trainer::Trainer(const TrainerConfig& cfg) : cfg_(cfg) {
   threads_ = cfg_.threads > 0 ? cfg_.threads : (int)std::thread::hardware_concurrency();
   if (threads_ < 1) threads_ = 1;

@@ -116,6 +116,11 @@ class HipBackend final : public Backend {
   void table_prefill(const TableView& t, int64_t n, u64 seed) override {
     hip::launch_table_prefill(t, n, seed, stream_);
   }
+  EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {
+    EvalMetrics m;
+    hip::launch_eval_metrics(pctr, labels, n, &m, stream_);
+    return m;
+  }
   int64_t table_nonzero(const TableView& t, const OptSpec& o) override {
     hip::launch_table_nonzero(t, o, counter_, stream_);
     unsigned long long n = 0;

@@ -42,6 +42,10 @@ void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long lo
 void launch_forward_backward(const FwdArgs& a, hipStream_t st);
 void launch_slice_masks(const BatchView& b, const u32* pos, u32* tmask, hipStream_t st);
 
+// kernels_eval.hip
+void launch_eval_metrics(const float* pctr, const float* labels, int64_t n, EvalMetrics* out,
+                         hipStream_t st);
+
 // kernels_synth.hip
 void launch_synth(const SynthArgs& a, hipStream_t st);
 

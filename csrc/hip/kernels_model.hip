@@ -909,12 +909,110 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
   flush_stats<BLOCK>(st, a.stats);
 }
 
+// ---------------------------------------------------------------------------
+// Standard-math FM forward on the matrix cores (v_mfma_f32_16x16x4_f32), the
+// row-indicator form of DESIGN.md section 6: a wave owns 16 rows; for every
+// (row quad m, field f) one MFMA adds, for the 4 rows of the quad, the
+// field's latent row v (columns 0..D-1) and its squares (columns D..2D-1) to
+// the 16 x 16 accumulator tile D[row][column]:
+//   A[i][q] = (i == 4m + q)       (one-hot: 4 of the 64 A entries are 1)
+//   B[q][c] = v[row 4m+q, f][c], v^2[..][c - D]
+// so D[i][k] = sum_f v_ik = vs_k and D[i][D+k] = sum_f v_ik^2, exact f32 adds
+// in field order (fmaf chain).  y = sum_f w + 0.5 sum_k (vs_k^2 - sum_f v^2)
+// (Rendle's sum trick; fm_math = standard).  An honest A/B against the VALU
+// forward (one lane per row) -- see profiles/r2_fm_mfma_ab.txt: 15/16 of each
+// MFMA's work multiplies by the zero entries of A, so the matrix-core form
+// needs 4*F instructions per 16 rows where the VALU form spends F*D FMAs per
+// row; both are bound by the gather of the pulled rows.
+// Selected for forward-only standard FM with ModelSpec::fm_mfma.
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+template <int D>
+__global__ void __launch_bounds__(256) k_fm_fwd_mfma(FwdArgs a) {
+  static_assert(2 * D <= 16, "one 16-column tile: D <= 8");
+  constexpr int PS = fm_ps(D);
+  const BatchView& b = a.batch;
+  const int lane = lane_id();
+  const int q = lane >> 4, c = lane & 15;
+  const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * 16;
+  int F = b.nnz_per_row;
+  if (b.row_ptr) {  // longest row of the wave's 16
+    int len = 0;
+    const int64_t r = r0 + (lane & 15);
+    if (lane < 16 && r < b.rows) len = (int)(b.row_ptr[r + 1] - b.row_ptr[r]);
+    F = wave_max(len);
+  }
+  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+  float wx[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // lanes with c == 0: w sums of rows 4m+q
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int64_t row = r0 + 4 * m + q;
+    RowSpan rs;
+    if (row < b.rows) rs = row_span(b, row);
+    const float av = (c == 4 * m + q) ? 1.0f : 0.0f;  // A[i = c][k = q]
+    for (int f = 0; f < F; ++f) {
+      float bv = 0.0f, w = 0.0f;
+      if (f < rs.len) {
+        const float* src = a.wpull + (size_t)a.pos[rs.at(f)] * PS;
+        w = src[0];
+        const float v = c < D ? src[1 + c] : (c < 2 * D ? src[1 + c - D] : 0.0f);
+        bv = c < D ? v : v * v;
+      }
+      wx[m] += w;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+  }
+  // D[row = 4*(lane>>4) + reg][col = lane & 15]: per row, sum over the 16 columns
+  float t[4];
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const float x = acc[reg];
+    t[reg] = c < D ? x * x : (c < 2 * D ? -x : 0.0f);
+  }
+  // (vs_k^2 terms first, then the squares: same association on every lane)
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) t[reg] += __shfl_xor(t[reg], o);
+  // lane 16*g + 0 holds rows 4g .. 4g+3; their w sums sit in lanes (q = reg, c = 0), index m = g
+  StatAcc st;
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) {
+    const int g = lane >> 4;
+    float wxs = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float x = __shfl(wx[m], 16 * reg);  // lane (q = reg, c = 0)
+      if (m == g) wxs = x;
+    }
+    const int64_t row = r0 + 4 * g + reg;
+    if (c == 0 && row < b.rows) {
+      const float p = sigmoid_ref(wxs + 0.5f * t[reg]);
+      const float lab = b.labels[row];
+      if (a.pctr) a.pctr[row] = p;
+      st.add(p, lab);
+    }
+  }
+  flush_stats<256>(st, a.stats);
+}
+
 template <bool kGrad>
 static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.model.fm_math == kFmReference && a.red_pairs && a.red_nb > 0 &&
                    a.red_nb <= kRedMaxBuckets;
   if (a.fm_compact && !red) throw std::runtime_error("fm_compact needs the FM reduction path");
+  if (!kGrad && a.model.fm_math == kFmStandard && a.model.fm_mfma) {
+    const int g = (int)((a.batch.rows + 63) / 64);  // 4 waves x 16 rows
+    switch (a.model.v_dim) {
+      case 1: hipLaunchKernelGGL(k_fm_fwd_mfma<1>, dim3(g), dim3(256), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(k_fm_fwd_mfma<2>, dim3(g), dim3(256), 0, st, a); break;
+      case 4: hipLaunchKernelGGL(k_fm_fwd_mfma<4>, dim3(g), dim3(256), 0, st, a); break;
+      case 8: hipLaunchKernelGGL(k_fm_fwd_mfma<8>, dim3(g), dim3(256), 0, st, a); break;
+      default: throw std::runtime_error("FM MFMA forward: v_dim 1, 2, 4 or 8");
+    }
+    return;
+  }
   if (a.fm_vals) {
     if (a.model.fm_math != kFmReference) throw std::runtime_error("fm_vals: reference math only");
     constexpr int R = kFmGroupRows;

@@ -609,88 +609,82 @@ __global__ void __launch_bounds__(kBlock) k_pull_probe(TableView t, const u64* _
   block_count_add<kBlock>(t.size, claims);
 }
 
-// Keys per lane group in flight in the lane-group pull/apply: each key is a
-// dependent chain (slot index -> slot state), and with G lanes per key a wave
-// holds only 64/G keys, so the group issues the chains of kGroupKeys keys
-// before resolving any (k_pull_values<16> for FM-8: 130 us -> see profiles).
-constexpr int kGroupKeys = 4;
+// Packed lane groups for the multi-parameter pull/apply: P lanes per key
+// (lane p owns parameter p), floor(64/P) keys per wave, never straddling a
+// wave.  These kernels are VALU-issue bound (FTRL closed form with IEEE
+// division/sqrt, lazy N(0,1) init): the cost is per wave instruction, so
+// packing 7 FM-8 keys (P = 9) into a wave instead of 4 in pow2 groups of 16
+// lanes is 1.75x fewer instructions per key.  PMC of the pow2-group apply
+// (FM-8): 1626 VALU instructions per wave for 16 keys, 50 % of wave cycles
+// waiting.
+struct PackedLane {
+  int P, K, g, p;        // lanes per key, keys per wave, key in wave, param
+  bool on;               // lane belongs to a key group (64 % P lanes idle)
+  int64_t first, stride;  // key index of this lane's group, grid stride in keys
+};
 
-template <int G>
+__device__ __forceinline__ PackedLane packed_lane(int P) {
+  PackedLane r;
+  r.P = P;
+  r.K = kWave / P;
+  const int lane = threadIdx.x % kWave;
+  r.g = lane / P;
+  r.p = lane - r.g * P;
+  r.on = r.g < r.K;
+  const int64_t waves = (int64_t)(blockDim.x / kWave);
+  r.first = ((int64_t)blockIdx.x * waves + threadIdx.x / kWave) * r.K + r.g;
+  r.stride = (int64_t)gridDim.x * waves * r.K;
+  return r;
+}
+
 __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
-  constexpr int U = kGroupKeys;
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
-  const bool ftrl = L.opt == kFTRL;
-  const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
-  const int p = threadIdx.x % G;
-  const int64_t first = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
-  // (group-uniform trip counts: every lane of a key's group reaches the shuffles)
-  for (int64_t i0 = first; i0 < n; i0 += stride * U) {
-    u32 slot[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * stride;
-      slot[u] = i < n ? a.out_slot[i] : kNoSlot;
+  const PackedLane pl = packed_lane(L.P);
+  const int p = pl.p;
+  const int gbase = (threadIdx.x % kWave) - p;  // lane of the group's param 0
+  // (a key group's lanes share i: the group-uniform loop keeps them together
+  // through the shuffles; idle lanes run no iteration)
+  for (int64_t i = pl.on ? pl.first : n; i < n; i += pl.stride) {
+    const u32 slot = a.out_slot[i];
+    float v;
+    if (slot == kNoSlot) {
+      v = absent_weight(sanitize_key(a.keys[i]), p, L, a.opt);
+    } else {
+      const u32* sp = a.table.words + (u64)slot * L.stride;
+      v = slot_weight(sp, *reinterpret_cast<const u64*>(sp), p, L, a.opt);
     }
-    u64 key[U];
-    u32 flag[U];
-    float s0[U], s1[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      key[u] = 0ull;
-      flag[u] = 1u;
-      s0[u] = s1[u] = 0.0f;
-      if (slot[u] == kNoSlot || p >= L.P) continue;
-      const u32* sp = a.table.words + (u64)slot[u] * L.stride;
-      key[u] = *reinterpret_cast<const u64*>(sp);
-      if (L.has_flag) flag[u] = sp[L.flag_word];
-      if (ftrl) {
-        const float2 nz = *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
-        s0[u] = nz.x;
-        s1[u] = nz.y;
-      } else {
-        s0[u] = __uint_as_float(sp[2 + p]);
-      }
+    if (a.out_w) {
+      a.out_w[(size_t)i * a.pstride + p] = v;
+      for (int c = L.P + p; c < a.pstride; c += L.P) a.out_w[(size_t)i * a.pstride + c] = 0.0f;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * stride;
-      if (i >= n) break;
-      float v = 0.0f;
-      if (p < L.P)
-        v = slot[u] == kNoSlot ? absent_weight(sanitize_key(a.keys[i]), p, L, a.opt)
-                               : state_weight(key[u], flag[u] != 0u, s0[u], s1[u], p, L, a.opt);
-      if (a.out_w && p < a.pstride) a.out_w[(size_t)i * a.pstride + p] = v;
-      if (a.zero_out && p < a.zero_width) a.zero_out[(size_t)i * a.zero_width + p] = 0.0f;
-      if (!a.out_vals) continue;
-      const size_t row = a.out_map ? a.out_map[i] : (size_t)i;
-      if (a.fm_vals) {
-        // (w, Σ_k v_k, Σ_k v_k^2) of the key: fixed shuffle tree over the group
-        float sv = (p >= L.p_w && p < L.P) ? v : 0.0f, qv = sv * sv;
-#pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) {
-          sv += __shfl_xor(sv, o);
-          qv += __shfl_xor(qv, o);
-        }
-        if (p == 0)
-          reinterpret_cast<float4*>(a.out_vals)[row] = make_float4(v, sv, qv, 0.0f);
-      } else if (p < a.pstride) {
-        a.out_vals[row * a.pstride + p] = v;
+    if (a.zero_out)
+      for (int c = p; c < a.zero_width; c += L.P) a.zero_out[(size_t)i * a.zero_width + c] = 0.0f;
+    if (!a.out_vals) continue;
+    const size_t row = a.out_map ? a.out_map[i] : (size_t)i;
+    if (a.fm_vals) {
+      // (w, Σ_k v_k, Σ_k v_k^2) of the key, summed in param order by lane 0
+      float sv = 0.0f, qv = 0.0f;
+      for (int j = L.p_w; j < L.P; ++j) {
+        const float x = __shfl(v, gbase + j);
+        sv += x;
+        qv += x * x;
       }
+      if (p == 0) reinterpret_cast<float4*>(a.out_vals)[row] = make_float4(v, sv, qv, 0.0f);
+    } else {
+      a.out_vals[row * a.pstride + p] = v;
+      for (int c = L.P + p; c < a.pstride; c += L.P) a.out_vals[row * a.pstride + c] = 0.0f;
     }
   }
 }
 
-template <int G>
-static void launch_pull_values(const PullArgs& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_pull_values<G>, dim3(grid), dim3(kBlock), 0, st, a);
+// grid for packed groups: one key per group up to the cap
+static int packed_grid(int64_t n, int P) {
+  const int64_t keys_per_block = (int64_t)(kBlock / kWave) * (kWave / P);
+  const int64_t g = (n + keys_per_block - 1) / keys_per_block;
+  return (int)(g < 1 ? 1 : (g < kGroupGridCap ? g : kGroupGridCap));
 }
 
-static int group_for(int width) {
-  int g = 1;
-  while (g < width) g <<= 1;
-  return g;
-}
 
 void launch_table_pull(const PullArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
@@ -703,26 +697,16 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_pull_lr16, dim3(g > 0 ? g : 1), dim3(kBlock), 0, st, a.table, a.opt.ftrl, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot, a.out_vals, a.out_map,
                        reinterpret_cast<float2*>(a.out_nz), a.zero_out);
-  } else if (a.out_slot && a.pstride >= 2 && a.pstride <= 64) {
-    if (a.fm_vals && group_for(a.pstride) < 2) throw std::runtime_error("fm_vals: bad layout");
-    int64_t nm = a.n_dev ? a.n_max : a.n_host;
-    int g1 = (int)((nm + kPullChunk - 1) / kPullChunk);
+  } else if (a.out_slot && a.pstride >= 2 && L.P <= kWave) {
+    if (a.fm_vals && L.P < 2) throw std::runtime_error("fm_vals: bad layout");
+    const int64_t nm = a.n_dev ? a.n_max : a.n_host;
+    const int g1 = (int)((nm + kPullChunk - 1) / kPullChunk);
     hipLaunchKernelGGL(k_pull_probe, dim3(g1 > 0 ? g1 : 1), dim3(kBlock), 0, st, a.table, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot);
-    if (a.zero_width > group_for(a.pstride)) throw std::runtime_error("table_pull: zero_width");
     if (a.out_vals || a.out_w || a.zero_out) {
-      const int G = group_for(a.pstride);
       // one key per lane group where possible: the grid-stride iterations of
       // a group are dependent random-access chains (latency bound)
-      const int g2 = grid_for(nm * G, kBlock, kGroupGridCap);
-      switch (G) {
-        case 2: launch_pull_values<2>(a, g2, st); break;
-        case 4: launch_pull_values<4>(a, g2, st); break;
-        case 8: launch_pull_values<8>(a, g2, st); break;
-        case 16: launch_pull_values<16>(a, g2, st); break;
-        case 32: launch_pull_values<32>(a, g2, st); break;
-        default: launch_pull_values<64>(a, g2, st); break;
-      }
+      hipLaunchKernelGGL(k_pull_values, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
     }
   } else {
     if (a.fm_vals || a.out_w) throw std::runtime_error("table_pull: fm_vals/out_w need the group path");
@@ -893,175 +877,114 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
   }
 }
 
-// Multi-parameter apply: a group of G lanes per key (G = pow2 >= pstride),
-// lane p owns parameter p's optimizer state, so a wave touches a few
+// Multi-parameter apply on packed lane groups (packed_lane: P lanes per key,
+// lane p owns parameter p's optimizer state), so a wave touches a few
 // contiguous slots instead of 64 scattered ones.  Every lane reads the
-// "pushed" flag before lane 0 of the group writes it (same wave, program
-// order); latent params use their lazy init value until the key's first push.
-// U keys per group are in flight: their slot states are loaded before any is
-// updated (the chains are independent: one key per slot per launch).
-// With a.grp (several sources, U = 1) the group of a key's leader entry
-// applies the (source, slice) contributions in that order; other entries skip.
-template <int G, int U>
+// "pushed" flag before lane 0 of the group writes it (one group never
+// straddles a wave: program order); latent params use their lazy init value
+// until the key's first push.  With a.grp (several sources) the group of a
+// key's leader entry applies the (source, slice) contributions in that
+// order; other entries skip.
 __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
-  static_assert(G <= kWave, "a key's lanes must share a wave");
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
   const int S = a.S, ps = a.pstride, gs = a.gstride ? a.gstride : ps;
   const u32 all = (S >= 32) ? 0xFFFFFFFFu : ((1u << S) - 1u);
-  const int p = threadIdx.x % G;
+  const PackedLane pl = packed_lane(L.P);
+  const int p = pl.p;
   const bool multi = a.grp.oidx != nullptr;
   const bool ftrl = L.opt == kFTRL;
-  const int64_t stride = (int64_t)gridDim.x * (blockDim.x / G);
-  const int64_t first = (int64_t)blockIdx.x * (blockDim.x / G) + threadIdx.x / G;
-  for (int64_t i0 = first; i0 < n; i0 += stride * U) {
-    u32 slot[U];
-    const u64* grow[U];
-    int src0[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * stride;
-      slot[u] = kNoSlot;
-      grow[u] = nullptr;
-      src0[u] = 0;
-      if (i >= n) continue;
-      if (multi && !group_leader(a.grp, i, grow[u], src0[u])) continue;  // uniform per key
-      slot[u] = a.slots[i];
-      XF_DASSERT(slot[u] == kNoSlot || slot[u] < a.table.cap);
+  for (int64_t i = pl.on ? pl.first : n; i < n; i += pl.stride) {
+    const u64* grow = nullptr;
+    int src0 = 0, nsrc = 1;
+    if (multi) {
+      if (!group_leader(a.grp, i, grow, src0)) continue;  // uniform over the key's lanes
+      nsrc = a.grp.nsrc;
     }
-    u64 key[U];
-    bool pushed[U];
-    float n0[U], z0[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      key[u] = 0ull;
-      pushed[u] = true;
-      n0[u] = z0[u] = 0.0f;
-      if (slot[u] == kNoSlot || p >= L.P) continue;
-      const u32* sp = a.table.words + (u64)slot[u] * L.stride;
-      key[u] = *reinterpret_cast<const u64*>(sp);
-      pushed[u] = !L.has_flag || sp[L.flag_word] != 0u;
+    const u32 slot = a.slots[i];
+    XF_DASSERT(slot == kNoSlot || slot < a.table.cap);
+    if (slot != kNoSlot) {
+      u32* sp = a.table.words + (u64)slot * L.stride;
+      const u64 key = *reinterpret_cast<const u64*>(sp);
+      bool pushed = !L.has_flag || sp[L.flag_word] != 0u;
+      float n0, z0 = 0.0f;
       if (ftrl) {
-        const float2 nz = (a.nz_stash && L.P == 1)
-                              ? reinterpret_cast<const float2*>(a.nz_stash)[i0 + (int64_t)u * stride]
-                              : *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
-        n0[u] = nz.x;
-        z0[u] = nz.y;
+        const float2 nz = (a.nz_stash && L.P == 1) ? reinterpret_cast<const float2*>(a.nz_stash)[i]
+                                                   : *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
+        n0 = nz.x;
+        z0 = nz.y;
       } else {
-        n0[u] = __uint_as_float(sp[2 + p]);  // (SGD: w)
+        n0 = __uint_as_float(sp[2 + p]);  // (SGD: w)
       }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * stride;
-      if (i >= n) break;
-      if (slot[u] != kNoSlot && p < L.P) {
-        u32* sp = a.table.words + (u64)slot[u] * L.stride;
-        float nn = n0[u], zz = z0[u];
-        bool pu = pushed[u];
-        auto weight = [&]() -> float {
-          return ftrl ? state_weight(key[u], pu, nn, zz, p, L, a.opt)
-                      : state_weight(key[u], pu, nn, 0.0f, p, L, a.opt);
-        };
-        auto push = [&](float gv) {
-          const float w = weight();
-          if (ftrl) ftrl_push(nn, zz, w, gv, a.opt.ftrl);
-          else nn = w - a.opt.sgd.lr * gv;
-          pu = true;
-        };
-        // compact reference-math FM rows (B, C): expand with the pre-step
-        // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
-        const float w_pre =
-            a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : weight()) : 0.0f;
-        u32 any = 0;
-        const int nsrc = multi ? a.grp.nsrc : 1;
-        for (int sc = src0[u]; sc < nsrc; ++sc) {
-          u32 e = (u32)i;
-          if (multi) {
-            const u64 v = grow[u][sc];
-            if ((u32)(v >> 32) != a.grp.epoch) continue;
-            e = (u32)v;
-          }
-          const u32 row = a.grad_map ? a.grad_map[e] : e;
-          const float* g = a.grads + (size_t)row * S * gs;
-          const u32 m = a.masks ? a.masks[row] : all;
-          any |= m;
-          auto raw_of = [&](int s) -> float {
-            if (!a.fm_compact) return g[s * gs + p];
-            const float Bv = g[s * gs], Cv = g[s * gs + 1];
-            return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
-          };
-          if (a.sum_slices) {
-            float acc = 0.0f;
-            for (int s = 0; s < S; ++s)
-              if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
-            if (m) push(acc);
-          } else {
-            for (int s = 0; s < S; ++s)
-              if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
-          }
+      // current weight; w_next caches it between pushes (the closed form is
+      // the bulk of this kernel's instructions)
+      float w_next = state_weight(key, pushed, n0, z0, p, L, a.opt);
+      auto push = [&](float gv) {
+        if (ftrl) ftrl_push(n0, z0, w_next, gv, a.opt.ftrl);
+        else n0 = w_next - a.opt.sgd.lr * gv;
+        pushed = true;
+        w_next = state_weight(key, true, n0, z0, p, L, a.opt);
+      };
+      // compact reference-math FM rows (B, C): expand with the pre-step
+      // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
+      const float w_pre = a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : w_next) : 0.0f;
+      u32 any = 0;
+      for (int sc = src0; sc < nsrc; ++sc) {
+        u32 e = (u32)i;
+        if (multi) {
+          const u64 v = grow[sc];
+          if ((u32)(v >> 32) != a.grp.epoch) continue;
+          e = (u32)v;
         }
-        if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(nn, zz);
-        else sp[2 + p] = __float_as_uint(nn);
-        if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
+        const u32 row = a.grad_map ? a.grad_map[e] : e;
+        const float* g = a.grads + (size_t)row * S * gs;
+        const u32 m = a.masks ? a.masks[row] : all;
+        any |= m;
+        auto raw_of = [&](int s) -> float {
+          if (!a.fm_compact) return g[s * gs + p];
+          const float Bv = g[s * gs], Cv = g[s * gs + 1];
+          return p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
+        };
+        if (a.sum_slices) {
+          float acc = 0.0f;
+          for (int s = 0; s < S; ++s)
+            if (m & (1u << s)) acc += norm_grad(raw_of(s), a.slice_rows, s);
+          if (m) push(acc);
+        } else {
+          for (int s = 0; s < S; ++s)
+            if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
+        }
       }
-      if (!multi && a.zero_after && p < (a.fm_compact ? 2 : ps)) {
-        const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
-        float* g = a.grads + (size_t)row * S * gs;
-        for (int s = 0; s < S; ++s) g[s * gs + p] = 0.0f;
-        if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
-      }
+      if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
+      else sp[2 + p] = __float_as_uint(n0);
+      if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
+    }
+    if (!multi && a.zero_after) {
+      const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+      float* g = a.grads + (size_t)row * S * gs;
+      const int w = a.fm_compact ? 2 : ps;
+      for (int s = 0; s < S; ++s)
+        for (int c = p; c < w; c += L.P) g[s * gs + c] = 0.0f;
+      if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }
   }
-}
-
-template <int G>
-static void launch_apply_group(const ApplyArgs& a, int grid, hipStream_t st) {
-  if (a.grp.oidx)
-    hipLaunchKernelGGL((k_apply_group<G, 1>), dim3(grid), dim3(kBlock), 0, st, a);
-  else
-    hipLaunchKernelGGL((k_apply_group<G, kGroupKeys>), dim3(grid), dim3(kBlock), 0, st, a);
 }
 
 void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
   const TableLayout& L = a.table.L;
   int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
+  const int64_t nm = a.n_dev ? a.n_max : a.n_host;
   const bool lr16 = L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag && a.S == 1 &&
                     !a.masks && a.pstride == 1;
   if (a.grp.oidx) {
-    if (a.zero_after || a.reset_pos || a.pstride > 64)
-      throw std::runtime_error("multi-source apply: unsupported arguments");
-    if (lr16) {
-      hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);
-    } else {
-      int64_t nm = a.n_dev ? a.n_max : a.n_host;
-      const int G = group_for(a.pstride);
-      const int g2 = grid_for(nm * G, kBlock, kGroupGridCap);
-      switch (G) {
-        case 1: launch_apply_group<1>(a, g2, st); break;
-        case 2: launch_apply_group<2>(a, g2, st); break;
-        case 4: launch_apply_group<4>(a, g2, st); break;
-        case 8: launch_apply_group<8>(a, g2, st); break;
-        case 16: launch_apply_group<16>(a, g2, st); break;
-        case 32: launch_apply_group<32>(a, g2, st); break;
-        default: launch_apply_group<64>(a, g2, st); break;
-      }
-    }
+    if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");
+    if (lr16) hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else if (lr16) {
     hipLaunchKernelGGL(k_apply_lr16, dim3(grid), dim3(kBlock), 0, st, a);
-  } else if (a.pstride >= 2 && a.pstride <= 64 && !a.reset_pos) {
-    int64_t nm = a.n_dev ? a.n_max : a.n_host;
-    const int G = group_for(a.pstride);
-    const int g2 = grid_for(nm * G, kBlock, kGroupGridCap);
-    switch (G) {
-      case 2: launch_apply_group<2>(a, g2, st); break;
-      case 4: launch_apply_group<4>(a, g2, st); break;
-      case 8: launch_apply_group<8>(a, g2, st); break;
-      case 16: launch_apply_group<16>(a, g2, st); break;
-      case 32: launch_apply_group<32>(a, g2, st); break;
-      default: launch_apply_group<64>(a, g2, st); break;
-    }
+  } else if (a.pstride >= 2 && L.P <= kWave && !a.reset_pos) {
+    hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_apply_generic, dim3(grid), dim3(kBlock), 0, st, a);
   }

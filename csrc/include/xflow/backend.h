@@ -268,6 +268,16 @@ struct SynthArgs {                 // synthetic Criteo-shaped batch generator
   int64_t col_stride = 0;            // > 0: field-major output (BatchView::col_stride)
 };
 
+// Evaluation sums of a prediction set (Backend::eval_metrics): the inputs of
+// the reference's calculate_auc print (base.h:84-110).
+struct EvalMetrics {
+  int64_t n = 0;          // predictions
+  int64_t tp = 0;         // positives
+  uint64_t area = 0;      // sum over negatives of the positives ranked above (pctr desc, stable)
+  double log2_sum = 0;    // sum y*log2(p) + (1-y)*log2(1-p)
+  double ln_sum = 0;      // sum of -ln likelihood, p clipped to [1e-7, 1-1e-7]
+};
+
 class Backend {
  public:
   virtual ~Backend() = default;
@@ -339,6 +349,8 @@ class Backend {
   // keys a long run has accumulated but the current batches do not touch
   // (occupancy-realistic benchmarks).
   virtual void table_prefill(const TableView& t, int64_t n, u64 seed) = 0;
+  // AUC / logloss sums of n predictions (backend memory; labels 0/1 floats)
+  virtual EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) = 0;
 };
 
 std::unique_ptr<Backend> make_cpu_backend();

@@ -94,6 +94,12 @@ class Engine {
   // worker: release the per-step dedup scratch.
   void w_finish();
 
+  // AUC / logloss sums of n predictions in backend memory (labels 0/1 floats),
+  // computed on the device: only the scalars come back (base.h:84-110)
+  EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) {
+    return be_->eval_metrics(pctr, labels, n);
+  }
+
   // ---- stats / introspection -------------------------------------------
   // which = 0: training forward passes, 1: eval_step passes.
   LossStats read_stats(bool reset, int which = 0);

@@ -55,6 +55,10 @@ struct EvalResult {
 
 // Reference AUC / logloss printer semantics (base.h:84-110) on host data.
 EvalResult reference_auc(std::vector<std::pair<int, float>>& label_pctr);
+// The same printed line from device-computed sums (Backend::eval_metrics):
+// exact integer area, deterministic double log-likelihood sums, rounded to
+// the reference's float accumulators once at the end.
+EvalResult eval_result(const EvalMetrics& m);
 
 class Trainer {
  public:

@@ -32,6 +32,7 @@ struct ModelSpec {
   int fm_math = kFmReference;
   int mvm_math = kMvmCompat;
   int max_fields = 64;  // MVM per-row field buckets (device LDS budget)
+  int fm_mfma = 0;      // standard-math FM forward on the matrix cores (HIP, v_dim <= 8)
 
   XF_HD int P() const { return kind == kLR ? 1 : (kind == kFM ? 1 + v_dim : v_dim); }
   XF_HD int p_w() const { return kind == kMVM ? 0 : 1; }

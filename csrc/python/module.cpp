@@ -58,6 +58,7 @@ ModelSpec model_from(py::dict d) {
   if (d.contains("v_dim")) m.v_dim = d["v_dim"].cast<int>();
   if (d.contains("fm_math")) m.fm_math = d["fm_math"].cast<int>();
   if (d.contains("mvm_math")) m.mvm_math = d["mvm_math"].cast<int>();
+  if (d.contains("fm_mfma")) m.fm_mfma = d["fm_mfma"].cast<bool>() ? 1 : 0;
   return m;
 }
 
@@ -218,6 +219,25 @@ PYBIND11_MODULE(_xflow_native, m) {
              std::vector<u64> k(keys.data(), keys.data() + keys.size());
              std::vector<float> g(grads.data(), grads.data() + grads.size());
              e.push_host(k, g);
+           })
+      .def("eval_metrics",
+           [](Engine& e, uintptr_t pctr, uintptr_t labels, int64_t n) {
+             EvalMetrics m;
+             {
+               py::gil_scoped_release nogil;
+               m = e.eval_metrics(P<const float>(pctr), P<const float>(labels), n);
+             }
+             EvalResult r = eval_result(m);
+             py::dict d;
+             d["n"] = m.n;
+             d["tp"] = m.tp;
+             d["area"] = m.area;
+             d["log2_sum"] = m.log2_sum;
+             d["logloss_printed"] = r.logloss_printed;
+             d["ln_logloss"] = r.ln_logloss;
+             d["auc"] = r.auc;
+             d["line"] = r.line;
+             return d;
            })
       .def("prefill", &Engine::prefill, py::arg("n"), py::arg("seed") = 0x5eedull,
            py::call_guard<py::gil_scoped_release>())

@@ -60,6 +60,11 @@ def build_parser() -> argparse.ArgumentParser:
                          "(python -m xflow_amd.data.binfmt convert); default 65536")
     ap.add_argument("--cpu", action="store_true", help="use the native CPU backend")
     ap.add_argument("--pred-dir", default=".")
+    ap.add_argument("--no-pred-file", action="store_true",
+                    help="skip pred_<rank>_<block>.txt (AUC/logloss are computed on the device "
+                         "either way; the file is the only reason predictions reach the host)")
+    ap.add_argument("--fm-mfma", action="store_true",
+                    help="standard-math FM forward on the matrix cores (v_dim <= 8; A/B option)")
     ap.add_argument("--save", default="", help="checkpoint directory to write after training")
     ap.add_argument("--load", default="", help="checkpoint directory to resume from")
     ap.add_argument("--resume", default="",
@@ -80,10 +85,12 @@ def config_from_args(a) -> TrainConfig:
         resident=a.resident, fixed_width=not a.csr_only,
         test_block_bytes=a.test_block_bytes, serial_slices=a.serial_slices,
         keep_remainder=a.keep_remainder, mvm_predict_compat=a.mvm_predict_compat,
-        init_push=not a.no_init_push, pred_dir=a.pred_dir, checkpoint_dir=a.save,
+        init_push=not a.no_init_push, pred_dir=a.pred_dir, write_pred=not a.no_pred_file,
+        checkpoint_dir=a.save,
         save_every=a.save_every, resume_dir=a.resume,
         metrics_file=a.metrics, async_p2p=a.async_p2p,
-        model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math),
+        model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math,
+                          fm_mfma=a.fm_mfma),
         optim=OptimConfig(kind=a.optimizer, alpha=a.alpha, beta=a.beta, lambda1=a.lambda1,
                           lambda2=a.lambda2, lr=a.lr),
         engine=EngineConfig(table_log2_cap=a.log2_cap, sum_slices=a.sum_slices))

@@ -47,10 +47,14 @@ class ModelConfig:
     v_dim: int = 10
     fm_math: str = "reference"   # reference (fm_worker.cc math) | standard (Rendle FM)
     mvm_math: str = "compat"     # compat (fields [0,max)) | fixed (fields [0,max])
+    # standard-math FM forward on the matrix cores (v_mfma_f32_16x16x4_f32,
+    # GPU, v_dim <= 8); measured slower than the VALU form, see DESIGN.md 6
+    fm_mfma: bool = False
 
     def native(self) -> dict:
         return {"kind": model_kind(self.kind), "v_dim": int(self.v_dim),
-                "fm_math": FM_MATH[self.fm_math], "mvm_math": MVM_MATH[self.mvm_math]}
+                "fm_math": FM_MATH[self.fm_math], "mvm_math": MVM_MATH[self.mvm_math],
+                "fm_mfma": bool(self.fm_mfma)}
 
     @property
     def params_per_key(self) -> int:
@@ -103,6 +107,7 @@ class TrainConfig:
     mvm_predict_compat: bool = False
     init_push: bool = True
     pred_dir: str = "."
+    write_pred: bool = True      # the reference's pred_<rank>_<block>.txt (lr_worker.cc:74-77)
     checkpoint_dir: str = ""
     save_every: int = 0          # versioned checkpoint every N epochs (checkpoint.publish)
     resume_dir: str = ""         # versioned checkpoint root: resume from LATEST, save there

@@ -296,6 +296,20 @@ class Engine:
         self._sync_stream()
         return int(self._e.nonzero_weights())
 
+    def eval_metrics(self, pctr: torch.Tensor, labels: torch.Tensor) -> dict:
+        """AUC / logloss of predictions on this engine's device, computed there
+        (GPU: radix sort + rank sums; only scalars come back).  Returns the
+        reference's printed line (base.h:84-110) with auc / logloss_printed /
+        ln_logloss / n / tp."""
+        if pctr.device != self.device or labels.device != self.device:
+            raise ValueError("eval_metrics: tensors must be on the engine's device")
+        p = pctr.contiguous().float()
+        y = labels.contiguous().float()
+        if p.numel() != y.numel():
+            raise ValueError("eval_metrics: pctr and labels differ in length")
+        self._sync_stream()
+        return dict(self._e.eval_metrics(p.data_ptr(), y.data_ptr(), int(p.numel())))
+
     def export_table(self):
         self._sync_stream()
         return self._e.export_table()

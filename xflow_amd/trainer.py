@@ -278,10 +278,13 @@ class Trainer:
 
     # --------------------------------------------------------------- predict
     def predict(self, block: int = 0) -> Optional[dict]:
-        """Rank 0 predicts its test shard; other ranks serve their table shards."""
+        """Rank 0 predicts its test shard; other ranks serve their table shards.
+        AUC / logloss are computed on the device (Engine.eval_metrics: radix
+        sort + rank sums, csrc/hip/kernels_eval.hip); the predictions travel to
+        the host only for the reference's pred_<rank>_<block>.txt file."""
         cfg = self.cfg
         nat = _native.load()
-        labels, preds = [], []
+        dev_p, dev_y = [], []
         reader = None
         if self.rank == 0:
             tpath = shard_path(cfg.test_prefix, 0)
@@ -304,25 +307,35 @@ class Trainer:
                 continue
             if b.rows == 0:
                 continue
-            p = pctr.cpu().numpy()
-            lab = blk["labels"][:used].astype(np.int32)
+            p, y = pctr[:used], b.labels[:used]
             if compat_mvm and sr > 0:
-                keep = (np.arange(used) % sr) < min(self.engine.model.v_dim, sr)
-                p, lab = p[keep], lab[keep]
-            preds.append(p)
-            labels.append(lab)
+                keep = torch.from_numpy((np.arange(used) % sr) < min(self.engine.model.v_dim, sr))
+                keep = keep.to(p.device)
+                p, y = p[keep], y[keep]
+            dev_p.append(p.clone())
+            dev_y.append(y.clone())
         if self.rank != 0:
             return None
-        p = np.concatenate(preds) if preds else np.zeros(0, np.float32)
-        y = np.concatenate(labels) if labels else np.zeros(0, np.int32)
-        os.makedirs(cfg.pred_dir or ".", exist_ok=True)
-        with open(os.path.join(cfg.pred_dir or ".", "pred_%d_%d.txt" % (self.rank, block)), "w") as f:
-            for pi, yi in zip(p.tolist(), y.tolist()):
-                f.write("%s\t%d\t%d\n" % (_fmt_float(pi), 1 - yi, yi))
-        res = reference_auc(y, p)
+        dev = self.device
+        p = torch.cat(dev_p) if dev_p else torch.zeros(0, dtype=torch.float32, device=dev)
+        y = torch.cat(dev_y) if dev_y else torch.zeros(0, dtype=torch.float32, device=dev)
+        res = self.engine.eval_metrics(p, y)
+        dev_auc = res["auc"]
+        if cfg.write_pred:
+            os.makedirs(cfg.pred_dir or ".", exist_ok=True)
+            ph, yh = p.cpu().numpy(), y.cpu().numpy().astype(np.int32)
+            with open(os.path.join(cfg.pred_dir or ".", "pred_%d_%d.txt" % (self.rank, block)),
+                      "w") as f:
+                for pi, yi in zip(ph.tolist(), yh.tolist()):
+                    f.write("%s\t%d\t%d\n" % (_fmt_float(pi), 1 - yi, yi))
+            # predictions are on the host anyway: print the reference's exact
+            # line, whose AUC depends on std::sort's (unspecified) order of
+            # equal pctr values; the device AUC breaks ties by prediction order
+            res = reference_auc(yh, ph)
         _say(res["line"])
-        self.metrics.log(event="eval", auc=res["auc"], ln_logloss=res["ln_logloss"],
-                         logloss_printed=res["logloss_printed"], n=res["n"])
+        self.metrics.log(event="eval", auc=res["auc"], auc_device=dev_auc,
+                         ln_logloss=res["ln_logloss"], logloss_printed=res["logloss_printed"],
+                         n=res["n"])
         return res
 
     def train(self) -> Optional[dict]:
