@@ -21,7 +21,7 @@ def _dev(name):
 
 def _np_metrics(p, y):
     order = np.argsort(-p, kind="stable")
-    ys = y[order]
+    ys = y[order].astype(np.int64)  # (exact integer sums)
     tp_before = np.cumsum(ys) - ys
     area = int(tp_before[ys == 0].sum())
     return area, int(ys.sum())
