@@ -68,6 +68,16 @@ class CpuBackend final : public Backend {
   bool is_gpu() const override { return false; }
   std::string name() const override { return "cpu"; }
 
+  void upload_small(void* dst, const void* src, size_t bytes) override {
+    if (bytes) std::memcpy(dst, src, bytes);
+  }
+  void* stage_pinned(int s, size_t bytes) override {
+    if (stage_buf_[s].size() < bytes) stage_buf_[s].resize(bytes);
+    return stage_buf_[s].data();
+  }
+  void stage_copy(int s, void* dst, size_t off, size_t bytes) override {
+    if (bytes) std::memcpy(dst, stage_buf_[s].data() + off, bytes);
+  }
   void* alloc(size_t bytes) override {
     void* p = std::aligned_alloc(64, ((bytes ? bytes : 16) + 63) & ~size_t(63));
     if (!p) throw std::bad_alloc();
@@ -432,6 +442,9 @@ class CpuBackend final : public Backend {
     }
     return n;
   }
+
+ private:
+  std::vector<char> stage_buf_[2];
 };
 
 }  // namespace

@@ -139,6 +139,10 @@ Engine::~Engine() {
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, own_pos_[0],
                   own_pos_[1], own_idx_[0], own_idx_[1], srv_w_[0], srv_w_[1], fm_grad_};
   for (void* p : ptrs) be.free(p);
+  for (StageSet& a : aset_) {
+    void* ap[] = {a.keys, a.rowptr, a.fgid, a.labels};
+    for (void* p : ap) be.free(p);
+  }
   for (WorkerSet& w : wset_) {
     void* wp[] = {w.pos, w.uniq_pos, w.inv, w.n_uniq, w.send_pos};
     for (void* p : wp) be.free(p);
@@ -202,7 +206,7 @@ const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
     // an empty slice has no gradient rows; 1 keeps 0/rows finite
     h[s] = (int32_t)(rem < sr ? (rem > 0 ? rem : 1) : sr);
   }
-  be_->copy_h2d(slice_rows_, h, sizeof(int32_t) * S);
+  be_->upload_small(slice_rows_, h, sizeof(int32_t) * S);  // (no host wait)
   cached_S_ = S;
   cached_rows_ = b.rows;
   cached_slice_rows_ = b.slice_rows;
@@ -884,6 +888,46 @@ BatchView Engine::stage_host_batch(const BatchView& h) {
   be_->copy_h2d(st_labels_, h.labels, sizeof(float) * h.rows);
   b.labels = st_labels_;
   return b;
+}
+
+BatchView Engine::stage_host_batch_async(const BatchView& h) {
+  if (h.rows > cfg_.max_rows || h.nnz > cfg_.max_nnz)
+    throw std::invalid_argument("host batch exceeds engine capacity");
+  const int s = astage_next_;
+  astage_next_ ^= 1;
+  StageSet& d = aset_[s];
+  if (!d.keys) {
+    d.keys = balloc<u64>(*be_, cfg_.max_nnz);
+    d.rowptr = balloc<int32_t>(*be_, cfg_.max_rows + 1);
+    d.fgid = balloc<int32_t>(*be_, cfg_.max_nnz);
+    d.labels = balloc<float>(*be_, cfg_.max_rows);
+  }
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bk = sizeof(u64) * h.nnz, br = h.row_ptr ? sizeof(int32_t) * (h.rows + 1) : 0,
+               bf = h.fgid ? sizeof(int32_t) * h.nnz : 0, bl = sizeof(float) * h.rows;
+  const size_t ok = 0, orp = up(bk), of = orp + up(br), ol = of + up(bf);
+  be_->stage_begin(s);
+  char* pin = static_cast<char*>(be_->stage_pinned(s, ol + up(bl)));
+  std::memcpy(pin + ok, h.keys, bk);
+  if (br) std::memcpy(pin + orp, h.row_ptr, br);
+  if (bf) std::memcpy(pin + of, h.fgid, bf);
+  std::memcpy(pin + ol, h.labels, bl);
+  be_->stage_copy(s, d.keys, ok, bk);
+  if (br) be_->stage_copy(s, d.rowptr, orp, br);
+  if (bf) be_->stage_copy(s, d.fgid, of, bf);
+  be_->stage_copy(s, d.labels, ol, bl);
+  be_->stage_commit(s);
+  astage_last_ = s;
+  BatchView b = h;
+  b.keys = d.keys;
+  b.row_ptr = h.row_ptr ? d.rowptr : nullptr;
+  b.fgid = h.fgid ? d.fgid : nullptr;
+  b.labels = d.labels;
+  return b;
+}
+
+void Engine::stage_release() {
+  if (astage_last_ >= 0) be_->stage_release(astage_last_);
 }
 
 // ---------------------------------------------------------------------------

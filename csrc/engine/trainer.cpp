@@ -1,6 +1,8 @@
 // xflow-amd: native training loop (see xflow/trainer.h).
 #include "xflow/trainer.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -129,11 +131,16 @@ void Trainer::train_block(const CsrBlock& blk) {
   h.rows = used;
   h.nnz = blk.row_ptr[used];
   h.slice_rows = slice_rows;
-  BatchView d = engine_->stage_host_batch(h);
-  if (!cfg_.serial_slices) {
+  static const bool sync_staging = std::getenv("XFLOW_SYNC_STAGING") != nullptr;  // (A/B)
+  if (!cfg_.serial_slices && !sync_staging) {
+    // double-buffered: this block's H2D copies run on the copy queue while
+    // the previous block trains; the host returns to parsing right away
+    BatchView d = engine_->stage_host_batch_async(h);
     engine_->train_step(d);
+    engine_->stage_release();
     return;
   }
+  BatchView d = engine_->stage_host_batch(h);
   // serial: one engine step per slice, in slice order
   for (int64_t s0 = 0; s0 < used; s0 += slice_rows) {
     int64_t n = std::min(slice_rows, used - s0);

@@ -25,8 +25,57 @@ class HipBackend final : public Backend {
   }
   ~HipBackend() override {
     hipSetDevice(device_);
+    if (copy_stream_) (void)hipStreamSynchronize(copy_stream_);
+    for (int s = 0; s < 2; ++s) {
+      if (pinned_[s]) (void)hipHostFree(pinned_[s]);
+      if (ev_copied_[s]) (void)hipEventDestroy(ev_copied_[s]);
+      if (ev_used_[s]) (void)hipEventDestroy(ev_used_[s]);
+    }
+    if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     if (counter_) (void)hipFree(counter_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
+  }
+
+  // ---- double-buffered H2D staging on a copy stream (see Backend) ----
+  void stage_begin(int s) override {
+    if (!copy_stream_) {
+      XF_HIP_CHECK(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+      for (int i = 0; i < 2; ++i) {
+        XF_HIP_CHECK(hipEventCreateWithFlags(&ev_copied_[i], hipEventDisableTiming));
+        XF_HIP_CHECK(hipEventCreateWithFlags(&ev_used_[i], hipEventDisableTiming));
+      }
+    }
+    if (copied_pending_[s]) {  // the pinned buffer is free once its copies finished
+      XF_HIP_CHECK(hipEventSynchronize(ev_copied_[s]));
+      copied_pending_[s] = false;
+    }
+    waited_used_[s] = false;
+  }
+  void* stage_pinned(int s, size_t bytes) override {
+    if (bytes > pinned_cap_[s]) {
+      if (pinned_[s]) XF_HIP_CHECK(hipHostFree(pinned_[s]));
+      pinned_cap_[s] = bytes + bytes / 4;
+      XF_HIP_CHECK(hipHostMalloc(&pinned_[s], pinned_cap_[s], hipHostMallocDefault));
+    }
+    return pinned_[s];
+  }
+  void stage_copy(int s, void* dst, size_t off, size_t bytes) override {
+    if (!bytes) return;
+    if (used_pending_[s] && !waited_used_[s]) {  // the last step reading slot s's buffers
+      XF_HIP_CHECK(hipStreamWaitEvent(copy_stream_, ev_used_[s], 0));
+      waited_used_[s] = true;
+    }
+    XF_HIP_CHECK(hipMemcpyAsync(dst, static_cast<char*>(pinned_[s]) + off, bytes,
+                                hipMemcpyHostToDevice, copy_stream_));
+  }
+  void stage_commit(int s) override {
+    XF_HIP_CHECK(hipEventRecord(ev_copied_[s], copy_stream_));
+    XF_HIP_CHECK(hipStreamWaitEvent(stream_, ev_copied_[s], 0));
+    copied_pending_[s] = true;
+  }
+  void stage_release(int s) override {
+    XF_HIP_CHECK(hipEventRecord(ev_used_[s], stream_));
+    used_pending_[s] = true;
   }
 
   bool is_gpu() const override { return true; }
@@ -57,6 +106,9 @@ class HipBackend final : public Backend {
   }
   void copy_d2d(void* dst, const void* src, size_t bytes) override {
     if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
+  }
+  void upload_small(void* dst, const void* src, size_t bytes) override {
+    hip::launch_upload_small(dst, src, bytes, stream_);
   }
   void synchronize() override { XF_HIP_CHECK(hipStreamSynchronize(stream_)); }
   // nullptr selects the null (default) stream, which is what torch reports as
@@ -133,6 +185,12 @@ class HipBackend final : public Backend {
   hipStream_t own_stream_ = nullptr;
   hipStream_t stream_ = nullptr;
   unsigned long long* counter_ = nullptr;
+  hipStream_t copy_stream_ = nullptr;
+  hipEvent_t ev_copied_[2] = {nullptr, nullptr}, ev_used_[2] = {nullptr, nullptr};
+  void* pinned_[2] = {nullptr, nullptr};
+  size_t pinned_cap_[2] = {0, 0};
+  bool copied_pending_[2] = {false, false}, used_pending_[2] = {false, false};
+  bool waited_used_[2] = {false, false};
 };
 
 }  // namespace

@@ -19,6 +19,8 @@
 // several independent probes in flight per lane, count bookkeeping with one
 // atomic per workgroup (single-address atomics serialise), and read
 // device-side element counts so a whole step runs without host syncs.
+#include <cstring>
+
 #include "kernels.h"
 #include "hip_util.h"
 
@@ -403,6 +405,24 @@ void launch_scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, i
 __global__ void k_fill_u64(u64* p, u64 v, size_t n) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+struct SmallBytes {
+  unsigned char b[256];
+};
+
+__global__ void k_upload_small(unsigned char* __restrict__ dst, SmallBytes v, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = v.b[i];
+}
+
+void launch_upload_small(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return;
+  if (bytes > sizeof(SmallBytes)) throw std::runtime_error("upload_small: at most 256 bytes");
+  SmallBytes v;
+  std::memcpy(v.b, src, bytes);
+  hipLaunchKernelGGL(k_upload_small, dim3(1), dim3(64), 0, st, static_cast<unsigned char*>(dst),
+                     v, (int)bytes);
+  XF_HIP_CHECK(hipGetLastError());
 }
 
 void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st) {

@@ -292,9 +292,25 @@ class Backend {
   virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;
   virtual void copy_d2h(void* dst, const void* src, size_t bytes) = 0;  // synchronising
   virtual void copy_d2d(void* dst, const void* src, size_t bytes) = 0;
+  // <= 256 bytes from the host, queued without a host wait (HIP: the bytes
+  // travel as a kernel argument)
+  virtual void upload_small(void* dst, const void* src, size_t bytes) = 0;
   virtual void synchronize() = 0;
   virtual void set_stream(void* stream) = 0;
   virtual void* stream() const = 0;
+
+  // Asynchronous double-buffered host -> device staging (the native trainer's
+  // input path).  Slot s in {0, 1}: stage_begin(s) waits on the host until
+  // slot s's previous copies have left its pinned buffer; stage_pinned
+  // returns that pinned buffer (grow-only); stage_copy queues dst <- pinned+off
+  // on a copy queue, after the compute work that last read slot s's device
+  // buffers (stage_release); stage_commit makes the compute queue wait for the
+  // slot's copies.  The CPU backend copies synchronously.
+  virtual void stage_begin(int s) { (void)s; }
+  virtual void* stage_pinned(int s, size_t bytes) = 0;
+  virtual void stage_copy(int s, void* dst, size_t off, size_t bytes) = 0;
+  virtual void stage_commit(int s) { (void)s; }
+  virtual void stage_release(int s) { (void)s; }
 
   // kernels
   // Mark every slot free (key words = kEmptyKey) with zero optimizer state.

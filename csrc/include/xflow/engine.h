@@ -136,6 +136,13 @@ class Engine {
   BatchView synth_batch(const SynthArgs& a, int64_t slice_rows);
   // Copy a host CSR batch into engine-owned staging buffers.
   BatchView stage_host_batch(const BatchView& host);
+  // Asynchronous, double-buffered variant (the native trainer's input path):
+  // the host arrays are copied into a pinned buffer and sent on the
+  // backend's copy queue while earlier steps run; the compute queue waits
+  // for them.  Call stage_release() after queueing the steps that read the
+  // returned batch, before staging the batch after the next one.
+  BatchView stage_host_batch_async(const BatchView& host);
+  void stage_release();
 
  private:
   void ensure_server_capacity(int64_t n, int buf = 0);
@@ -223,6 +230,15 @@ class Engine {
   int cached_S_ = -1;
   int64_t last_nsend_ = 0;
 
+  // async staging sets (stage_host_batch_async)
+  struct StageSet {
+    u64* keys = nullptr;
+    int32_t* rowptr = nullptr;
+    int32_t* fgid = nullptr;
+    float* labels = nullptr;
+  };
+  StageSet aset_[2];
+  int astage_next_ = 0, astage_last_ = -1;
   // staging batch buffers (backend memory)
   u64* st_keys_ = nullptr;
   int32_t* st_rowptr_ = nullptr;

@@ -59,6 +59,7 @@ int main(int argc, char* argv[]) {
     else if (a == "--mvm-predict-compat") cfg.mvm_predict_compat = true;
     else if (a == "--v-dim") cfg.model_spec.v_dim = std::atoi(next());
     else if (a == "--log2-cap") cfg.table_log2_cap = std::atoi(next());
+    else if (a == "--train-block-bytes") cfg.train_block_bytes = std::atoll(next());
     else if (a == "--save") save = next();
     else if (a == "--load") load = next();
     else {

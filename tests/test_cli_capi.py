@@ -139,3 +139,60 @@ def test_local_sh_records_pids_and_stop_sh_kills_them(tmp_path):
     finally:
         if launcher.poll() is None:
             launcher.kill()
+
+
+GPU_ENV = dict(os.environ, PYTHONPATH=ROOT, XFLOW_DEVICE="0")
+
+
+def _eval_line(out):
+    line = [l for l in _lines(out) if l.startswith("logloss: ")][-1]
+    ll = float(line.split("\t")[0].split()[1])
+    auc = float(line.split("auc = ")[1].split("\t")[0])
+    return ll, auc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["0", "1", "2"])
+def test_native_binary_gpu_matches_cpu(tmp_path, model):
+    """build/bin/xflow_lr on the HIP backend (double-buffered H2D staging on a
+    copy queue) trains the same model as on the native CPU backend."""
+    binp = os.path.join(ROOT, "build", "bin", "xflow_lr")
+    (tmp_path / "cpu").mkdir()
+    (tmp_path / "gpu").mkdir()
+    a = _run([binp, TRAIN, TEST, model, "5", "--threads", "8"], tmp_path / "cpu")
+    b = _run([binp, TRAIN, TEST, model, "5", "--threads", "8", "--device", "0"],
+             tmp_path / "gpu", env=GPU_ENV)
+    (lla, auca), (llb, aucb) = _eval_line(a), _eval_line(b)
+    assert abs(lla - llb) <= 1e-4 * abs(lla) and abs(auca - aucb) <= 2e-3
+    pa = [[float(x) for x in l.split()] for l in open(tmp_path / "cpu" / "pred_0_0.txt")]
+    pb = [[float(x) for x in l.split()] for l in open(tmp_path / "gpu" / "pred_0_0.txt")]
+    import numpy as np
+
+    np.testing.assert_allclose(np.array(pb), np.array(pa), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_c_api_gpu_matches_cpu(tmp_path):
+    lib = ctypes.CDLL(os.path.join(ROOT, "build", "lib", "libxflow_api.so"))
+    lib.XFCreateEx.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_char_p, ctypes.c_char_p,
+                               ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.XFGetLastError.restype = ctypes.c_char_p
+    res = []
+    cwd = os.getcwd()
+    for dev in (-1, 0):
+        d = tmp_path / str(dev)
+        d.mkdir()
+        os.chdir(d)
+        try:
+            h = ctypes.c_void_p()
+            assert lib.XFCreateEx(ctypes.byref(h), TRAIN.encode(), TEST.encode(), 0, 10, 8,
+                                  dev) == 0
+            assert lib.XFStartTrain(ctypes.byref(h)) == 0, lib.XFGetLastError()
+            ll, auc = ctypes.c_double(), ctypes.c_double()
+            assert lib.XFPredict(ctypes.byref(h), ctypes.byref(ll), ctypes.byref(auc)) == 0
+            res.append((ll.value, auc.value))
+            assert lib.XFFree(ctypes.byref(h)) == 0
+        finally:
+            os.chdir(cwd)
+    (la, aa), (lb, ab) = res
+    assert abs(la - lb) <= 1e-4 * abs(la) and abs(aa - ab) <= 2e-3
