@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=262144, help="rows per GPU per step")
     ap.add_argument("--model", default="lr", choices=["lr", "fm", "mvm"])
     ap.add_argument("--v-dim", type=int, default=8)
+    ap.add_argument("--slices", type=int, default=1,
+                    help="Hogwild slices per step (lr_worker.cc:190-199): every slice reads the "
+                         "same weights, gradients normalised per slice, pushes applied per key in "
+                         "slice order")
     ap.add_argument("--optimizer", default="ftrl", choices=["ftrl", "sgd"])
     ap.add_argument("--log2-cap", type=int, default=0,
                     help="table slots per GPU = 2^N (default: 2^31 across the node)")
@@ -107,9 +111,11 @@ def main():
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
                                        v_init_scale=a.v_init_scale),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
-                                 max_slices=1),
+                                 max_slices=a.slices),
                     device=device)
-    gen = SyntheticCriteo(engine, a.batch, synth, rank=rank)
+    if a.batch % a.slices:
+        raise SystemExit("--batch must be a multiple of --slices")
+    gen = SyntheticCriteo(engine, a.batch, synth, rank=rank, slice_rows=a.batch // a.slices)
     if a.table_load < 0:  # (the CPU smoke path runs on a small table: no default prefill)
         n_prefill = a.features // world if use_gpu else 0
     else:
@@ -221,6 +227,7 @@ def main():
                        "global_batch": a.batch * world, "seq_len": synth.fields,
                        "parallelism": f"dp{world}+table-shard{world}",
                        "rows_per_gpu": a.batch, "nnz_per_row": synth.fields,
+                       "slices": a.slices,
                        "hashed_features": a.features, "table_slots_per_gpu": 2 ** log2_cap,
                        "backend": engine.backend_name,
                        "a2a_transport": sharded.transport if sharded is not None else "none",

@@ -137,6 +137,7 @@ class CpuBackend final : public Backend {
     }
     *o.n_uniq = u;
     if (o.n_uniq_copy) *o.n_uniq_copy = u;
+    if (o.cap_out) *o.cap_out = s.cap;
   }
 
   void scratch_reset(ScratchView s, const u32* pos, const int64_t* n_dev, int64_t n_max) override {

@@ -82,6 +82,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   wset_[0].uniq_pos = uniq_pos_;
   wset_[0].n_uniq = n_uniq_;
   wset_[0].send_pos = send_pos_;
+  bcap_ = balloc<unsigned long long>(be, 1);
+  be.memset(bcap_, 0, sizeof(unsigned long long));
+  wset_[0].bcap = bcap_;
   // slot-indexed buffers carry one extra row: the trash slot (index cap) that
   // a dedup probe overflow sends its occurrences to (flagged, never applied)
   const uint64_t rows1 = scratch_.cap + 1;
@@ -97,9 +100,18 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     const int nv = fm_ref ? 2 : 1, shift = red_shift(nv);
     const int group_rows = fm_ref ? kFmGroupRows : (mvm ? kMvmGroupRows : kLrGroupRows);
     // (the trash slot's occurrences are never reduced: FwdArgs::trash_pos)
+    // Buckets of 2^shift dests at the allocated capacity; beyond
+    // kRedMaxBuckets the device widens the buckets (FwdArgs::red_bcap) and
+    // sums a wide bucket with red_nsub workgroups -- only when the adaptive
+    // scratch has grown that far (bench shape: S = 8 at 2^23 active slots
+    // stays at 4096 buckets of 2^14).
     const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
-    const int nb = (int)((dests + (1ull << shift) - 1) >> shift);
-    if (nb <= kRedMaxBuckets) {
+    int nb = (int)((dests + (1ull << shift) - 1) >> shift);
+    int nsub = 1;
+    while ((uint64_t)nb > (uint64_t)kRedMaxBuckets * nsub) nsub <<= 1;
+    if (nsub > 1) nb = kRedMaxBuckets;
+    red_nsub_ = nsub;
+    if (nb <= kRedMaxBuckets && dests < (1ull << 32)) {
       const int64_t groups = (cfg_.max_rows + group_rows - 1) / group_rows;
       red_nb_ = nb;
       red_pairs_ = balloc<u64>(be, (size_t)nnz * nv);  // nv u64 words per record
@@ -144,7 +156,7 @@ Engine::~Engine() {
     for (void* p : ap) be.free(p);
   }
   for (WorkerSet& w : wset_) {
-    void* wp[] = {w.pos, w.uniq_pos, w.inv, w.n_uniq, w.send_pos};
+    void* wp[] = {w.pos, w.uniq_pos, w.inv, w.n_uniq, w.send_pos, w.bcap};
     for (void* p : wp) be.free(p);
   }
 }
@@ -159,6 +171,7 @@ void Engine::use_worker_set(int wb) {
   c.send_pos = send_pos_;
   c.send_map = send_map_;
   c.inv_valid = inv_valid_;
+  c.bcap = bcap_;
   WorkerSet& w = wset_[wb];
   if (!w.pos) {  // second set: allocated on first use (pipelined sharded step)
     const int64_t nnz = cfg_.max_nnz;
@@ -167,6 +180,8 @@ void Engine::use_worker_set(int wb) {
     w.send_pos = balloc<u32>(*be_, nnz);
     w.n_uniq = balloc<int64_t>(*be_, 1);
     be_->memset(w.n_uniq, 0, sizeof(int64_t));
+    w.bcap = balloc<unsigned long long>(*be_, 1);
+    be_->memset(w.bcap, 0, sizeof(unsigned long long));
   }
   pos_ = w.pos;
   uniq_pos_ = w.uniq_pos;
@@ -175,12 +190,16 @@ void Engine::use_worker_set(int wb) {
   send_pos_ = w.send_pos;
   send_map_ = w.send_map;
   inv_valid_ = w.inv_valid;
+  bcap_ = w.bcap;
   cur_wb_ = wb;
 }
 
 void Engine::set_reduction(FwdArgs& fa) const {
   fa.trash_pos = (u32)scratch_.cap;
   if (!red_pairs_) return;
+  fa.red_bcap = bcap_;
+  fa.red_cap = scratch_.cap;
+  fa.red_nsub = red_nsub_;
   fa.red_pairs = red_pairs_;
   fa.red_sorted = red_sorted_;
   fa.red_hist = red_hist_;
@@ -244,6 +263,7 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
   o.block_counts = block_counts_;
   o.inv = want_inv ? inv_ : nullptr;
   o.n_uniq_copy = n_copy;
+  o.cap_out = bcap_;
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 
@@ -267,9 +287,14 @@ void Engine::train_step(const BatchView& b) {
   // slot -> unique index map) and the apply takes (n, z) from the pull, so it
   // reads nothing at random and writes the slot once.
   const TableLayout& L = table_.L;
-  const bool lr16 = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 && L.P == 1 &&
-                    L.opt == kFTRL && !L.has_flag && S == 1 && red_pairs_ &&
-                    (double)scratch_.cap < 4294967295.0 && !lr16_disabled();
+  const bool lr16_layout_ok = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 &&
+                              L.P == 1 && L.opt == kFTRL && !L.has_flag && red_pairs_ &&
+                              (double)scratch_.cap < 4294967295.0 && !lr16_disabled();
+  const bool lr16 = lr16_layout_ok && S == 1;
+  // several slices: slot-indexed sums, ordered per-slice pushes (packed
+  // apply), but still the pull-time (n, z) stash
+  const bool lr16s = lr16_layout_ok && S > 1;
+  if (lr16s && !lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   if (lr16) {
     ensure_inv();
     if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz);
@@ -300,6 +325,7 @@ void Engine::train_step(const BatchView& b) {
     pa.out_nz = lr_nz_;
     pa.zero_out = lr_grad_;
   }
+  if (lr16s) pa.out_nz = lr_nz_;
   if (fmu) {
     pa.zero_out = fm_grad_;
     pa.zero_width = 2;
@@ -360,6 +386,7 @@ void Engine::train_step(const BatchView& b) {
     aa.slice_rows = nullptr;
     aa.nz_stash = lr_nz_;
   }
+  if (lr16s) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
   if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
     aa.grads = fm_grad_;
     aa.grad_map = nullptr;

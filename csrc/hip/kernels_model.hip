@@ -24,6 +24,25 @@ __device__ __forceinline__ int slice_of(const BatchView& b, int64_t r, int S) {
   return (int)(s < S ? s : S - 1);
 }
 
+// Bucket geometry of this step's gradient reduction (FwdArgs::red_bcap):
+// the smallest shift >= base that keeps ceil(dests / 2^shift) within
+// kRedMaxBuckets, dests = (batch scratch capacity) * S.
+struct RedGeom {
+  const unsigned long long* bcap;
+  u64 cap;
+  int S;
+  __device__ __forceinline__ int shift(int base) const {
+    const u64 dests = (bcap ? (u64)*bcap : cap) * (u64)S;
+    int sh = base;
+    while (((dests + (1ull << sh) - 1) >> sh) > (u64)kRedMaxBuckets) ++sh;
+    return sh;
+  }
+};
+
+__host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
+  return RedGeom{a.red_bcap, a.red_cap, a.S};
+}
+
 // Per-row loss statistics, reduced per workgroup then one f64 atomic each.
 struct StatAcc {
   double ln = 0, l2 = 0, rows = 0, pos = 0;
@@ -165,6 +184,7 @@ struct ListAgg {
   u32* hist;    // [red_nb]
   u64* region;  // this workgroup's pair region
   u32 written;  // pairs written so far (workgroup-uniform)
+  int shift = kShift;  // bucket = dest >> shift (RedGeom: runtime, >= kShift)
 
   __device__ __forceinline__ void init(int nb) {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
@@ -234,8 +254,8 @@ struct ListAgg {
         reinterpret_cast<uint4*>(region)[written + i] =
             make_uint4(d, __float_as_uint(v), __float_as_uint(v2), 0u);
       }
-      XF_DASSERT((int)(d >> kShift) < kRedMaxBuckets);
-      atomicAdd(&hist[d >> kShift], 1u);
+      XF_DASSERT((int)(d >> shift) < kRedMaxBuckets);
+      atomicAdd(&hist[d >> shift], 1u);
     }
     written += n;
   }
@@ -299,6 +319,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
     const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
     lagg.region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
     lagg.init(a.red_nb);
+    lagg.shift = red_geom(a).shift(red_shift(1));
   }
   // block-uniform longest row: selects the register path and bounds the
   // backward column walk
@@ -565,10 +586,11 @@ __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows
                                                            const u32* __restrict__ hist,
                                                            const u32* __restrict__ tot,
                                                            u32* __restrict__ start, int nb,
-                                                           void* __restrict__ sorted) {
+                                                           void* __restrict__ sorted,
+                                                           RedGeom geom) {
   using R = RedRec<NV>;
   using T = typename R::T;
-  constexpr int kShift = red_shift(NV);
+  const int kShift = geom.shift(red_shift(NV));
   __shared__ u32 cur[kRedMaxBuckets];
   const int g = blockIdx.x, groups = gridDim.x;
   u32 carry = 0;
@@ -626,14 +648,21 @@ struct RedFinal {
 
 template <int NV>
 __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ sorted,
-                                                       const u32* __restrict__ start, RedFinal f) {
+                                                       const u32* __restrict__ start, RedFinal f,
+                                                       RedGeom geom, int nb) {
   using T = typename RedRec<NV>::T;
   constexpr int kShift = red_shift(NV);
   constexpr u32 kR = 1u << kShift;
   constexpr int kFx = FxBits<NV>::kFx;
+  // workgroup (bucket, sub): a bucket of 2^shift dests is summed by 2^(shift -
+  // kShift) workgroups of kR dests each (one in the common case)
+  const int b = (int)(blockIdx.x % (unsigned)nb), sub = (int)(blockIdx.x / (unsigned)nb);
+  const int shift = geom.shift(kShift);
+  if (sub >= (1 << (shift - kShift))) return;
+  const u64 lo = ((u64)b << shift) + ((u64)sub << kShift);
   // fixed-point accumulators: the bucket's sums do not depend on record order
   __shared__ long long acc[kR * NV];
-  const u32 beg = start[blockIdx.x], end = start[blockIdx.x + 1];
+  const u32 beg = start[b], end = start[b + 1];
   if (beg == end) return;
   for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
   __syncthreads();
@@ -648,11 +677,12 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
 #pragma unroll
     for (int q = 0; q < kRedUnroll; ++q) {
       if (i0 + (u32)q * kRedBlock >= end) continue;
+      const u64 l = (u64)RedRec<NV>::dest(pr[q]) - lo;
+      if (l >= kR) continue;  // another sub-bucket's dest
       if constexpr (NV == 1) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[(u32)pr[q] & (kR - 1)]),
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l]),
                   (unsigned long long)fx_from<kFx>(__uint_as_float((u32)(pr[q] >> 32))));
       } else {
-        const u32 l = pr[q].x & (kR - 1);
         atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2]),
                   (unsigned long long)fx_from<kFx>(__uint_as_float(pr[q].y)));
         atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2 + 1]),
@@ -661,7 +691,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
     }
   }
   __syncthreads();
-  const u64 d0 = (u64)blockIdx.x << kShift;
+  const u64 d0 = lo;
   if constexpr (NV == 1) {
     if (f.out) {
       // normalised like the gather would (lr_worker.cc:116-118, in double)
@@ -725,13 +755,14 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
   u32* start = a.red_tot + a.red_nb + 1;
   hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
                      rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
-                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
+                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
+                     red_geom(a));
   if (a.red_out && (a.S != 1 || (NV == 2 && !a.fm_compact)))
     throw std::runtime_error("red_out: one slice (and compact rows for FM) only");
   RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim, a.red_out, a.red_inv,
              a.red_rows, NV == 2 && a.fm_compact};
-  hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb), dim3(kRedBlock), 0, st,
-                     static_cast<const void*>(a.red_sorted), start, f);
+  hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb * a.red_nsub), dim3(kRedBlock), 0, st,
+                     static_cast<const void*>(a.red_sorted), start, f, red_geom(a), a.red_nb);
 }
 
 // Reference-math FM on the atomic-free reduction path.  The gradient of key i
@@ -763,6 +794,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
                                                   : r0 * b.nnz_per_row));
   ListAgg<LOG2, 2> lagg{s_tag64, s_acc, s_list, s_nlist, s_hist, region, 0u};
   lagg.init(a.red_nb);
+  lagg.shift = red_geom(a).shift(red_shift(2));
   int maxlen;
   if (!b.row_ptr) {
     maxlen = b.nnz_per_row;
@@ -854,6 +886,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
     lagg.region = reinterpret_cast<u64*>(reinterpret_cast<uint4*>(a.red_pairs) +
                                          (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row));
     lagg.init(a.red_nb);
+    lagg.shift = red_geom(a).shift(red_shift(2));
     if (!b.row_ptr) {
       maxlen = b.nnz_per_row;
       __syncthreads();
@@ -1241,6 +1274,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
       const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
       u64* region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
       const int lane = lane_id();
+      const int hshift = red_geom(a).shift(kRedShift);
       for (int j = 0; j < maxlen; ++j) {
         const u32 pj = emit && j < len ? pos[rs.at(j)] : a.trash_pos;
         const bool has = pj != a.trash_pos;
@@ -1254,8 +1288,8 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           if (has) {
             region[base + (u32)__popcll(bm & ((1ull << lane) - 1ull))] =
                 (u64)dest | ((u64)(u32)r << 32);
-            XF_DASSERT((int)(dest >> kRedShift) < a.red_nb);
-            atomicAdd(&s_hist[dest >> kRedShift], 1u);
+            XF_DASSERT((int)(dest >> hshift) < a.red_nb);
+            atomicAdd(&s_hist[dest >> hshift], 1u);
           }
         }
       }
@@ -1318,6 +1352,8 @@ struct MvmRedFinal {
   const float* wpull;
   const float* rowv;
   int S, nb;
+  RedGeom geom;
+  int nsubt;  // sub-buckets per bucket in the grid (NSUB x the largest bucket widening)
 };
 
 template <int D>
@@ -1330,9 +1366,13 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
   constexpr u32 kSub = 1u << kSubShift;
   __shared__ float acc[kSub * D];
   const u32 q = blockIdx.x >> 3;
-  const u32 sub = q % NSUB;
-  const int bucket = (int)((q / NSUB) * 8 + (blockIdx.x & 7));
+  const u32 sub = q % (u32)f.nsubt;
+  const int bucket = (int)((q / (u32)f.nsubt) * 8 + (blockIdx.x & 7));
   if (bucket >= f.nb) return;
+  // a bucket of 2^shift dests (RedGeom) has NSUB << (shift - kRedShift) subs
+  const int shift = f.geom.shift(kRedShift);
+  if (sub >= ((u32)NSUB << (shift - kRedShift))) return;
+  const u64 lo = ((u64)bucket << shift) + ((u64)sub << kSubShift);
   const u32 beg = start[bucket], end = start[bucket + 1];
   if (beg == end) return;
   for (u32 i = threadIdx.x; i < kSub * D; i += kRedBlock) acc[i] = 0.0f;
@@ -1349,7 +1389,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
 #pragma unroll
     for (int u = 0; u < kRedUnroll; ++u) {
       const u32 d = (u32)pr[u];
-      bool pending = pr[u] != ~0ull && ((d >> kSubShift) & (NSUB - 1)) == sub;
+      bool pending = pr[u] != ~0ull && (u64)d - lo < (u64)kSub;
       float t[PS];
       if (pending) load_row<PS>(f.rowv, (u32)(pr[u] >> 32), t);
       // Power-law keys: a hot key's records arrive many to a wave and would
@@ -1380,7 +1420,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
     }
   }
   __syncthreads();
-  const u64 d0 = ((u64)bucket << kRedShift) + ((u64)sub << kSubShift);
+  const u64 d0 = lo;
   for (u32 l = threadIdx.x; l < kSub; l += kRedBlock) {
     const u64 dest = d0 + l;
     float* g = f.grad + dest * PS;
@@ -1402,9 +1442,11 @@ static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
   u32* start = a.red_tot + a.red_nb + 1;
   hipLaunchKernelGGL(k_red_scatter<1>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
                      kMvmGroupRows, static_cast<const void*>(a.red_pairs), a.red_count,
-                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted));
-  const int grid = ((a.red_nb + 7) / 8) * 8 * mvm_nsub(D);
-  MvmRedFinal f{a.grad, a.wpull, a.red_rowv, a.S, a.red_nb};
+                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
+                     red_geom(a));
+  const int nsubt = mvm_nsub(D) * a.red_nsub;
+  const int grid = ((a.red_nb + 7) / 8) * 8 * nsubt;
+  MvmRedFinal f{a.grad, a.wpull, a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
   hipLaunchKernelGGL(k_mvm_red_sum<D>, dim3(grid), dim3(kRedBlock), 0, st,
                      reinterpret_cast<const u64*>(a.red_sorted), static_cast<const u32*>(start), f);
 }

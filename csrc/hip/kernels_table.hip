@@ -249,7 +249,8 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
 __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
     unsigned int* __restrict__ counts, int nb, unsigned long long* __restrict__ n_out,
     unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
-    u64 cap_alloc, unsigned long long* __restrict__ n_copy) {
+    u64 cap_alloc, unsigned long long* __restrict__ n_copy,
+    unsigned long long* __restrict__ cap_out) {
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
     int i = c0 + (int)threadIdx.x;
@@ -277,6 +278,7 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
         *claims = 0ull;
       }
     }
+    if (cap_out) *cap_out = ctl ? ctl[3] : cap_alloc;  // (the reduction's bucket geometry)
   }
 }
 
@@ -378,7 +380,7 @@ void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipSt
   hipLaunchKernelGGL(k_compact_count, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts);
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanBlock), 0, st, o.block_counts, g2,
                      reinterpret_cast<unsigned long long*>(o.n_uniq), s.claims, s.ctl, s.cap,
-                     reinterpret_cast<unsigned long long*>(o.n_uniq_copy));
+                     reinterpret_cast<unsigned long long*>(o.n_uniq_copy), o.cap_out);
   hipLaunchKernelGGL(k_compact_write, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts,
                      o.uniq_keys, o.uniq_pos, o.inv);
   XF_HIP_CHECK(hipGetLastError());
@@ -1003,7 +1005,8 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
     else hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else if (lr16) {
     hipLaunchKernelGGL(k_apply_lr16, dim3(grid), dim3(kBlock), 0, st, a);
-  } else if (a.pstride >= 2 && L.P <= kWave && !a.reset_pos) {
+  } else if ((a.pstride >= 2 || (L.P == 1 && a.nz_stash)) && L.P <= kWave && !a.reset_pos) {
+    // (LR with several slices and the pull's stash: one lane per key, packed)
     hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_apply_generic, dim3(grid), dim3(kBlock), 0, st, a);

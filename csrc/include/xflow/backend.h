@@ -73,6 +73,7 @@ struct DedupOut {
   u32* block_counts = nullptr; // [cap/4096 + 1] compaction workspace (HIP backend)
   u32* inv = nullptr;          // optional [cap]: unique-list index of each slot of the batch (HIP)
   int64_t* n_uniq_copy = nullptr;  // optional second destination of the unique count
+  unsigned long long* cap_out = nullptr;  // optional: the capacity this batch was deduplicated with
 };
 
 struct FwdArgs {
@@ -102,7 +103,15 @@ struct FwdArgs {
   u32* red_hist = nullptr;         // [red_nb][workgroups] pairs per (bucket, workgroup)
   u32* red_tot = nullptr;          // [red_nb + 1] pairs per bucket, then bucket starts
   u32* red_count = nullptr;        // [workgroups] pairs per workgroup
-  int red_nb = 0;                  // buckets = ceil(grad dests / 2^kRedShift)
+  int red_nb = 0;                  // buckets allocated (<= kRedMaxBuckets)
+  // This step's bucket width is decided on the device: dests = slot*S + s lie
+  // below red_bcap[0]*S (the scratch capacity the batch was deduplicated
+  // with, adaptive), and the shift is the smallest >= red_shift(NV) giving at
+  // most kRedMaxBuckets buckets; a bucket wider than the LDS accumulator is
+  // summed by several workgroups (red_nsub: the most that can be needed).
+  const unsigned long long* red_bcap = nullptr;
+  uint64_t red_cap = 0;            // allocated scratch capacity (upper bound)
+  int red_nsub = 1;
   // One slice: the bucket sums go straight to a unique-order (= send order in
   // the multi-rank step) buffer through the compaction's slot -> unique map,
   // instead of the slot-indexed grad (no gather, a dense apply read):

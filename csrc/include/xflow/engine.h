@@ -156,6 +156,7 @@ class Engine {
     u32* send_pos = nullptr;
     const u32* send_map = nullptr;
     bool inv_valid = false;
+    unsigned long long* bcap = nullptr;  // scratch capacity of the set's batch (device)
   };
   WorkerSet wset_[2];
   int cur_wb_ = 0;
@@ -218,6 +219,8 @@ class Engine {
   float* lr_nz_ = nullptr;       // LR-FTRL fused step: pulled (n, z) [max_nnz][2]
   float* fm_grad_ = nullptr;     // reference FM fused step: unique-order (B, C) [max_nnz][2]
   int red_nb_ = 0;
+  int red_nsub_ = 1;
+  unsigned long long* bcap_ = nullptr;  // current worker set's batch scratch capacity
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
   void set_reduction(FwdArgs& fa) const;

@@ -20,16 +20,17 @@ from xflow_amd.engine import Batch, Engine
 pytestmark = pytest.mark.gpu
 
 
-def _train(kind, dev, rows, small, steps_small, steps, v_dim=8, gpu_batches=None):
+def _train(kind, dev, rows, small, steps_small, steps, v_dim=8, gpu_batches=None, S=1):
     eng = Engine(ModelConfig(kind=kind, v_dim=v_dim), OptimConfig(),
-                 EngineConfig(table_log2_cap=23, max_rows=rows, max_nnz=rows * 39), device=dev)
+                 EngineConfig(table_log2_cap=23, max_rows=rows, max_nnz=rows * 39, max_slices=S),
+                 device=dev)
     caps = []
     # the CPU backend generates the (bit-identical) batches; the GPU trains on copies
     for i, r in enumerate([small] * steps_small + [rows] * (steps - steps_small)):
         b = gpu_batches[i]
         if dev.type == "cuda":
             b = Batch(keys=b.keys.to(dev), labels=b.labels.to(dev), nnz_per_row=b.nnz_per_row,
-                      field_major=True)
+                      field_major=True, slice_rows=b.slice_rows)
         eng.train_step(b)
         caps.append(eng.scratch_capacity())
     assert not eng.overflowed()
@@ -38,12 +39,12 @@ def _train(kind, dev, rows, small, steps_small, steps, v_dim=8, gpu_batches=None
     return keys, eng.pull(keys), caps, eng.read_stats()
 
 
-def _batches(rows, small, steps_small, steps):
+def _batches(rows, small, steps_small, steps, S=1):
     gen_eng = Engine(ModelConfig(), OptimConfig(),
                      EngineConfig(table_log2_cap=10, max_rows=rows, max_nnz=rows * 39))
     out = []
     for i, r in enumerate([small] * steps_small + [rows] * (steps - steps_small)):
-        g = SyntheticCriteo(gen_eng, r, SynthConfig(seed=11))
+        g = SyntheticCriteo(gen_eng, r, SynthConfig(seed=11), slice_rows=r // S)
         g.step = i
         b = g.alloc_batch()
         g.next(out=b)
@@ -51,22 +52,25 @@ def _batches(rows, small, steps_small, steps):
     return out
 
 
-@pytest.mark.parametrize("kind,rows,small,steps_small,steps",
-                         [("lr", 262144, 32768, 4, 22), ("fm", 65536, 8192, 3, 8)])
+@pytest.mark.parametrize("kind,rows,small,steps_small,steps,S",
+                         [("lr", 262144, 32768, 4, 22, 1), ("fm", 65536, 8192, 3, 8, 1),
+                          ("lr", 262144, 32768, 3, 10, 8), ("fm", 65536, 8192, 2, 6, 4)])
 def test_bench_scale_deterministic_and_matches_cpu(gpu_device, kind, rows, small, steps_small,
-                                                   steps):
-    batches = _batches(rows, small, steps_small, steps)
+                                                   steps, S):
+    """S > 1: the reference's Hogwild slices (lr_worker.cc:190-199) at bench
+    scale stay on the atomic-free fixed-point reduction."""
+    batches = _batches(rows, small, steps_small, steps, S)
     k1, w1, caps1, st1 = _train(kind, gpu_device, rows, small, steps_small, steps,
-                                gpu_batches=batches)
+                                gpu_batches=batches, S=S)
     k2, w2, caps2, _ = _train(kind, gpu_device, rows, small, steps_small, steps,
-                              gpu_batches=batches)
+                              gpu_batches=batches, S=S)
     # the adaptive scratch grew on the device when the batches got larger
     assert caps1[steps_small] > caps1[0], caps1
     assert caps1 == caps2
     np.testing.assert_array_equal(k1, k2)
     np.testing.assert_array_equal(w1.view(np.uint32), w2.view(np.uint32))  # bitwise
     kc, wc, _, stc = _train(kind, torch.device("cpu"), rows, small, steps_small, steps,
-                            gpu_batches=batches)
+                            gpu_batches=batches, S=S)
     np.testing.assert_array_equal(k1, kc)
     np.testing.assert_allclose(w1, wc, rtol=1e-4, atol=1e-6)
     assert st1["rows"] == stc["rows"]
