@@ -149,7 +149,8 @@ Engine::~Engine() {
                   srv_slots_[0], srv_slots_[1], srv_nz_[0], srv_nz_[1], host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, own_pos_[0],
-                  own_pos_[1], own_idx_[0], own_idx_[1], srv_w_[0], srv_w_[1], fm_grad_};
+                  own_pos_[1], own_idx_[0], own_idx_[1], srv_w_[0], srv_w_[1], fm_grad_,
+                  lr_mask_};
   for (void* p : ptrs) be.free(p);
   for (StageSet& a : aset_) {
     void* ap[] = {a.keys, a.rowptr, a.fgid, a.labels};
@@ -192,6 +193,14 @@ void Engine::use_worker_set(int wb) {
   inv_valid_ = w.inv_valid;
   bcap_ = w.bcap;
   cur_wb_ = wb;
+}
+
+// The GPU reduction path sees every (key, slice) that occurs (a record per
+// column-table entry), so it can write the slice bits: LR and reference FM.
+bool Engine::reduction_masks() const {
+  return red_pairs_ && (double)scratch_.cap * cfg_.max_slices * pstride() < 4294967295.0 &&
+         (cfg_.model.kind == kLR ||
+          (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference));
 }
 
 void Engine::set_reduction(FwdArgs& fa) const {
@@ -282,23 +291,24 @@ void Engine::train_step(const BatchView& b) {
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
-  // LR-FTRL on 16-byte slots, one slice, bucket reduction: the reduction
-  // writes normalised gradients in unique order (through the compaction's
-  // slot -> unique index map) and the apply takes (n, z) from the pull, so it
-  // reads nothing at random and writes the slot once.
+  // LR-FTRL on 16-byte slots, bucket reduction: the reduction writes
+  // normalised gradients in unique order (through the compaction's slot ->
+  // unique index map; S > 1: [unique][slice] plus the slice bits) and the
+  // apply takes (n, z) from the pull, so it reads nothing at random and
+  // writes the slot once.
   const TableLayout& L = table_.L;
   const bool lr16_layout_ok = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 &&
                               L.P == 1 && L.opt == kFTRL && !L.has_flag && red_pairs_ &&
                               (double)scratch_.cap < 4294967295.0 && !lr16_disabled();
-  const bool lr16 = lr16_layout_ok && S == 1;
-  // several slices: slot-indexed sums, ordered per-slice pushes (packed
-  // apply), but still the pull-time (n, z) stash
-  const bool lr16s = lr16_layout_ok && S > 1;
+  const bool lr16 = lr16_layout_ok && (S == 1 || (masks && reduction_masks()));
+  // summed slices: slot-indexed sums (packed apply), still the (n, z) stash
+  const bool lr16s = lr16_layout_ok && S > 1 && !lr16;
   if (lr16s && !lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   if (lr16) {
     ensure_inv();
-    if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz);
+    if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * cfg_.max_slices);
     if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
+    if (S > 1 && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
   }
   // reference FM, one slice: the (B, C) sums land in unique order (dense apply read)
   const bool fmu = fm_vals_ && S == 1;
@@ -323,7 +333,8 @@ void Engine::train_step(const BatchView& b) {
   pa.fm_vals = fm_vals_;
   if (lr16) {
     pa.out_nz = lr_nz_;
-    pa.zero_out = lr_grad_;
+    // S > 1: only a key's present slices are read, so only its bits need clearing
+    pa.zero_out = S == 1 ? lr_grad_ : reinterpret_cast<float*>(lr_mask_);
   }
   if (lr16s) pa.out_nz = lr_nz_;
   if (fmu) {
@@ -331,8 +342,6 @@ void Engine::train_step(const BatchView& b) {
     pa.zero_width = 2;
   }
   be_->table_pull(pa);
-
-  if (masks) be_->slice_masks(b, pos_, tmask_);
 
   FwdArgs fa;
   fa.batch = b;
@@ -344,6 +353,10 @@ void Engine::train_step(const BatchView& b) {
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
+  // slice bits from the reduction (LR / reference FM), else per occurrence
+  if (masks && lr16) fa.red_masks = lr_mask_;
+  else if (masks && reduction_masks()) fa.red_masks = tmask_;
+  else if (masks) be_->slice_masks(b, pos_, tmask_);
   // reference-math FM on the GPU reduction path: (B, C) rows, expanded by the apply
   fa.fm_compact = fa.red_pairs && fa.agg_ok && cfg_.model.kind == kFM &&
                   cfg_.model.fm_math == kFmReference;
@@ -385,6 +398,8 @@ void Engine::train_step(const BatchView& b) {
     aa.zero_after = false;
     aa.slice_rows = nullptr;
     aa.nz_stash = lr_nz_;
+    aa.masks = S > 1 ? lr_mask_ : nullptr;
+    aa.masks_rw = nullptr;
   }
   if (lr16s) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
   if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
@@ -713,7 +728,6 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   // the direct path's send buffer is zeroed by the scatter
   be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, vstride_,
                     direct ? grads_out : nullptr, grad_width());
-  if (masks) be_->slice_masks(b, pos_, tmask_);
   FwdArgs fa;
   fa.batch = b;
   fa.pos = pos_;
@@ -724,6 +738,8 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   set_reduction(fa);
+  if (masks && reduction_masks()) fa.red_masks = tmask_;
+  else if (masks) be_->slice_masks(b, pos_, tmask_);
   fa.fm_compact = sharded_fm_compact() && fa.agg_ok;
   fa.fm_vals = fm_vals_;
   if (sharded_fm_compact() && !fa.fm_compact)

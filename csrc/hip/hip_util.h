@@ -52,6 +52,20 @@ inline int grid_for(int64_t n, int block = kBlock, int cap = kMaxGrid) {
   return (int)(g < cap ? g : cap);
 }
 
+// Compute units of the current device (cached per device id).
+inline int device_cus() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Wave-aggregated append: every lane with `pred` gets a unique index from one

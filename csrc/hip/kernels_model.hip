@@ -37,10 +37,22 @@ struct RedGeom {
     while (((dests + (1ull << sh) - 1) >> sh) > (u64)kRedMaxBuckets) ++sh;
     return sh;
   }
+  // buckets this step's dests reach (of the nb allocated for the full
+  // capacity): producers, scans and sums skip the rest
+  __device__ __forceinline__ int active(int shift, int nb) const {
+    const u64 dests = (bcap ? (u64)*bcap : cap) * (u64)S;
+    const u64 n = (dests + (1ull << shift) - 1) >> shift;
+    return n < (u64)nb ? (int)n : nb;
+  }
 };
 
 __host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
   return RedGeom{a.red_bcap, a.red_cap, a.S};
+}
+
+__device__ __forceinline__ int red_active(const FwdArgs& a, int base) {
+  const RedGeom g = red_geom(a);
+  return g.active(g.shift(base), a.red_nb);
 }
 
 // Per-row loss statistics, reduced per workgroup then one f64 atomic each.
@@ -318,7 +330,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
     // (published to the other waves by the barrier below)
     const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
     lagg.region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
-    lagg.init(a.red_nb);
+    lagg.init(red_active(a, red_shift(1)));
     lagg.shift = red_geom(a).shift(red_shift(1));
   }
   // block-uniform longest row: selects the register path and bounds the
@@ -407,7 +419,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   if constexpr (kRed) {
     __syncthreads();
     if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
-    for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+    for (int i = threadIdx.x, n = red_active(a, red_shift(1)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
   flush_stats<BLOCK>(st, a.stats);
@@ -551,7 +563,9 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
 //   3. k_red_sum      per bucket: LDS sums, one plain store per non-zero dest
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_red_scan(u32* __restrict__ hist, int groups,
-                                                     u32* __restrict__ tot) {
+                                                     u32* __restrict__ tot, RedGeom geom,
+                                                     int base) {
+  if ((int)blockIdx.x >= geom.active(geom.shift(base), (int)gridDim.x)) return;
   const size_t row = (size_t)blockIdx.x * groups;
   u32 carry = 0;
   for (int c0 = 0; c0 < groups; c0 += kBlock) {
@@ -593,6 +607,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows
   const int kShift = geom.shift(red_shift(NV));
   __shared__ u32 cur[kRedMaxBuckets];
   const int g = blockIdx.x, groups = gridDim.x;
+  nb = geom.active(kShift, nb);
   u32 carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kRedBlock) {
     const int i = c0 + (int)threadIdx.x;
@@ -644,81 +659,145 @@ struct RedFinal {
   const u32* inv;
   const int32_t* rows;
   bool compact;        // NV == 2: store (B, C) only (FwdArgs::fm_compact)
+  u32* masks;          // slice-presence bits (FwdArgs::red_masks; unique order with out), or null
 };
 
+// Slice bits of one slot from the presence bitmap: its dests slot*S + s that
+// fall in [lo, lo + kR).
+template <u32 kR>
+__device__ __forceinline__ u32 slot_bits(const u32* pbits, u64 slot, u64 S, u64 lo) {
+  u32 bits = 0;
+  for (u64 s = 0; s < S; ++s) {
+    const u64 d = slot * S + s;
+    if (d >= lo && d < lo + kR && ((pbits[(d - lo) >> 5] >> ((d - lo) & 31)) & 1u))
+      bits |= 1u << s;
+  }
+  return bits;
+}
+
+// A bucket's sums are either initialised and written densely (all kR dests)
+// or per record: with the 8x-headroom dedup scratch and S slices, a bucket's
+// dests are mostly untouched (S = 8 at bench shape: ~700 records over 16384
+// dests), and the dense passes cost more than three passes over the records.
+// One (bucket, sub) unit of k_red_sum: records [beg, end) of bucket b, dests
+// [lo, lo + kR).  Barriers are LDS-only: a unit's global stores need not land
+// before the next unit starts.
 template <int NV>
-__global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ sorted,
-                                                       const u32* __restrict__ start, RedFinal f,
-                                                       RedGeom geom, int nb) {
+__device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
+                                             const void* __restrict__ sorted, const RedFinal& f,
+                                             long long* acc, u32* pbits, u32* cbits) {
   using T = typename RedRec<NV>::T;
   constexpr int kShift = red_shift(NV);
   constexpr u32 kR = 1u << kShift;
   constexpr int kFx = FxBits<NV>::kFx;
-  // workgroup (bucket, sub): a bucket of 2^shift dests is summed by 2^(shift -
-  // kShift) workgroups of kR dests each (one in the common case)
-  const int b = (int)(blockIdx.x % (unsigned)nb), sub = (int)(blockIdx.x / (unsigned)nb);
-  const int shift = geom.shift(kShift);
-  if (sub >= (1 << (shift - kShift))) return;
-  const u64 lo = ((u64)b << shift) + ((u64)sub << kShift);
-  // fixed-point accumulators: the bucket's sums do not depend on record order
-  __shared__ long long acc[kR * NV];
-  const u32 beg = start[b], end = start[b + 1];
   if (beg == end) return;
-  for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
-  __syncthreads();
+  // sparse units hold their records in registers across the three phases
+  constexpr int kSp = 2 * kRedUnroll;
+  const bool dense = end - beg > (u32)(kSp * kRedBlock);  // (block-uniform)
   const T* src = static_cast<const T*>(sorted);
-  for (u32 i0 = beg + threadIdx.x; i0 < end; i0 += kRedUnroll * kRedBlock) {
-    T pr[kRedUnroll];
-#pragma unroll
-    for (int q = 0; q < kRedUnroll; ++q) {
-      const u32 i = i0 + (u32)q * kRedBlock;
-      if (i < end) pr[q] = src[i];
-    }
-#pragma unroll
-    for (int q = 0; q < kRedUnroll; ++q) {
-      if (i0 + (u32)q * kRedBlock >= end) continue;
-      const u64 l = (u64)RedRec<NV>::dest(pr[q]) - lo;
-      if (l >= kR) continue;  // another sub-bucket's dest
-      if constexpr (NV == 1) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l]),
-                  (unsigned long long)fx_from<kFx>(__uint_as_float((u32)(pr[q] >> 32))));
-      } else {
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2]),
-                  (unsigned long long)fx_from<kFx>(__uint_as_float(pr[q].y)));
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2 + 1]),
-                  (unsigned long long)fx_from<kFx>(__uint_as_float(pr[q].z)));
-      }
-    }
-  }
-  __syncthreads();
-  const u64 d0 = lo;
-  if constexpr (NV == 1) {
-    if (f.out) {
-      // normalised like the gather would (lr_worker.cc:116-118, in double)
-      const double rows = (double)f.rows[0];
-      for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-        const long long a = acc[i];
-        if (a == 0) continue;
-        const u32 o = f.inv[d0 + i];
-        if (o != 0xFFFFFFFFu) f.out[o] = (float)(fx_to_double<kFx>(a) / rows);  // (not the trash slot)
-      }
+  const u64 S = (u64)f.S;
+  auto add = [&](const T& r, u32 l) {
+    if (f.masks) atomicOr(&pbits[l >> 5], 1u << (l & 31));
+    if constexpr (NV == 1) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l]),
+                (unsigned long long)fx_from<kFx>(__uint_as_float((u32)(r >> 32))));
     } else {
-      float* g = f.grad + d0;
-      for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-        const long long a = acc[i];
-        if (a != 0) g[i] = (float)fx_to_double<kFx>(a);  // grad is zero outside this step's keys
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2]),
+                (unsigned long long)fx_from<kFx>(__uint_as_float(r.y)));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[l * 2 + 1]),
+                (unsigned long long)fx_from<kFx>(__uint_as_float(r.z)));
+    }
+  };
+  T pr[kSp];
+  u32 lr[kSp];  // (sparse) the record's local dest, kR: none
+  if (dense) {
+    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
+    if (f.masks)
+      for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) pbits[i] = 0u;
+    lds_barrier();
+    for (u32 i0 = beg + threadIdx.x; i0 < end; i0 += kRedUnroll * kRedBlock) {
+#pragma unroll
+      for (int q = 0; q < kRedUnroll; ++q) {
+        const u32 i = i0 + (u32)q * kRedBlock;
+        if (i < end) pr[q] = src[i];
+      }
+#pragma unroll
+      for (int q = 0; q < kRedUnroll; ++q) {
+        if (i0 + (u32)q * kRedBlock >= end) continue;
+        const u64 l = (u64)RedRec<NV>::dest(pr[q]) - lo;
+        if (l < kR) add(pr[q], (u32)l);  // (else another sub-bucket's dest)
       }
     }
   } else {
-    for (u32 i = threadIdx.x; i < kR; i += kRedBlock) {
-      if (acc[2 * i] == 0 && acc[2 * i + 1] == 0) continue;
-      const float B = (float)fx_to_double<kFx>(acc[2 * i]);
-      const float C = (float)fx_to_double<kFx>(acc[2 * i + 1]);
-      const u64 dest = d0 + i;
+#pragma unroll
+    for (int q = 0; q < kSp; ++q) {
+      const u32 i = beg + threadIdx.x + (u32)q * kRedBlock;
+      lr[q] = kR;
+      if (i < end) {
+        pr[q] = src[i];
+        const u64 l = (u64)RedRec<NV>::dest(pr[q]) - lo;
+        if (l < kR) lr[q] = (u32)l;
+      }
+    }
+    // zero what the records touch (same-value plain stores), and for the
+    // masks every bitmap word their slots' dests cover
+#pragma unroll
+    for (int q = 0; q < kSp; ++q) {
+      const u32 l = lr[q];
+      if (l >= kR) continue;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[(u64)l * NV + v] = 0ll;
+      cbits[l >> 5] = 0u;
+      if (f.masks) {
+        const u64 d0 = ((lo + l) / S) * S;
+        const u64 a0 = d0 > lo ? d0 - lo : 0, a1 = d0 + S - 1 - lo;
+        pbits[a0 >> 5] = 0u;
+        if (a1 < kR) pbits[a1 >> 5] = 0u;
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < kSp; ++q)
+      if (lr[q] < kR) add(pr[q], lr[q]);
+  }
+  lds_barrier();
+  // slice bits of a slot: one plain store per slot inside [lo, lo + kR), an
+  // atomic OR for a slot that straddles its edge (S not dividing kR)
+  auto put_mask = [&](u64 slot, u32 bits) {
+    u64 m = slot;
+    if (f.out) {  // (NV == 1, S > 1) unique order
+      m = f.inv[slot];
+      if (m == 0xFFFFFFFFu) return;
+    }
+    if (slot * S >= lo && slot * S + S <= lo + kR) f.masks[m] = bits;
+    else atomicOr(&f.masks[m], bits);
+  };
+  // the sum of dest lo + l (skipped when zero: grad is zero outside this
+  // step's keys -- except a present slice of the unique-order S > 1 output,
+  // which the apply reads by its slice bit)
+  auto emit = [&](u32 l, bool present) {
+    const u64 dest = lo + l;
+    if constexpr (NV == 1) {
+      const long long a = acc[l];
+      if (a == 0 && !(present && f.out && S > 1)) return;
+      if (f.out) {
+        // normalised like the gather would (lr_worker.cc:116-118, in double);
+        // S > 1: [unique][slice], per-slice rows
+        const u64 slot = dest / S, sl = dest - slot * S;
+        const u32 o = f.inv[slot];
+        if (o != 0xFFFFFFFFu)  // (not the trash slot)
+          f.out[(u64)o * S + sl] = (float)(fx_to_double<kFx>(a) / (double)f.rows[sl]);
+      } else {
+        f.grad[dest] = (float)fx_to_double<kFx>(a);
+      }
+    } else {
+      if (acc[2 * l] == 0 && acc[2 * l + 1] == 0) return;
+      const float B = (float)fx_to_double<kFx>(acc[2 * l]);
+      const float C = (float)fx_to_double<kFx>(acc[2 * l + 1]);
       if (f.compact) {  // expanded by the apply (k_apply_group)
         if (f.out) {    // one slice: unique (send) order
           const u32 o = f.inv[dest];
-          if (o == 0xFFFFFFFFu) continue;
+          if (o == 0xFFFFFFFFu) return;
           if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
             const double rows = (double)f.rows[0];
             reinterpret_cast<float2*>(f.out)[o] =
@@ -729,10 +808,10 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
         } else {
           *reinterpret_cast<float2*>(f.grad + dest * f.ps) = make_float2(B, C);
         }
-        continue;
+        return;
       }
       // rows are padded to 16 B: dwordx4 loads of v and stores of the row
-      const float4* v4 = reinterpret_cast<const float4*>(f.wpull + (dest / (u64)f.S) * f.ps);
+      const float4* v4 = reinterpret_cast<const float4*>(f.wpull + (dest / S) * f.ps);
       float4* g4 = reinterpret_cast<float4*>(f.grad + dest * f.ps);
       for (int q = 0; q < f.ps / 4; ++q) {
         const float4 v = v4[q];
@@ -745,23 +824,87 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
         g4[q] = make_float4(o[0], o[1], o[2], o[3]);
       }
     }
+  };
+  if (dense) {
+    for (u32 l = threadIdx.x; l < kR; l += kRedBlock)
+      emit(l, f.masks && ((pbits[l >> 5] >> (l & 31)) & 1u));
+    if (f.masks) {
+      const u64 s0 = lo / S, s1 = (lo + kR + S - 1) / S;
+      for (u64 slot = s0 + threadIdx.x; slot < s1; slot += kRedBlock) {
+        const u32 bits = slot_bits<kR>(pbits, slot, S, lo);
+        if (bits) put_mask(slot, bits);
+      }
+    }
+  } else {
+    // one writer per dest (the record that claims its bit), and per slot the
+    // writer of its lowest present dest
+#pragma unroll
+    for (int q = 0; q < kSp; ++q) {
+      const u32 l = lr[q];
+      if (l >= kR) continue;
+      const u32 bit = 1u << (l & 31);
+      if (atomicOr(&cbits[l >> 5], bit) & bit) continue;
+      emit(l, true);
+      if (f.masks) {
+        const u64 slot = (lo + l) / S;
+        const u32 bits = slot_bits<kR>(pbits, slot, S, lo);
+        if (slot * S + (u64)__ffs(bits) - 1 == lo + l) put_mask(slot, bits);
+      }
+    }
+  }
+}
+
+// A persistent grid (one workgroup per CU: the accumulator fills the LDS)
+// walks this step's (bucket, sub) units -- a bucket of 2^shift dests is
+// summed in 2^(shift - kShift) units of kR dests (one in the common case) --
+// so the sparse units of a many-slice step do not each pay a workgroup
+// launch; the next unit's record range is loaded during the current one.
+template <int NV>
+__global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ sorted,
+                                                       const u32* __restrict__ start, RedFinal f,
+                                                       RedGeom geom, int nb) {
+  constexpr int kShift = red_shift(NV);
+  constexpr u32 kR = 1u << kShift;
+  // fixed-point accumulators: the bucket's sums do not depend on record order
+  __shared__ long long acc[kR * NV];
+  __shared__ u32 pbits[kR / 32];  // (f.masks) dests some record reached
+  __shared__ u32 cbits[kR / 32];  // (sparse) dests whose sum is being stored
+  const int shift = geom.shift(kShift);
+  const u32 act = (u32)geom.active(shift, nb);
+  const u32 units = act << (shift - kShift);
+  u32 id = blockIdx.x, nbeg = 0, nend = 0;
+  if (id < units) {
+    nbeg = start[id % act];
+    nend = start[id % act + 1];
+  }
+  for (; id < units; id += gridDim.x) {
+    const u32 beg = nbeg, end = nend, b = id % act, sub = id / act;
+    const u32 nid = id + gridDim.x;
+    if (nid < units) {
+      nbeg = start[nid % act];
+      nend = start[nid % act + 1];
+    }
+    const u64 lo = ((u64)b << shift) + ((u64)sub << kShift);
+    red_sum_unit<NV>(lo, beg, end, sorted, f, acc, pbits, cbits);
+    lds_barrier();  // the next unit reinitialises what this one read
   }
 }
 
 template <int NV>
 static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, hipStream_t st) {
   hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
-                     a.red_tot);
+                     a.red_tot, red_geom(a), red_shift(NV));
   u32* start = a.red_tot + a.red_nb + 1;
   hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
                      rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
                      red_geom(a));
-  if (a.red_out && (a.S != 1 || (NV == 2 && !a.fm_compact)))
-    throw std::runtime_error("red_out: one slice (and compact rows for FM) only");
+  if (a.red_out && (NV == 2 ? (a.S != 1 || !a.fm_compact) : (a.S != 1 && !a.red_masks)))
+    throw std::runtime_error("red_out: one slice or slice bits (LR), compact rows (FM)");
   RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim, a.red_out, a.red_inv,
-             a.red_rows, NV == 2 && a.fm_compact};
-  hipLaunchKernelGGL(k_red_sum<NV>, dim3(a.red_nb * a.red_nsub), dim3(kRedBlock), 0, st,
+             a.red_rows, NV == 2 && a.fm_compact, a.S > 1 ? a.red_masks : nullptr};
+  const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
+  hipLaunchKernelGGL(k_red_sum<NV>, dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, f, red_geom(a), a.red_nb);
 }
 
@@ -793,7 +936,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
                                        (b.row_ptr ? (int64_t)b.row_ptr[r0]
                                                   : r0 * b.nnz_per_row));
   ListAgg<LOG2, 2> lagg{s_tag64, s_acc, s_list, s_nlist, s_hist, region, 0u};
-  lagg.init(a.red_nb);
+  lagg.init(red_active(a, red_shift(2)));
   lagg.shift = red_geom(a).shift(red_shift(2));
   int maxlen;
   if (!b.row_ptr) {
@@ -849,7 +992,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
-  for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+  for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
     a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   flush_stats<BLOCK>(st, a.stats);
 }
@@ -885,7 +1028,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
   if constexpr (kGrad) {
     lagg.region = reinterpret_cast<u64*>(reinterpret_cast<uint4*>(a.red_pairs) +
                                          (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row));
-    lagg.init(a.red_nb);
+    lagg.init(red_active(a, red_shift(2)));
     lagg.shift = red_geom(a).shift(red_shift(2));
     if (!b.row_ptr) {
       maxlen = b.nnz_per_row;
@@ -936,7 +1079,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
     }
     __syncthreads();
     if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
-    for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+    for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
   flush_stats<BLOCK>(st, a.stats);
@@ -1035,6 +1178,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool red = agg && a.model.fm_math == kFmReference && a.red_pairs && a.red_nb > 0 &&
                    a.red_nb <= kRedMaxBuckets;
   if (a.fm_compact && !red) throw std::runtime_error("fm_compact needs the FM reduction path");
+  if (a.red_masks && a.S > 1 && !red) throw std::runtime_error("red_masks need the FM reduction path");
   if (!kGrad && a.model.fm_math == kFmStandard && a.model.fm_mfma) {
     const int g = (int)((a.batch.rows + 63) / 64);  // 4 waves x 16 rows
     switch (a.model.v_dim) {
@@ -1128,7 +1272,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
   __shared__ u32 s_hist[kRed ? kRedMaxBuckets : 1];
   __shared__ u32 s_cnt;
   if constexpr (kRed) {  // published by the barrier before the record loop
-    for (int i = threadIdx.x; i < a.red_nb; i += BLOCK) s_hist[i] = 0u;
+    for (int i = threadIdx.x, n = red_active(a, kRedShift); i < n; i += BLOCK) s_hist[i] = 0u;
     if (threadIdx.x == 0) s_cnt = 0u;
   }
   const BatchView& b = a.batch;
@@ -1295,7 +1439,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
       }
       __syncthreads();
       if (threadIdx.x == 0) a.red_count[blockIdx.x] = s_cnt;
-      for (int i = threadIdx.x; i < a.red_nb; i += BLOCK)
+      for (int i = threadIdx.x, n = red_active(a, kRedShift); i < n; i += BLOCK)
         a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
     } else if constexpr (!kAgg) {
       for (int j = 0; j < len; ++j) {
@@ -1371,7 +1515,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
   if (bucket >= f.nb) return;
   // a bucket of 2^shift dests (RedGeom) has NSUB << (shift - kRedShift) subs
   const int shift = f.geom.shift(kRedShift);
-  if (sub >= ((u32)NSUB << (shift - kRedShift))) return;
+  if (sub >= ((u32)NSUB << (shift - kRedShift)) || bucket >= f.geom.active(shift, f.nb)) return;
   const u64 lo = ((u64)bucket << shift) + ((u64)sub << kSubShift);
   const u32 beg = start[bucket], end = start[bucket + 1];
   if (beg == end) return;
@@ -1438,7 +1582,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
 template <int D>
 static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
   hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
-                     a.red_tot);
+                     a.red_tot, red_geom(a), kRedShift);
   u32* start = a.red_tot + a.red_nb + 1;
   hipLaunchKernelGGL(k_red_scatter<1>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
                      kMvmGroupRows, static_cast<const void*>(a.red_pairs), a.red_count,
@@ -1492,8 +1636,10 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
       int g = (int)((a.batch.rows + kLrBlock - 1) / kLrBlock);
       const bool red = grad && a.agg_ok && a.red_pairs && a.red_nb > 0 &&
                        a.red_nb <= kRedMaxBuckets;
-      if (a.red_out && !(red && a.S == 1))
-        throw std::runtime_error("red_out needs the one-slice LR bucket reduction");
+      if (a.red_out && !(red && (a.S == 1 || a.red_masks)))
+        throw std::runtime_error("red_out needs the LR bucket reduction (S > 1: with slice bits)");
+      if (a.red_masks && a.S > 1 && !red)
+        throw std::runtime_error("red_masks need the LR bucket reduction");
       if (red) {
         constexpr int R = kLrGroupRows;
         const int gr = (int)((a.batch.rows + R - 1) / R);

@@ -748,24 +748,39 @@ __device__ __forceinline__ float norm_grad(float raw, const int32_t* slice_rows,
 // One key per lane, grid-stride: measured faster than issuing four keys per
 // lane up front (54 vs 49 us for 850 K keys) -- twice the waves in flight hide
 // the dependent slot -> state chain better than per-lane ILP.
+template <bool kSlices>
 __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
   int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const FtrlParams fp = a.opt.ftrl;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     u32 slot = a.slots[i];
-    u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
-    float raw = a.grads[row];
-    if (a.zero_after) a.grads[row] = 0.0f;
-    if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
-    if (slot == kNoSlot) continue;
-    float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
-    // (n, z) as pulled this step: coalesced, instead of a second random read
-    float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
-    float w = ftrl_weight(nz.y, nz.x, fp);
-    float g = norm_grad(raw, a.slice_rows, 0);
-    ftrl_push(nz.x, nz.y, w, g, fp);
-    *st = nz;
+    if constexpr (kSlices) {
+      // unique-order [key][slice] normalised sums: the present slices' pushes
+      // in slice order (the CPU backend's Hogwild order)
+      if (slot == kNoSlot) continue;
+      float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
+      float2 nz = reinterpret_cast<const float2*>(a.nz_stash)[i];
+      const float* g = a.grads + (size_t)i * a.S;
+      for (u32 m = a.masks[i]; m; m &= m - 1) {
+        const float w = ftrl_weight(nz.y, nz.x, fp);
+        ftrl_push(nz.x, nz.y, w, g[__ffs(m) - 1], fp);
+      }
+      *st = nz;
+    } else {
+      u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+      float raw = a.grads[row];
+      if (a.zero_after) a.grads[row] = 0.0f;
+      if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
+      if (slot == kNoSlot) continue;
+      float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
+      // (n, z) as pulled this step: coalesced, instead of a second random read
+      float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
+      float w = ftrl_weight(nz.y, nz.x, fp);
+      float g = norm_grad(raw, a.slice_rows, 0);
+      ftrl_push(nz.x, nz.y, w, g, fp);
+      *st = nz;
+    }
   }
 }
 
@@ -997,14 +1012,21 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   const TableLayout& L = a.table.L;
   int grid = grid_for(a.n_dev ? a.n_max : a.n_host);
   const int64_t nm = a.n_dev ? a.n_max : a.n_host;
-  const bool lr16 = L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag && a.S == 1 &&
-                    !a.masks && a.pstride == 1;
+  const bool lr16_slot = L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag &&
+                         a.pstride == 1;
+  const bool lr16 = lr16_slot && a.S == 1 && !a.masks;
+  // S > 1 on unique-order sums and slice bits (Engine::train_step's fused LR step)
+  const bool lr16_slices = lr16_slot && a.S > 1 && a.masks && !a.masks_rw && !a.grad_map &&
+                           !a.zero_after && !a.reset_pos && a.nz_stash && !a.sum_slices &&
+                           !a.slice_rows && !a.grp.oidx;
   if (a.grp.oidx) {
     if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");
     if (lr16) hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);
     else hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else if (lr16) {
-    hipLaunchKernelGGL(k_apply_lr16, dim3(grid), dim3(kBlock), 0, st, a);
+    hipLaunchKernelGGL(k_apply_lr16<false>, dim3(grid), dim3(kBlock), 0, st, a);
+  } else if (lr16_slices) {
+    hipLaunchKernelGGL(k_apply_lr16<true>, dim3(grid), dim3(kBlock), 0, st, a);
   } else if ((a.pstride >= 2 || (L.P == 1 && a.nz_stash)) && L.P <= kWave && !a.reset_pos) {
     // (LR with several slices and the pull's stash: one lane per key, packed)
     hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);

@@ -112,6 +112,10 @@ struct FwdArgs {
   const unsigned long long* red_bcap = nullptr;
   uint64_t red_cap = 0;            // allocated scratch capacity (upper bound)
   int red_nsub = 1;
+  // S > 1: the reduction also writes each slot's slice-presence bits
+  // (red_masks[slot] |= 1 << s for every (key, slice) with an occurrence),
+  // replacing one global atomic per occurrence (slice_masks) on hot keys
+  u32* red_masks = nullptr;
   // One slice: the bucket sums go straight to a unique-order (= send order in
   // the multi-rank step) buffer through the compaction's slot -> unique map,
   // instead of the slot-indexed grad (no gather, a dense apply read):

@@ -215,8 +215,9 @@ class Engine {
   u32* red_tot_ = nullptr;
   u32* red_count_ = nullptr;
   float* red_rowv_ = nullptr;    // MVM: per-row loss*M (FwdArgs::red_rowv)
-  float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz]
+  float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz][max_slices]
   float* lr_nz_ = nullptr;       // LR-FTRL fused step: pulled (n, z) [max_nnz][2]
+  u32* lr_mask_ = nullptr;       // LR-FTRL fused step, S > 1: unique-order slice bits [max_nnz]
   float* fm_grad_ = nullptr;     // reference FM fused step: unique-order (B, C) [max_nnz][2]
   int red_nb_ = 0;
   int red_nsub_ = 1;
@@ -224,6 +225,7 @@ class Engine {
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
   void set_reduction(FwdArgs& fa) const;
+  bool reduction_masks() const;
   void ensure_inv();
   LossStats* stats_ = nullptr;  // [1]
   u32* send_pos_ = nullptr;     // [max_nnz]
