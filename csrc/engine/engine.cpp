@@ -64,8 +64,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   scratch_.epoch = 0;
   if (be.is_gpu()) {
     // adaptive active capacity (ScratchView::ctl): starts at the allocation
-    scratch_.ctl = balloc<unsigned long long>(be, 4);
-    unsigned long long c0[4] = {scratch_.cap, 0ull, 0ull, 0ull};
+    scratch_.ctl = balloc<unsigned long long>(be, 5);
+    unsigned long long c0[5] = {scratch_.cap, 0ull, 0ull, 0ull, 0ull};
     be.copy_h2d(scratch_.ctl, c0, sizeof(c0));
   }
   block_counts_ = balloc<u32>(be, scratch_.cap / 4096 + 1);
@@ -263,6 +263,10 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
   }
   // (n_uniq is written, not accumulated, by both backends' dedup)
   if (++scratch_.epoch == 0) scratch_.epoch = 1;  // 0 marks never-stamped slots
+  scratch_.grow = 0.0f;
+  if (scratch_.ctl && nnz_seen_ > 0 && b.nnz > nnz_seen_)
+    scratch_.grow = (float)((double)b.nnz / (double)nnz_seen_);
+  if (b.nnz > nnz_seen_) nnz_seen_ = b.nnz;
   DedupOut o;
   o.pos = pos_;
   o.uniq_keys = uniq_keys_out ? uniq_keys_out : uniq_keys_;

@@ -676,9 +676,11 @@ __device__ __forceinline__ u32 slot_bits(const u32* pbits, u64 slot, u64 S, u64 
 }
 
 // A bucket's sums are either initialised and written densely (all kR dests)
-// or per record: with the 8x-headroom dedup scratch and S slices, a bucket's
-// dests are mostly untouched (S = 8 at bench shape: ~700 records over 16384
-// dests), and the dense passes cost more than three passes over the records.
+// or per record: with the 4x-headroom dedup scratch and S slices, a bucket's
+// dests are mostly untouched (S = 8 at bench shape: ~1500 records over 16384
+// dests), and the dense passes cost more than the per-record phases on
+// register-held records.
+//
 // One (bucket, sub) unit of k_red_sum: records [beg, end) of bucket b, dests
 // [lo, lo + kR).  Barriers are LDS-only: a unit's global stores need not land
 // before the next unit starts.

@@ -54,6 +54,11 @@ __device__ __forceinline__ u64 batch_cap(const ScratchView& sv) {
   return sv.ctl ? (u64)sv.ctl[3] : sv.cap;
 }
 
+// this batch spilled past the active capacity (ScratchView::ctl[4])
+__device__ __forceinline__ bool batch_spilled(const ScratchView& sv) {
+  return sv.ctl && sv.ctl[4] == (unsigned long long)sv.epoch;
+}
+
 __global__ void k_scratch_maybe_clear(u64* __restrict__ skeys, u64 cap,
                                       const unsigned long long* __restrict__ claims,
                                       u64 rebuild_at, const unsigned long long* __restrict__ ctl) {
@@ -80,6 +85,16 @@ __global__ void k_scratch_claims_reset(unsigned long long* claims, u64 rebuild_a
   } else if (*claims > rebuild_at) {
     *claims = 0ull;
   }
+}
+
+// ScratchView::grow: rebuild at the grown capacity before the insert
+// (k_scratch_maybe_clear and k_scratch_claims_reset apply ctl[2]).
+__global__ void k_scratch_grow(unsigned long long* __restrict__ ctl, u64 cap_alloc, float grow) {
+  const double need = (double)kScratchHeadroom * (double)ctl[1] * (double)grow;
+  u64 want = kScratchMinCap;
+  while ((double)want < need && want < cap_alloc) want <<= 1;
+  if (want > cap_alloc) want = cap_alloc;
+  ctl[2] = want > ctl[0] ? want : 0ull;
 }
 
 // Step 1 -- insert / stamp, two levels.
@@ -167,6 +182,33 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
         if (prev == k[j]) break;
       }
       if (++n >= R) {
+        // the active table is full (a surge of distinct keys): probe on in
+        // the rest of the allocation, which this batch's compaction then
+        // covers (ScratchView::ctl[4])
+        if (sv.ctl && parts == 1 && cap < sv.cap && n == R) {
+          sv.ctl[4] = sv.epoch;
+          const u64 Z = sv.cap - cap;
+          sj = cap + fmix64(k[j]) % Z;
+          c = skeys[sj];
+          for (u64 m = 0; c != k[j]; ) {
+            if (c == kEmptyKey) {
+              u64 prev = atomicCAS((unsigned long long*)&skeys[sj], (unsigned long long)kEmptyKey,
+                                   (unsigned long long)k[j]);
+              if (prev == kEmptyKey) {
+                ++claimed;
+                break;
+              }
+              if (prev == k[j]) break;
+            }
+            if (++m >= Z) {
+              sj = sv.cap;
+              break;
+            }
+            if (++sj == sv.cap) sj = cap;
+            c = skeys[sj];
+          }
+          if (sj < sv.cap) break;
+        }
         // no free slot: the key's occurrences go to the trash slot (index
         // cap: never stamped, so never in the unique list; its pulled row is
         // zero and its gradients are dropped) and the step is flagged --
@@ -183,7 +225,7 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
       }
       c = skeys[sj];
     }
-    XF_DASSERT(sj < cap || sj == sv.cap);
+    XF_DASSERT(sj <= sv.cap);
     t_key[h[j]] = sj;
     if (sj < sv.cap) sv.stamps[sj] = sv.epoch;
   }
@@ -234,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_count(ScratchView sv,
                                                           unsigned int* __restrict__ counts) {
   const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
   unsigned int cnt;
-  compact_hits(sv, base, active_cap(sv), cnt);
+  compact_hits(sv, base, batch_spilled(sv) ? sv.cap : active_cap(sv), cnt);
   unsigned int tot;
   block_exclusive_scan<kBlock>(cnt, &tot);
   if (threadIdx.x == 0) counts[blockIdx.x] = tot;
@@ -250,7 +292,7 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
     unsigned int* __restrict__ counts, int nb, unsigned long long* __restrict__ n_out,
     unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
     u64 cap_alloc, unsigned long long* __restrict__ n_copy,
-    unsigned long long* __restrict__ cap_out) {
+    unsigned long long* __restrict__ cap_out, u32 epoch) {
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
     int i = c0 + (int)threadIdx.x;
@@ -270,6 +312,8 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
       while (want < kScratchHeadroom * mx && want < cap_alloc) want <<= 1;
       if (want > cap_alloc) want = cap_alloc;
       const u64 cur = ctl[0];
+      // (stale claims <= cur / 2 at a batch start: 2x the most unique keys
+      // seen fit in the active table; a larger surge spills, see ctl[4])
       const bool rebuild = *claims > cur / 2 || want > cur || want * 4 <= cur;
       ctl[3] = cur;
       ctl[2] = rebuild ? want : 0ull;
@@ -278,7 +322,8 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
         *claims = 0ull;
       }
     }
-    if (cap_out) *cap_out = ctl ? ctl[3] : cap_alloc;  // (the reduction's bucket geometry)
+    // (the reduction's bucket geometry: a spilled batch's slots reach cap_alloc)
+    if (cap_out) *cap_out = ctl && ctl[4] != epoch ? ctl[3] : cap_alloc;
   }
 }
 
@@ -289,7 +334,7 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
                                                           u32* __restrict__ inv) {
   const u64 base = (u64)blockIdx.x * kCompactChunk + (u64)threadIdx.x * kCompactItems;
   unsigned int cnt;
-  unsigned int hit = compact_hits(sv, base, batch_cap(sv), cnt);
+  unsigned int hit = compact_hits(sv, base, batch_spilled(sv) ? sv.cap : batch_cap(sv), cnt);
   unsigned int tot;
   unsigned int ex = block_exclusive_scan<kBlock>(cnt, &tot);
   unsigned long long dst = (unsigned long long)offs[blockIdx.x] + ex;
@@ -365,7 +410,9 @@ void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
 
 void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipStream_t st) {
   if (nnz <= 0) return;
-  if (!s.ctl) {  // fixed capacity: threshold rebuild before the batch
+  if (!s.ctl || s.grow > 0.0f) {
+    // fixed capacity: threshold rebuild before the batch; adaptive: growth
+    if (s.ctl) hipLaunchKernelGGL(k_scratch_grow, dim3(1), dim3(1), 0, st, s.ctl, s.cap, s.grow);
     hipLaunchKernelGGL(k_scratch_maybe_clear, dim3(grid_for((int64_t)s.cap)), dim3(kBlock), 0, st,
                        s.keys, s.cap, s.claims, s.rebuild_at, s.ctl);
     hipLaunchKernelGGL(k_scratch_claims_reset, dim3(1), dim3(1), 0, st, s.claims, s.rebuild_at,
@@ -380,7 +427,7 @@ void launch_dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o, hipSt
   hipLaunchKernelGGL(k_compact_count, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts);
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kScanBlock), 0, st, o.block_counts, g2,
                      reinterpret_cast<unsigned long long*>(o.n_uniq), s.claims, s.ctl, s.cap,
-                     reinterpret_cast<unsigned long long*>(o.n_uniq_copy), o.cap_out);
+                     reinterpret_cast<unsigned long long*>(o.n_uniq_copy), o.cap_out, s.epoch);
   hipLaunchKernelGGL(k_compact_write, dim3(g2), dim3(kBlock), 0, st, s, o.block_counts,
                      o.uniq_keys, o.uniq_pos, o.inv);
   XF_HIP_CHECK(hipGetLastError());

@@ -48,11 +48,19 @@ struct ScratchView {
   // HIP backend: adaptive active capacity, kept on the device (no host sync).
   // ctl[0] = active cap for the next batch (power of two <= cap), ctl[1] = most
   // unique keys seen in one batch, ctl[2] = slots the compaction frees for a
-  // rebuild (0: none), ctl[3] = the cap the current batch was deduplicated with.
+  // rebuild (0: none), ctl[3] = the cap the current batch was deduplicated with,
+  // ctl[4] = epoch of the last batch that spilled past the active capacity (a
+  // full active table: the insert probes on into [ctl[0], cap) and that
+  // batch's compaction and reduction cover the whole allocation).
   // The table is probed modulo ctl[0]; the compaction scan re-sizes it to
   // kScratchHeadroom x the largest batch seen (a table that fits the Infinity
   // Cache instead of one sized for all-distinct batches).  Null: use cap.
   unsigned long long* ctl = nullptr;
+  // (with ctl) > 0 when this batch has more occurrences than any before, by
+  // this factor: the active capacity grows to kScratchHeadroom x (most unique
+  // keys seen) x grow before the insert, so a batch larger than the ones the
+  // capacity was fitted to cannot fill the table
+  float grow = 0.0f;
   // HIP: owner-partitioned probing for the sharded step.  With parts > 1 the
   // active capacity is split into `parts` equal ranges and a key probes only
   // the range of its owner (owner_of(key, parts)), so the slot-ordered unique
@@ -61,7 +69,7 @@ struct ScratchView {
   int parts = 1;
 };
 constexpr int kMaxParts = 1024;
-constexpr u64 kScratchHeadroom = 8;      // active cap >= 8 x max unique keys per batch
+constexpr u64 kScratchHeadroom = 4;      // active cap >= 4 x max unique keys per batch (A/B: 8 and 2 slower)
 constexpr u64 kScratchMinCap = 1ull << 16;
 
 struct DedupOut {

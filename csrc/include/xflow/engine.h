@@ -217,6 +217,7 @@ class Engine {
   float* red_rowv_ = nullptr;    // MVM: per-row loss*M (FwdArgs::red_rowv)
   float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz][max_slices]
   float* lr_nz_ = nullptr;       // LR-FTRL fused step: pulled (n, z) [max_nnz][2]
+  int64_t nnz_seen_ = 0;          // most occurrences in one batch (ScratchView::grow)
   u32* lr_mask_ = nullptr;       // LR-FTRL fused step, S > 1: unique-order slice bits [max_nnz]
   float* fm_grad_ = nullptr;     // reference FM fused step: unique-order (B, C) [max_nnz][2]
   int red_nb_ = 0;

@@ -139,9 +139,11 @@ def test_ftrl_single_key_closed_form(devname):
 
 @pytest.mark.gpu
 def test_adaptive_scratch_capacity_matches_cpu(gpu_device):
-    """The GPU dedup scratch shrinks to 8x the batch's unique keys, grows again
-    on a surge (device-side rebuilds), and training still equals the CPU
-    backend's (fixed-capacity scratch) step for step."""
+    """The GPU dedup scratch shrinks to kScratchHeadroom (4) x the batch's
+    unique keys, and a surge of distinct keys larger than the active table
+    spills into the rest of the allocation (ScratchView::ctl[4]) instead of
+    dropping keys, then grows it (device-side rebuilds); training still equals
+    the CPU backend's (fixed-capacity scratch) step for step."""
     rows, fields = 8192, 8
     engines = [Engine(ModelConfig(kind="lr"), OptimConfig(),
                       EngineConfig(table_log2_cap=20, max_rows=rows, max_nnz=rows * fields),
@@ -149,8 +151,11 @@ def test_adaptive_scratch_capacity_matches_cpu(gpu_device):
     caps = []
     allk = []
     for step in range(12):
-        vocab = 400 if step < 6 else 40000  # small batches, then a surge of new keys
-        k, rp, fg, lab = random_csr(rows, fields, vocab, seed=500 + step, variable=False)
+        k, rp, fg, lab = random_csr(rows, fields, 400, seed=500 + step, variable=False)
+        if step >= 6:  # small vocabularies, then a surge of ~63 K distinct keys
+            rng = np.random.default_rng(step)
+            pool = rng.integers(0, 1 << 62, size=2_000_000, dtype=np.int64).astype(np.uint64)
+            k = pool[rng.integers(0, pool.size, size=k.size)]
         allk.append(k)
         for e in engines:
             e.train_step(to_batch(k, rp, fg, lab, e.device))
