@@ -71,6 +71,9 @@ class CpuBackend final : public Backend {
   void upload_small(void* dst, const void* src, size_t bytes) override {
     if (bytes) std::memcpy(dst, src, bytes);
   }
+  void download_small(void* dst, const void* src, size_t bytes) override {
+    if (bytes) std::memcpy(dst, src, bytes);
+  }
   void* stage_pinned(int s, size_t bytes) override {
     if (stage_buf_[s].size() < bytes) stage_buf_[s].resize(bytes);
     return stage_buf_[s].data();

@@ -107,6 +107,9 @@ class HipBackend final : public Backend {
   void copy_d2d(void* dst, const void* src, size_t bytes) override {
     if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
   }
+  void download_small(void* dst, const void* src, size_t bytes) override {
+    hip::launch_download_small(dst, src, bytes, stream_);
+  }
   void upload_small(void* dst, const void* src, size_t bytes) override {
     hip::launch_upload_small(dst, src, bytes, stream_);
   }

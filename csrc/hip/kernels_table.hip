@@ -474,6 +474,22 @@ void launch_upload_small(void* dst, const void* src, size_t bytes, hipStream_t s
   XF_HIP_CHECK(hipGetLastError());
 }
 
+// (e.g. the sharded step's split sizes into pinned memory: a copy-engine D2H
+// left ~6 us of idle GPU behind it per step)
+__global__ void k_download_small(unsigned char* __restrict__ dst,
+                                 const unsigned char* __restrict__ src, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
+
+void launch_download_small(void* host_dst, const void* src, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return;
+  if (bytes > (1u << 16)) throw std::runtime_error("download_small: at most 64 KB");
+  hipLaunchKernelGGL(k_download_small, dim3(1), dim3(256), 0, st,
+                     static_cast<unsigned char*>(host_dst), static_cast<const unsigned char*>(src),
+                     (int)bytes);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
 void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st) {
   if (n == 0) return;
   hipLaunchKernelGGL(k_fill_u64, dim3(grid_for((int64_t)n)), dim3(kBlock), 0, st, p, v, n);

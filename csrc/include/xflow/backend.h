@@ -316,6 +316,10 @@ class Backend {
   // <= 256 bytes from the host, queued without a host wait (HIP: the bytes
   // travel as a kernel argument)
   virtual void upload_small(void* dst, const void* src, size_t bytes) = 0;
+  // device bytes into mapped pinned host memory, queued without a copy
+  // engine or host wait (HIP: a kernel's stores; the host reads them after an
+  // event recorded behind it)
+  virtual void download_small(void* host_dst, const void* src, size_t bytes) = 0;
   virtual void synchronize() = 0;
   virtual void set_stream(void* stream) = 0;
   virtual void* stream() const = 0;

@@ -57,6 +57,10 @@ class Engine {
   // Insert n synthetic keys no batch touches (Backend::table_prefill):
   // occupancy-realistic benchmarks of a long run's table.
   void prefill(int64_t n, uint64_t seed);
+  // Backend::download_small on the engine's stream
+  void download_small(void* host_dst, const void* src, size_t bytes) {
+    be_->download_small(host_dst, src, bytes);
+  }
   // Pull current values (host) of keys without inserting them.
   std::vector<float> pull_host(const std::vector<u64>& keys);
 

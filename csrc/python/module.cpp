@@ -239,6 +239,10 @@ PYBIND11_MODULE(_xflow_native, m) {
              d["line"] = r.line;
              return d;
            })
+      .def("download_small",
+           [](Engine& e, uintptr_t dst, uintptr_t src, size_t bytes) {
+             e.download_small(P<void>(dst), P<const void>(src), bytes);
+           })
       .def("prefill", &Engine::prefill, py::arg("n"), py::arg("seed") = 0x5eedull,
            py::call_guard<py::gil_scoped_release>())
       .def("pull_host",

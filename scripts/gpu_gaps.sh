@@ -5,8 +5,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/gaps
-for v in fused sharded; do
-  extra=""; [ "$v" = sharded ] && extra="--sharded"
+for v in ${GAP_VARIANTS:-fused sharded}; do
+  extra=""; [ "$v" = sharded ] && extra="--sharded"; [ "$v" = async ] && extra="--async"
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/gaps/$v -o run -- python3 bench.py --steps 20 --warmup 3 $extra > gpurun_out/gaps/$v.log 2>&1 || { echo "$v failed"; tail -20 gpurun_out/gaps/$v.log; exit 1; }
   f=$(find gpurun_out/gaps/$v -name "*kernel_trace.csv" | head -1)
   echo "== $v"; tail -1 gpurun_out/gaps/$v.log | cut -c1-200

@@ -296,6 +296,18 @@ class Engine:
         self._sync_stream()
         return int(self._e.nonzero_weights())
 
+    def download_small(self, dst: torch.Tensor, src: torch.Tensor) -> None:
+        """Queue a copy of a small device tensor into pinned host memory on the
+        current stream without the copy engine (read it after an event
+        recorded behind this call)."""
+        if self.is_gpu and not dst.is_pinned():
+            raise ValueError("download_small: dst must be pinned host memory")
+        if dst.numel() * dst.element_size() < src.numel() * src.element_size():
+            raise ValueError("download_small: dst too small")
+        self._sync_stream()
+        self._e.download_small(dst.data_ptr(), src.contiguous().data_ptr(),
+                               src.numel() * src.element_size())
+
     def eval_metrics(self, pctr: torch.Tensor, labels: torch.Tensor) -> dict:
         """AUC / logloss of predictions on this engine's device, computed there
         (GPU: radix sort + rank sums; only scalars come back).  Returns the

@@ -84,14 +84,15 @@ class AsyncShardedEngine(ShardedEngine):
             so += ns
             ro += nr
         if self._p2p_comm is not None:
+            if not peers:  # only the self part (copied on the compute stream)
+                return []
             self.p2p_ops += sum(1 for b in sbytes if b) + sum(1 for b in rbytes if b)
             cur = torch.cuda.current_stream(self.engine.device)
             st = self._p2p_stream
             st.wait_stream(cur)  # the gradients are written on the compute stream
             for t in (inp, out):
                 t.record_stream(st)
-            if peers:
-                self._p2p_comm.send_recv(peers, sends, sbytes, recvs, rbytes, st.cuda_stream)
+            self._p2p_comm.send_recv(peers, sends, sbytes, recvs, rbytes, st.cuda_stream)
             done = torch.cuda.Event()
             done.record(st)
             return [done]
@@ -136,9 +137,11 @@ class AsyncShardedEngine(ShardedEngine):
         ops = [(pulled, vals, send_splits, recv_splits)]
         if next_batch is not None:
             self.prepare(next_batch, exchange=False)
-            ops.append(self._counts_op(self._prep[1]))
+            cop = self._counts_op(self._prep[1])
+            if cop is not None:
+                ops.append(cop)
         self._a2a_ops(ops)
-        if next_batch is not None:
+        if next_batch is not None and not self._self_only():
             self._counts_sent(self._prep[1])
         # staleness 1: the previous step's pushes land after this step's pull
         self._apply_pending()

@@ -179,6 +179,10 @@ class ShardedEngine:
         return math.prod(t.shape[1:]) * t.element_size()  # bytes per split unit
 
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
+        if self.world == 1 and out.is_cuda:  # a self-exchange: one device copy
+            if out.data_ptr() != inp.data_ptr():
+                out.copy_(inp)
+            return
         if self._comm is None:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
             return
@@ -194,7 +198,7 @@ class ShardedEngine:
         """Several all-to-alls, each (out, inp, out_splits, in_splits) with
         None splits meaning equal parts: ONE RCCL group call (one kernel)
         natively, one call each (in list order on every rank) otherwise."""
-        if self._comm is None or len(ops) == 1:
+        if self._comm is None or len(ops) == 1 or self.world == 1:
             for out, inp, osp, isp in ops:
                 self._a2a(out, inp, osp, isp)
             return
@@ -222,11 +226,16 @@ class ShardedEngine:
         both = self._counts_both[wb]
         e.w_prepare(batch, W, both[:W], self._send_keys[wb], wb)
         self._prep = (batch, wb)
-        if exchange:
+        if self._self_only():  # receive counts = send counts (read from both[:W])
+            self._counts_sent(wb)
+        elif exchange:
             self._a2a(both[W:], both[:W], None, None)
             self._counts_sent(wb)
 
     def _counts_op(self, wb: int):
+        """The counts exchange of buffer set wb, or None (world 1: none)."""
+        if self._self_only():
+            return None
         both = self._counts_both[wb]
         return (both[self.world:], both[:self.world], None, None)
 
@@ -239,7 +248,7 @@ class ShardedEngine:
                 self._counts_host = [torch.empty(2 * self.world, dtype=torch.int64,
                                                  pin_memory=True) for _ in range(2)]
                 self._counts_ready = [torch.cuda.Event(), torch.cuda.Event()]
-            self._counts_host[wb].copy_(both, non_blocking=True)
+            self.engine.download_small(self._counts_host[wb], both)
             self._counts_ready[wb].record()
 
     def _take(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
@@ -262,14 +271,21 @@ class ShardedEngine:
             both = self._counts_host[wb].tolist()
         else:
             both = both.tolist()
-        send_splits, recv_splits = both[:W], both[W:]
+        send_splits, recv_splits = both[:W], (both[:W] if self._self_only() else both[W:])
         self.last_send, self.last_recv = int(sum(send_splits)), int(sum(recv_splits))
         return wb, send_splits, recv_splits, prefetch
 
     def _exchange_keys(self, wb: int, send_splits, recv_splits) -> torch.Tensor:
+        if self._self_only():  # world 1: the owner reads the send buffer in place
+            return self._send_keys[wb][:self.last_send]
         recv_keys = self._recv_keys.get(self.last_recv)
         self._a2a(recv_keys, self._send_keys[wb][:self.last_send], recv_splits, send_splits)
         return recv_keys
+
+    def _self_only(self) -> bool:
+        """World 1 on a GPU: every exchange is a self-exchange, so the step
+        aliases send and receive buffers instead of copying through RCCL."""
+        return self.world == 1 and self.engine.is_gpu
 
     @staticmethod
     def _offsets(splits):
@@ -298,26 +314,32 @@ class ShardedEngine:
         e.s_pull(recv_keys, n_recv, vals, insert=True, buf=0, offsets=offsets)
         if prefetch is not None:
             prefetch()
-        pulled = self._pulled.get(n_send * ps).view(n_send, ps)
-        ops = [(pulled, vals, send_splits, recv_splits)]
+        alias = self._self_only()
+        pulled = vals if alias else self._pulled.get(n_send * ps).view(n_send, ps)
+        ops = [] if alias else [(pulled, vals, send_splits, recv_splits)]
         if next_batch is not None:
             # the next batch's counts travel in the same group call as the values
             self.prepare(next_batch, exchange=False)
-            ops.append(self._counts_op(self._prep[1]))
+            cop = self._counts_op(self._prep[1])
+            if cop is not None:
+                ops.append(cop)
         self._a2a_ops(ops)
-        if next_batch is not None:
+        if next_batch is not None and not self._self_only():
             self._counts_sent(self._prep[1])
 
         W = S * e.grad_width  # (B, C) per slice for reference-math FM on the GPU
         grads_out = self._grads_out.get(n_send * W).view(n_send, W)
         masks_out = self._masks_out.get(n_send) if ordered_masks else None
         e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S, wb=wb)
-        grads_in = self._grads_in.get(n_recv * W).view(n_recv, W)
-        masks_in = self._masks_in.get(n_recv) if ordered_masks else None
-        ops = [(grads_in, grads_out, recv_splits, send_splits)]
-        if ordered_masks:  # slice masks in the same group call
-            ops.append((masks_in, masks_out, recv_splits, send_splits))
-        self._a2a_ops(ops)
+        if alias:
+            grads_in, masks_in = grads_out, masks_out
+        else:
+            grads_in = self._grads_in.get(n_recv * W).view(n_recv, W)
+            masks_in = self._masks_in.get(n_recv) if ordered_masks else None
+            ops = [(grads_in, grads_out, recv_splits, send_splits)]
+            if ordered_masks:  # slice masks in the same group call
+                ops.append((masks_in, masks_out, recv_splits, send_splits))
+            self._a2a_ops(ops)
         e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
         e.w_finish()
         self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)  # W = S * grad_width
