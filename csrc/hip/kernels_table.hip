@@ -684,8 +684,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_probe(TableView t, const u64* _
   const int64_t base = (int64_t)blockIdx.x * kPullChunk + threadIdx.x;
   unsigned int claims = 0;
   // (issuing every key's home-slot load before resolving any measured slower
-  // here, 97 vs 85 us per FM-8 step: the chains are resolved one lane-key at
-  // a time either way and the extra live registers cost occupancy)
+  // here: 97 vs 85 us per FM-8 step, profiles/r2_fm_pull_ab.txt)
 #pragma unroll
   for (int j = 0; j < kPullItems; ++j) {
     int64_t i = base + (int64_t)j * kBlock;
