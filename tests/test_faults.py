@@ -64,8 +64,8 @@ def test_checkpoint_resume_equals_uninterrupted(tmp_path):
 
 
 def _tracker(cwd, args, extra_env=None, timeout=300):
-    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="", XFLOW_DIST_TIMEOUT="30",
-               **(extra_env or {}))
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="", XFLOW_DIST_TIMEOUT="30")
+    env.update(extra_env or {})
     return subprocess.run([sys.executable, "-m", "xflow_amd.tracker", *args], cwd=cwd, env=env,
                           capture_output=True, text=True, timeout=timeout)
 
@@ -98,3 +98,23 @@ def test_tracker_gives_up_after_max_restarts(tmp_path):
                  {"XFLOW_FAULT": "kill:1:0"})
     assert r.returncode == 17
     assert r.stderr.count("exit 17,") == 2
+
+
+@pytest.mark.gpu
+def test_tracker_recovery_equals_uninterrupted_on_gpu(tmp_path, gpu_device):
+    """The same recovery on the HIP backend: the GPU gradient sums are
+    fixed-point (order-independent), so a run restarted from its epoch-2
+    checkpoint predicts bit-for-bit like the uninterrupted one."""
+    args = [TRAIN, TEST, "0", "4", "--threads", "8"]
+    env = {"HIP_VISIBLE_DEVICES": os.environ.get("HIP_VISIBLE_DEVICES", "0")}
+    a, b = tmp_path / "straight", tmp_path / "recovered"
+    a.mkdir()
+    b.mkdir()
+    r = _tracker(a, ["-n", "1", "--"] + args, env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _tracker(b, ["-n", "1", "--max-restarts", "2", "--ckpt", str(b / "ck"), "--"] + args,
+                 dict(env, XFLOW_FAULT="kill:0:2"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "attempt 0: exit 17" in r.stderr and "attempt 1: exit 0" in r.stderr
+    assert "resumed from" in r.stdout
+    np.testing.assert_array_equal(np.loadtxt(a / "pred_0_0.txt"), np.loadtxt(b / "pred_0_0.txt"))
