@@ -293,6 +293,13 @@ __global__ void __launch_bounds__(kScanBlock) k_compact_scan(
     unsigned long long* __restrict__ claims, unsigned long long* __restrict__ ctl,
     u64 cap_alloc, unsigned long long* __restrict__ n_copy,
     unsigned long long* __restrict__ cap_out, u32 epoch) {
+  // only the blocks of this batch's capacity hold stamps (the rest count 0):
+  // at 4x headroom that is 1/8 of the allocation's blocks
+  if (ctl) {
+    const u64 lim = ctl[4] == epoch ? cap_alloc : (u64)ctl[0];  // (read before thread 0 updates ctl)
+    const u64 nbl = (lim + kCompactChunk - 1) / kCompactChunk;
+    if (nbl < (u64)nb) nb = (int)nbl;
+  }
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nb; c0 += kScanBlock) {
     int i = c0 + (int)threadIdx.x;
