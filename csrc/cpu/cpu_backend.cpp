@@ -129,11 +129,11 @@ class CpuBackend final : public Backend {
       }
       if (n == s.cap) { *o.overflow = 1u; p = 0; }
       o.pos[i] = (u32)p;
-      s.stamps[p] = s.epoch;
+      s.stamps[p] = (unsigned char)s.epoch;
     }
     int64_t u = 0;
     for (u64 p = 0; p < s.cap; ++p) {
-      if (s.stamps[p] != s.epoch) continue;
+      if (s.stamps[p] != (unsigned char)s.epoch) continue;
       o.uniq_keys[u] = s.keys[p];
       o.uniq_pos[u] = (u32)p;
       ++u;

@@ -54,8 +54,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (scratch_.cap > (1ull << 31)) throw std::invalid_argument("max_nnz too large");
   scratch_.keys = balloc<u64>(be, scratch_.cap);
   be.fill_u64(scratch_.keys, kEmptyKey, scratch_.cap);
-  scratch_.stamps = balloc<u32>(be, scratch_.cap);
-  be.memset(scratch_.stamps, 0, sizeof(u32) * scratch_.cap);
+  scratch_.stamps = balloc<unsigned char>(be, scratch_.cap);
+  be.memset(scratch_.stamps, 0, scratch_.cap);
   scratch_.claims = balloc<unsigned long long>(be, 1);
   be.memset(scratch_.claims, 0, sizeof(unsigned long long));
   // Rebuild once half full: one more step adds at most max_nnz <= cap/factor
@@ -262,7 +262,16 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
     scratch_.parts = parts;
   }
   // (n_uniq is written, not accumulated, by both backends' dedup)
-  if (++scratch_.epoch == 0) scratch_.epoch = 1;  // 0 marks never-stamped slots
+  if (++scratch_.epoch > kStampEpochs) {
+    // byte stamps wrap: clear them (0 marks never-stamped slots) and the
+    // spill mark, which holds an epoch of the previous cycle
+    scratch_.epoch = 1;
+    be_->memset(scratch_.stamps, 0, scratch_.cap);
+    if (scratch_.ctl) {
+      const unsigned long long z = 0ull;
+      be_->upload_small(scratch_.ctl + 4, &z, sizeof(z));
+    }
+  }
   scratch_.grow = 0.0f;
   if (scratch_.ctl && nnz_seen_ > 0 && b.nnz > nnz_seen_)
     scratch_.grow = (float)((double)b.nnz / (double)nnz_seen_);

@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
     }
     XF_DASSERT(sj <= sv.cap);
     t_key[h[j]] = sj;
-    if (sj < sv.cap) sv.stamps[sj] = sv.epoch;
+    if (sj < sv.cap) sv.stamps[sj] = (unsigned char)sv.epoch;
   }
   __syncthreads();
 #pragma unroll
@@ -248,24 +248,18 @@ constexpr int kCompactItems = 16;
 constexpr int kCompactChunk = kBlock * kCompactItems;
 constexpr int kScanBlock = 1024;
 
-// 16 consecutive stamps as four dwordx4 loads (cap is a power of two >= 16,
-// so a 16-slot group is either fully inside the table or fully outside).
+// 16 consecutive byte stamps as one dwordx4 load (cap is a power of two >=
+// 16, so a 16-slot group is either fully inside the table or fully outside).
 __device__ __forceinline__ unsigned int compact_hits(const ScratchView& sv, u64 base, u64 cap,
                                                      unsigned int& cnt) {
   unsigned int hit = 0;
   cnt = 0;
   if (base >= cap) return 0;
-  const uint4* p = reinterpret_cast<const uint4*>(sv.stamps + base);
-  uint4 q[kCompactItems / 4];
+  const uint4 q = *reinterpret_cast<const uint4*>(sv.stamps + base);
+  const u32 w[4] = {q.x, q.y, q.z, q.w};
+  const u32 e = sv.epoch & 0xFFu;
 #pragma unroll
-  for (int j = 0; j < kCompactItems / 4; ++j) q[j] = p[j];
-#pragma unroll
-  for (int j = 0; j < kCompactItems / 4; ++j) {
-    unsigned int h = (unsigned int)(q[j].x == sv.epoch) | ((unsigned int)(q[j].y == sv.epoch) << 1) |
-                     ((unsigned int)(q[j].z == sv.epoch) << 2) |
-                     ((unsigned int)(q[j].w == sv.epoch) << 3);
-    hit |= h << (4 * j);
-  }
+  for (int j = 0; j < 16; ++j) hit |= (unsigned int)(((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) == e) << j;
   cnt = __popc(hit);
   return hit;
 }
@@ -395,7 +389,7 @@ __global__ void __launch_bounds__(kPartBlock) k_partition_counts(
     const u64 b = (u64)o * R, c = b / kCompactChunk, c0 = c * kCompactChunk;
     unsigned int hits = 0;
     for (u64 q = c0 + (u64)lane * 64; q < c0 + (u64)lane * 64 + 64; ++q)
-      hits += (q < b && sv.stamps[q] == sv.epoch) ? 1u : 0u;
+      hits += (q < b && sv.stamps[q] == (unsigned char)sv.epoch) ? 1u : 0u;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) hits += __shfl_xor(hits, d);
     if (lane == 0) start[o] = (int64_t)offs[c] + hits;

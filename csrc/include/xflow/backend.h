@@ -40,9 +40,13 @@ struct TableView {
 // inserted since the last clear) exceeds `rebuild_at`.
 struct ScratchView {
   u64* keys = nullptr;         // [cap], kEmptyKey when free
-  u32* stamps = nullptr;       // [cap], epoch of the last batch touching the slot
+  // [cap], epoch of the last batch touching the slot.  One byte (epochs
+  // cycle through 1..kStampEpochs, the stamps are cleared at the wrap): the
+  // leaders' scattered stamp stores dirty 4x fewer lines and the compaction
+  // reads 16 stamps per dwordx4
+  unsigned char* stamps = nullptr;
   u64 cap = 0;
-  u32 epoch = 1;               // current step (never 0)
+  u32 epoch = 1;               // current step (1..kStampEpochs)
   unsigned long long* claims = nullptr;  // device counter of inserted keys
   u64 rebuild_at = 0;          // clear the table before a step once claims > rebuild_at
   // HIP backend: adaptive active capacity, kept on the device (no host sync).
@@ -69,6 +73,7 @@ struct ScratchView {
   int parts = 1;
 };
 constexpr int kMaxParts = 1024;
+constexpr u32 kStampEpochs = 255;
 constexpr u64 kScratchHeadroom = 4;      // active cap >= 4 x max unique keys per batch (A/B: 8 and 2 slower)
 constexpr u64 kScratchMinCap = 1ull << 16;
 

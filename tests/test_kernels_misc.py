@@ -251,3 +251,25 @@ def test_field_major_synthetic_mvm_matches_cpu(gpu_device, rows):
     a, b = gpu.read_stats(), cpu.read_stats()
     print("mvm rows", rows, "gpu ln_loss/row", a["ln_loss"] / a["rows"], "cpu", b["ln_loss"] / b["rows"])
     assert abs(a["ln_loss"] - b["ln_loss"]) <= 1e-4 * abs(b["ln_loss"])
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+def test_stamp_epoch_wrap(devname):
+    """The dedup scratch stamps are one byte: epochs cycle through 1..255 and
+    the stamps are cleared at the wrap.  300 steps over recurring keys train
+    like the CPU backend (reference) across the wrap."""
+    dev = _dev(devname)
+    rows, fields = 256, 8
+    engines = [Engine(ModelConfig(kind="lr"), OptimConfig(),
+                      EngineConfig(table_log2_cap=16, max_rows=rows, max_nnz=rows * fields),
+                      device=d) for d in ([torch.device("cpu")] + ([dev] if dev.type == "cuda" else []))]
+    allk = []
+    for step in range(300):
+        k, rp, fg, lab = random_csr(rows, fields, 300, seed=9000 + step, variable=False)
+        allk.append(k)
+        for e in engines:
+            e.train_step(to_batch(k, rp, fg, lab, e.device))
+    keys = np.unique(np.concatenate(allk))
+    for e in engines:
+        assert not e.overflowed()
+    np.testing.assert_allclose(engines[-1].pull(keys), engines[0].pull(keys), rtol=1e-4, atol=1e-6)
