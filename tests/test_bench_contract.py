@@ -22,8 +22,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(n, extra):
-    args = ["--gpus", str(n), "--steps", "2", "--warmup", "1", "--cpu"] + extra
+def _run(n, extra, cpu=True):
+    args = ["--gpus", str(n), "--steps", "2", "--warmup", "1"] + (["--cpu"] if cpu else []) + extra
     if n == 1:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
     else:
@@ -38,7 +38,8 @@ def _run(n, extra):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n,extra", [(1, []), (2, []), (2, ["--model", "fm", "--v-dim", "8"])])
+@pytest.mark.parametrize("n,extra", [(1, []), (2, []), (2, ["--model", "fm", "--v-dim", "8"]),
+                                     (2, ["--async"]), (2, ["--slices", "4"])])
 def test_bench_json_line(n, extra):
     d = _run(n, extra)
     assert KEYS <= set(d)
@@ -51,3 +52,17 @@ def test_bench_json_line(n, extra):
     assert d["value"] == pytest.approx(cfg["global_batch"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3),
                                        rel=1e-6)
     assert 0.0 < d["logloss"] < 1.0 and d["table_keys"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--sharded"], ["--async"], ["--slices", "8"],
+                                   ["--model", "fm", "--v-dim", "8"], ["--model", "mvm", "--v-dim", "10"]])
+def test_bench_json_line_on_gpu(gpu_device, extra):
+    """The benchmark variants on the HIP backend (1 GPU, prefilled table):
+    the contract line, no overflow (bench.py exits non-zero on one), and a
+    table at the prefilled occupancy."""
+    d = _run(1, extra + ["--clock-warmup-s", "0"], cpu=False)
+    assert KEYS <= set(d)
+    assert d["config"]["backend"].startswith("hip:gfx950")
+    assert d["table_load"] > 0.4 and d["prefilled_keys"] > 0
+    assert 0.0 < d["logloss"] < 1.0
