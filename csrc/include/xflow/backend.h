@@ -152,7 +152,7 @@ constexpr int kRedMaxBuckets = 4096;
 // destinations per bucket for NV aggregated values per key (NV x 2^shift x 4 B <= 64 KB)
 constexpr int red_shift(int nv) { return nv == 1 ? kRedShift : kRedShift - 1; }
 constexpr int kLrGroupRows = 1024;  // rows per LR workgroup on the reduction path
-constexpr int kFmGroupRows = 512;   // rows per reference-FM workgroup on the reduction path
+constexpr int kFmGroupRows = 1024;  // rows per reference-FM workgroup on the reduction path (A/B: 512 -1.8 %)
 constexpr int kMvmGroupRows = 256;  // rows per MVM workgroup on the reduction path
 
 struct PullArgs {
