@@ -806,8 +806,15 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // apply (push)
 // ---------------------------------------------------------------------------
+// The reference divides a float sum by the row count in double and rounds to
+// float (lr_worker.cc:116-118).  For a float x and an integer n < 2^24 (exact
+// in float) that equals the correctly rounded float quotient x / n: double
+// rounding is innocuous for division when the wide format has >= 2p+2 bits
+// (53 >= 2*24+2), so the f64 division sequence is replaced by the f32 one.
 __device__ __forceinline__ float norm_grad(float raw, const int32_t* slice_rows, int s) {
-  return slice_rows ? (float)((double)raw / (double)slice_rows[s]) : raw;
+  if (!slice_rows) return raw;
+  const int32_t r = slice_rows[s];
+  return r < (1 << 24) ? raw / (float)r : (float)((double)raw / (double)r);
 }
 
 // LR-FTRL, one slice, 16-byte slots: read (n,z) as one dwordx2, write it back.

@@ -137,3 +137,21 @@ def test_gpu_matches_cpu_backend_eval(gpu_device):
         k, rp, fg, lab = random_csr(256, 8, 200, seed=99)
         outs.append(eng.eval_step(to_batch(k, rp, fg, lab, dev)).cpu().numpy())
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-4, atol=1e-6)
+
+
+def test_slice_normalisation_f32_division_equals_reference_double():
+    """The apply kernels normalise a float gradient sum by the slice's row count
+    with an f32 division (kernels_table.hip norm_grad); the reference divides
+    in double and rounds to float (lr_worker.cc:116-118).  Double rounding is
+    innocuous for division when the wide format has >= 2p+2 bits, so both give
+    the same float for rows < 2^24 -- checked here on random and edge values."""
+    rng = np.random.default_rng(7)
+    x = np.concatenate([
+        rng.standard_normal(200_000).astype(np.float32) * np.float32(10.0) ** rng.integers(-30, 30, 200_000).astype(np.float32),
+        np.array([0.0, -0.0, 1e-45, -1e-45, 1.17549435e-38, 3.4028235e38, -3.4028235e38], np.float32),
+    ]).astype(np.float32)
+    x = x[np.isfinite(x)]
+    for n in [1, 2, 3, 7, 10, 25, 200, 4095, 32768, 262143, 262144, (1 << 24) - 1]:
+        f32 = x / np.float32(n)
+        f64 = (x.astype(np.float64) / np.float64(n)).astype(np.float32)
+        assert np.array_equal(f32.view(np.uint32), f64.view(np.uint32)), n
