@@ -28,8 +28,10 @@ namespace xflow {
 namespace hip {
 
 constexpr u32 kNoSlot = 0xFFFFFFFFu;
-// grid cap of the lane-group pull/apply kernels (16 K workgroups of 256)
-constexpr int kGroupGridCap = 16384;
+// grid cap of the lane-group pull/apply kernels (8 K workgroups of 256: four
+// resident rounds; their grid-stride loops pipeline the random row accesses,
+// see RowPipe -- 16 K measured 2 % slower on FM-8, 64 K 6 %)
+constexpr int kGroupGridCap = 8192;
 
 // ---------------------------------------------------------------------------
 // dedup
@@ -677,17 +679,21 @@ __global__ void __launch_bounds__(kBlock) k_pull_generic(PullArgs a) {
 // (kPullItems keys in flight) and records the slot; phase 2 evaluates the
 // pull values with a group of G lanes per key (G = pow2 >= pstride), so the
 // slot's state words and the output row are read/written contiguously.
+// Keys per lane (sequential chains): 2 measured +0.6 % over 4 and 1 on FM-8
+// at table load 0.47; probing slot pairs per round trip -1.2 %
+// (profiles/r2_s3_fm_pull_apply_pipeline.txt).  The grid is sized by the
+// capacity, so blocks past the device count return at once.
+constexpr int kProbeItems = 2;
 __global__ void __launch_bounds__(kBlock) k_pull_probe(TableView t, const u64* __restrict__ keys,
                                                        const int64_t* n_dev, int64_t n_host,
                                                        int64_t n_max, bool insert,
                                                        u32* __restrict__ out_slot) {
   const int64_t n = dev_count(n_dev, n_host, n_max);
-  const int64_t base = (int64_t)blockIdx.x * kPullChunk + threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (kBlock * kProbeItems) + threadIdx.x;
+  if ((int64_t)blockIdx.x * (kBlock * kProbeItems) >= n) return;  // (grid sized by capacity)
   unsigned int claims = 0;
-  // (issuing every key's home-slot load before resolving any measured slower
-  // here: 97 vs 85 us per FM-8 step, profiles/r2_fm_pull_ab.txt)
 #pragma unroll
-  for (int j = 0; j < kPullItems; ++j) {
+  for (int j = 0; j < kProbeItems; ++j) {
     int64_t i = base + (int64_t)j * kBlock;
     if (i >= n) continue;
     bool claimed = false;
@@ -699,12 +705,13 @@ __global__ void __launch_bounds__(kBlock) k_pull_probe(TableView t, const u64* _
 
 // Packed lane groups for the multi-parameter pull/apply: P lanes per key
 // (lane p owns parameter p), floor(64/P) keys per wave, never straddling a
-// wave.  These kernels are VALU-issue bound (FTRL closed form with IEEE
-// division/sqrt, lazy N(0,1) init): the cost is per wave instruction, so
-// packing 7 FM-8 keys (P = 9) into a wave instead of 4 in pow2 groups of 16
-// lanes is 1.75x fewer instructions per key.  PMC of the pow2-group apply
-// (FM-8): 1626 VALU instructions per wave for 16 keys, 50 % of wave cycles
-// waiting.
+// wave.  In pow2 groups of 16 lanes these kernels were VALU-issue bound (FTRL
+// closed form with IEEE division/sqrt, lazy N(0,1) init; PMC of the FM-8
+// apply: 1626 VALU instructions per wave for 16 keys, 50 % of wave cycles
+// waiting): packing 7 FM-8 keys (P = 9) into a wave is 1.75x fewer
+// instructions per key.  Packed, they are bound by the dependent random row
+// accesses instead (an apply fed the pull's weights, skipping the closed
+// form, was slower), which RowPipe overlaps with the previous key's math.
 struct PackedLane {
   int P, K, g, p;        // lanes per key, keys per wave, key in wave, param
   bool on;               // lane belongs to a key group (64 % P lanes idle)
@@ -725,6 +732,58 @@ __device__ __forceinline__ PackedLane packed_lane(int P) {
   return r;
 }
 
+// One key's slot words a lane of its packed group needs (key, pushed flag,
+// the lane's param state), loaded one grid-stride iteration ahead of use by
+// the multi-parameter pull/apply: with the slot index loaded two ahead, the
+// random row access of iteration t+1 is in flight while iteration t computes.
+struct RowPre {
+  u64 key = 0;
+  u32 flag = 1;
+  float s0 = 0.0f, s1 = 0.0f;  // FTRL (n, z); SGD w
+};
+
+__device__ __forceinline__ RowPre row_pre(const u32* __restrict__ words, u32 slot, int p,
+                                          const TableLayout& L) {
+  RowPre r;
+  if (slot == kNoSlot) return r;
+  const u32* sp = words + (u64)slot * L.stride;
+  r.key = *reinterpret_cast<const u64*>(sp);
+  if (L.has_flag) r.flag = sp[L.flag_word];
+  if (L.opt == kFTRL) {
+    const float2 nz = *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
+    r.s0 = nz.x;
+    r.s1 = nz.y;
+  } else {
+    r.s0 = __uint_as_float(sp[2 + p]);
+  }
+  return r;
+}
+
+// Grid-stride pipeline over a packed group's keys: slots two iterations
+// ahead, row words one ahead (RowPre).
+struct RowPipe {
+  int64_t stride, n;
+  u32 s_cur, s_nx;
+  RowPre r_nx;
+  __device__ __forceinline__ void start(const u32* __restrict__ slots, const u32* words,
+                                        int64_t i, int p, const TableLayout& L) {
+    s_cur = i < n ? slots[i] : kNoSlot;
+    s_nx = i + stride < n ? slots[i + stride] : kNoSlot;
+    r_nx = row_pre(words, s_cur, p, L);
+  }
+  // at the top of iteration i: returns (slot, row) of i, issues i + stride's
+  // row loads and i + 2 * stride's slot load
+  __device__ __forceinline__ u32 next(const u32* __restrict__ slots, const u32* words, int64_t i,
+                                      int p, const TableLayout& L, RowPre& r) {
+    const u32 slot = s_cur;
+    r = r_nx;
+    s_cur = s_nx;
+    if (i + stride < n) r_nx = row_pre(words, s_cur, p, L);
+    if (i + 2 * stride < n) s_nx = slots[i + 2 * stride];
+    return slot;
+  }
+};
+
 __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
@@ -733,14 +792,19 @@ __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
   const int gbase = (threadIdx.x % kWave) - p;  // lane of the group's param 0
   // (a key group's lanes share i: the group-uniform loop keeps them together
   // through the shuffles; idle lanes run no iteration)
-  for (int64_t i = pl.on ? pl.first : n; i < n; i += pl.stride) {
-    const u32 slot = a.out_slot[i];
+  int64_t i = pl.on ? pl.first : n;
+  RowPipe pipe;
+  pipe.stride = pl.stride;
+  pipe.n = n;
+  pipe.start(a.out_slot, a.table.words, i, p, L);
+  for (; i < n; i += pl.stride) {
+    RowPre rp;
+    const u32 slot = pipe.next(a.out_slot, a.table.words, i, p, L, rp);
     float v;
     if (slot == kNoSlot) {
       v = absent_weight(sanitize_key(a.keys[i]), p, L, a.opt);
     } else {
-      const u32* sp = a.table.words + (u64)slot * L.stride;
-      v = slot_weight(sp, *reinterpret_cast<const u64*>(sp), p, L, a.opt);
+      v = state_weight(rp.key, rp.flag != 0u, rp.s0, rp.s1, p, L, a.opt);
     }
     if (a.out_w) {
       a.out_w[(size_t)i * a.pstride + p] = v;
@@ -788,7 +852,7 @@ void launch_table_pull(const PullArgs& a, hipStream_t st) {
   } else if (a.out_slot && a.pstride >= 2 && L.P <= kWave) {
     if (a.fm_vals && L.P < 2) throw std::runtime_error("fm_vals: bad layout");
     const int64_t nm = a.n_dev ? a.n_max : a.n_host;
-    const int g1 = (int)((nm + kPullChunk - 1) / kPullChunk);
+    const int g1 = (int)((nm + kBlock * kProbeItems - 1) / (kBlock * kProbeItems));
     hipLaunchKernelGGL(k_pull_probe, dim3(g1 > 0 ? g1 : 1), dim3(kBlock), 0, st, a.table, a.keys,
                        a.n_dev, a.n_host, a.n_max, a.insert, a.out_slot);
     if (a.out_vals || a.out_w || a.zero_out) {
@@ -1004,27 +1068,32 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   const int p = pl.p;
   const bool multi = a.grp.oidx != nullptr;
   const bool ftrl = L.opt == kFTRL;
-  for (int64_t i = pl.on ? pl.first : n; i < n; i += pl.stride) {
+  int64_t i = pl.on ? pl.first : n;
+  // (row words loaded an iteration ahead: another entry's slot -- keys are
+  // unique per launch, and of a key's entries only the leader writes)
+  RowPipe pipe;
+  pipe.stride = pl.stride;
+  pipe.n = n;
+  pipe.start(a.slots, a.table.words, i, p, L);
+  for (; i < n; i += pl.stride) {
+    RowPre rp;
+    const u32 slot = pipe.next(a.slots, a.table.words, i, p, L, rp);
     const u64* grow = nullptr;
     int src0 = 0, nsrc = 1;
     if (multi) {
       if (!group_leader(a.grp, i, grow, src0)) continue;  // uniform over the key's lanes
       nsrc = a.grp.nsrc;
     }
-    const u32 slot = a.slots[i];
     XF_DASSERT(slot == kNoSlot || slot < a.table.cap);
     if (slot != kNoSlot) {
       u32* sp = a.table.words + (u64)slot * L.stride;
-      const u64 key = *reinterpret_cast<const u64*>(sp);
-      bool pushed = !L.has_flag || sp[L.flag_word] != 0u;
-      float n0, z0 = 0.0f;
-      if (ftrl) {
-        const float2 nz = (a.nz_stash && L.P == 1) ? reinterpret_cast<const float2*>(a.nz_stash)[i]
-                                                   : *reinterpret_cast<const float2*>(sp + 2 + 2 * p);
+      const u64 key = rp.key;
+      bool pushed = rp.flag != 0u;
+      float n0 = rp.s0, z0 = rp.s1;  // FTRL (n, z); SGD w
+      if (ftrl && a.nz_stash && L.P == 1) {
+        const float2 nz = reinterpret_cast<const float2*>(a.nz_stash)[i];
         n0 = nz.x;
         z0 = nz.y;
-      } else {
-        n0 = __uint_as_float(sp[2 + p]);  // (SGD: w)
       }
       // current weight; w_next caches it between pushes and is recomputed
       // only when another push follows (the closed form is the bulk of this
