@@ -552,7 +552,7 @@ __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, b
 // registers, then whole lines.  Same table layout and probe order as
 // one-slot linear probing, but at a realistic load (0.47: a 1e9-key model in
 // 2^31 slots) a chain costs one extra round trip per line, not per slot.
-constexpr int kPullItems = 4;
+constexpr int kPullItems = 2;
 constexpr int kPullChunk = kBlock * kPullItems;
 constexpr int kLineSlots = 4;  // 16-byte slots per 64-byte line
 
@@ -566,6 +566,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
                                                       float2* __restrict__ out_nz,
                                                       float* __restrict__ zero_out) {
   const int64_t n = dev_count(n_dev, n_host, n_max);
+  if ((int64_t)blockIdx.x * kPullChunk >= n) return;  // (grid sized by capacity)
   const u64 mask = t.cap - 1;
   uint4* slots = reinterpret_cast<uint4*>(t.words);
   const int64_t base = (int64_t)blockIdx.x * kPullChunk + threadIdx.x;
