@@ -342,12 +342,25 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
   unsigned int ex = block_exclusive_scan<kBlock>(cnt, &tot);
   unsigned long long dst = (unsigned long long)offs[blockIdx.x] + ex;
   u32 iv[kCompactItems];
+  // the thread's 16 keys (one 128-byte line) loaded before any store: the
+  // stores to uk may alias sv.keys for the compiler, which would otherwise
+  // serialise one load round trip per hit
+  u64 kv[kCompactItems];
+  if (hit) {
+    const ulonglong2* kp = reinterpret_cast<const ulonglong2*>(sv.keys + base);
+#pragma unroll
+    for (int q = 0; q < kCompactItems / 2; ++q) {
+      const ulonglong2 v = kp[q];
+      kv[2 * q] = v.x;
+      kv[2 * q + 1] = v.y;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j) {
     iv[j] = 0xFFFFFFFFu;
     if (!(hit & (1u << j))) continue;
     u64 s = base + (u64)j;
-    uk[dst] = sv.keys[s];
+    uk[dst] = kv[j];
     up[dst] = (u32)s;
     iv[j] = (u32)dst;
     ++dst;
