@@ -596,6 +596,14 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
     int64_t i = base + (int64_t)j * kBlock;
     if (i < n) v[j] = slots[s[j]];
   }
+  // output rows loaded up front too: after the first key's stores the
+  // compiler could not hoist them (possible aliasing), one round trip each
+  u32 orow[kPullItems];
+#pragma unroll
+  for (int j = 0; j < kPullItems; ++j) {
+    int64_t i = base + (int64_t)j * kBlock;
+    orow[j] = (out_map && i < n) ? out_map[i] : (u32)i;
+  }
   unsigned int claims = 0;
 #pragma unroll
   for (int j = 0; j < kPullItems; ++j) {
@@ -657,7 +665,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
     }
     if (insert && slot == kNoSlot) *t.overflow = 1u;
     if (out_slot) out_slot[i] = slot;
-    if (out_vals) out_vals[out_map ? out_map[i] : i] = w;
+    if (out_vals) out_vals[out_map ? (int64_t)orow[j] : i] = w;
     if (out_nz) out_nz[i] = nz;
     if (zero_out) zero_out[i] = 0.0f;  // (width 1: LR)
   }
@@ -904,9 +912,9 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
   int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const FtrlParams fp = a.opt.ftrl;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    u32 slot = a.slots[i];
-    if constexpr (kSlices) {
+  if constexpr (kSlices) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      u32 slot = a.slots[i];
       // unique-order [key][slice] normalised sums: the present slices' pushes
       // in slice order (the CPU backend's Hogwild order)
       if (slot == kNoSlot) continue;
@@ -918,19 +926,41 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
         ftrl_push(nz.x, nz.y, w, g[__ffs(m) - 1], fp);
       }
       *st = nz;
-    } else {
-      u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
-      float raw = a.grads[row];
-      if (a.zero_after) a.grads[row] = 0.0f;
+    }
+  } else {
+    // the next key's loads are issued before this key's stores: on gfx9
+    // vmcnt also counts stores, so a load issued after them would wait for
+    // their completion as well
+    struct In {
+      u32 slot, row;
+      float raw;
+      float2 nz;
+    };
+    auto load = [&](int64_t i) {
+      In x;
+      x.slot = a.slots[i];
+      x.row = a.grad_map ? a.grad_map[i] : (u32)i;
+      x.raw = a.grads[x.row];
+      x.nz = make_float2(0.0f, 0.0f);
+      if (x.slot != kNoSlot)
+        x.nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i]
+                          : *reinterpret_cast<const float2*>(a.table.words + (u64)x.slot * 4 + 2);
+      return x;
+    };
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    In nx;
+    if (i < n) nx = load(i);
+    for (; i < n; i += stride) {
+      const In x = nx;
+      if (i + stride < n) nx = load(i + stride);
+      if (a.zero_after) a.grads[x.row] = 0.0f;
       if (a.reset_pos) a.scratch.keys[a.reset_pos[i]] = kEmptyKey;
-      if (slot == kNoSlot) continue;
-      float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
-      // (n, z) as pulled this step: coalesced, instead of a second random read
-      float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
-      float w = ftrl_weight(nz.y, nz.x, fp);
-      float g = norm_grad(raw, a.slice_rows, 0);
+      if (x.slot == kNoSlot) continue;
+      float2 nz = x.nz;
+      const float w = ftrl_weight(nz.y, nz.x, fp);
+      const float g = norm_grad(x.raw, a.slice_rows, 0);
       ftrl_push(nz.x, nz.y, w, g, fp);
-      *st = nz;
+      *reinterpret_cast<float2*>(a.table.words + (u64)x.slot * 4 + 2) = nz;
     }
   }
 }
