@@ -183,7 +183,8 @@ struct ColumnAgg {
 // drives the reduction kernels below.
 // NV = values aggregated per key: 1 (LR: Σ loss) or 2 (reference-math FM:
 // Σ loss and Σ loss*vsum, expanded to the 1+D gradient in k_red_sum).
-// Records: NV == 1 -> u64 (dest | value << 32), NV == 2 -> uint4 (dest, v0, v1, 0).
+// Records: NV == 1 -> u64 (dest | value << 32), NV == 2 -> uint3 (dest, v0, v1):
+// 12 bytes, dwordx3 accesses (a quarter less traffic than padded uint4 records).
 template <int LOG2, int NV = 1>
 struct ListAgg {
   static constexpr int kSlots = 1 << LOG2;
@@ -263,8 +264,8 @@ struct ListAgg {
       } else {
         const float v2 = (float)fx_to_double<kFx>(acc[t][hh * NV + 1]);
         acc[t][hh * NV + 1] = 0ll;
-        reinterpret_cast<uint4*>(region)[written + i] =
-            make_uint4(d, __float_as_uint(v), __float_as_uint(v2), 0u);
+        reinterpret_cast<uint3*>(region)[written + i] =
+            make_uint3(d, __float_as_uint(v), __float_as_uint(v2));
       }
       XF_DASSERT((int)(d >> shift) < kRedMaxBuckets);
       atomicAdd(&hist[d >> shift], 1u);
@@ -589,7 +590,7 @@ template <> struct RedRec<1> {
   __device__ static u32 dest(T r) { return (u32)r; }
 };
 template <> struct RedRec<2> {
-  using T = uint4;
+  using T = uint3;
   __device__ static u32 dest(T r) { return r.x; }
 };
 
@@ -934,7 +935,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   if (active) rs = row_span(b, r);
   const int len = rs.len;
   const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
-  u64* region = reinterpret_cast<u64*>(reinterpret_cast<uint4*>(a.red_pairs) +
+  u64* region = reinterpret_cast<u64*>(reinterpret_cast<uint3*>(a.red_pairs) +
                                        (b.row_ptr ? (int64_t)b.row_ptr[r0]
                                                   : r0 * b.nnz_per_row));
   ListAgg<LOG2, 2> lagg{s_tag64, s_acc, s_list, s_nlist, s_hist, region, 0u};
@@ -1028,7 +1029,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
                         s_nlist, s_hist, nullptr, 0u};
   int maxlen = 0;
   if constexpr (kGrad) {
-    lagg.region = reinterpret_cast<u64*>(reinterpret_cast<uint4*>(a.red_pairs) +
+    lagg.region = reinterpret_cast<u64*>(reinterpret_cast<uint3*>(a.red_pairs) +
                                          (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row));
     lagg.init(red_active(a, red_shift(2)));
     lagg.shift = red_geom(a).shift(red_shift(2));
