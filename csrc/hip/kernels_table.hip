@@ -1119,9 +1119,33 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
   pipe.stride = pl.stride;
   pipe.n = n;
   pipe.start(a.slots, a.table.words, i, p, L);
+  // one source, one slice: the key's gradient row joins the pipeline too
+  // (row index two iterations ahead, the lane's value(s) one ahead)
+  const bool gpipe = !multi && S == 1 && !a.masks && !a.sum_slices;
+  auto grad_row = [&](int64_t k) -> u32 { return a.grad_map ? a.grad_map[k] : (u32)k; };
+  auto grad_val = [&](u32 r) -> float2 {
+    const float* g = a.grads + (size_t)r * gs;
+    return a.fm_compact ? *reinterpret_cast<const float2*>(g) : make_float2(g[p], 0.0f);
+  };
+  u32 gr_cur = 0, gr_nx = 0;
+  float2 gv_nx = make_float2(0.0f, 0.0f);
+  if (gpipe && i < n) {
+    gr_cur = grad_row(i);
+    if (i + pl.stride < n) gr_nx = grad_row(i + pl.stride);
+    gv_nx = grad_val(gr_cur);
+  }
   for (; i < n; i += pl.stride) {
     RowPre rp;
     const u32 slot = pipe.next(a.slots, a.table.words, i, p, L, rp);
+    float2 gv = make_float2(0.0f, 0.0f);
+    u32 grow_i = 0;
+    if (gpipe) {
+      gv = gv_nx;
+      grow_i = gr_cur;
+      gr_cur = gr_nx;
+      if (i + pl.stride < n) gv_nx = grad_val(gr_cur);
+      if (i + 2 * pl.stride < n) gr_nx = grad_row(i + 2 * pl.stride);
+    }
     const u64* grow = nullptr;
     int src0 = 0, nsrc = 1;
     if (multi) {
@@ -1155,6 +1179,13 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
       // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
       const float w_pre = a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : w_next) : 0.0f;
       u32 any = 0;
+      if (gpipe) {
+        any = 1u;
+        const float raw = !a.fm_compact ? gv.x
+                          : (p == 0 ? (float)a.fm_D * gv.x : gv.y - w_pre * gv.x);
+        push(norm_grad(raw, a.slice_rows, 0));
+        nsrc = 0;  // (the per-source loop below is skipped)
+      }
       for (int sc = src0; sc < nsrc; ++sc) {
         u32 e = (u32)i;
         if (multi) {
@@ -1186,7 +1217,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
       if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
     }
     if (!multi && a.zero_after) {
-      const u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
+      const u32 row = gpipe ? grow_i : (a.grad_map ? a.grad_map[i] : (u32)i);
       float* g = a.grads + (size_t)row * S * gs;
       const int w = a.fm_compact ? 2 : ps;
       for (int s = 0; s < S; ++s)
