@@ -819,9 +819,14 @@ __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
   pipe.stride = pl.stride;
   pipe.n = n;
   pipe.start(a.out_slot, a.table.words, i, p, L);
+  // the output row index one iteration ahead as well: loaded after this
+  // iteration's stores it would wait for them (gfx9 vmcnt counts stores)
+  u32 om_nx = (a.out_map && i < n) ? a.out_map[i] : 0u;
   for (; i < n; i += pl.stride) {
     RowPre rp;
     const u32 slot = pipe.next(a.out_slot, a.table.words, i, p, L, rp);
+    const u32 om = om_nx;
+    if (a.out_map && i + pl.stride < n) om_nx = a.out_map[i + pl.stride];
     float v;
     if (slot == kNoSlot) {
       v = absent_weight(sanitize_key(a.keys[i]), p, L, a.opt);
@@ -835,7 +840,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
     if (a.zero_out)
       for (int c = p; c < a.zero_width; c += L.P) a.zero_out[(size_t)i * a.zero_width + c] = 0.0f;
     if (!a.out_vals) continue;
-    const size_t row = a.out_map ? a.out_map[i] : (size_t)i;
+    const size_t row = a.out_map ? (size_t)om : (size_t)i;
     if (a.fm_vals) {
       // (w, Σ_k v_k, Σ_k v_k^2) of the key, summed in param order by lane 0
       float sv = 0.0f, qv = 0.0f;
