@@ -1108,7 +1108,9 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
 // until the key's first push.  With a.grp (several sources) the group of a
 // key's leader entry applies the (source, slice) contributions in that
 // order; other entries skip.
-__global__ void __launch_bounds__(kBlock) k_apply_group(ApplyArgs a) {
+// (7 waves per SIMD: <= 72 VGPRs without spills -- 77 at the default gave 6;
+// 8 waves spills: FM-8 +1.7 % / -1 %, profiles/r2_s3_fm_pull_apply_pipeline.txt)
+__global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
   const int S = a.S, ps = a.pstride, gs = a.gstride ? a.gstride : ps;
