@@ -57,9 +57,13 @@ void RcclComm::alltoallv(const void* send, const std::vector<int64_t>& send_coun
 
 void RcclComm::alltoallv_group(const std::vector<A2AOp>& ops, uintptr_t stream) {
   if (!comm_) throw std::runtime_error("RCCL communicator was aborted");
-  for (const A2AOp& op : ops)
+  for (const A2AOp& op : ops) {
     if ((int)op.send_counts.size() != world_ || (int)op.recv_counts.size() != world_)
       throw std::invalid_argument("alltoallv: counts must have world entries");
+    for (int p = 0; p < world_; ++p)
+      if (op.send_counts[p] < 0 || op.recv_counts[p] < 0)
+        throw std::invalid_argument("alltoallv: negative count");
+  }
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   check(ncclGroupStart(), "ncclGroupStart");
@@ -87,11 +91,14 @@ void RcclComm::send_recv(const std::vector<int>& peers, const std::vector<uintpt
   const size_t n = peers.size();
   if (sends.size() != n || send_bytes.size() != n || recvs.size() != n || recv_bytes.size() != n)
     throw std::invalid_argument("send_recv: list lengths differ");
+  // (validated before the group opens: a throw must not leave it open)
+  for (size_t i = 0; i < n; ++i)
+    if (peers[i] < 0 || peers[i] >= world_ || send_bytes[i] < 0 || recv_bytes[i] < 0)
+      throw std::invalid_argument("send_recv: bad peer or size");
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   check(ncclGroupStart(), "ncclGroupStart");
   for (size_t i = 0; i < n; ++i) {
-    if (peers[i] < 0 || peers[i] >= world_) throw std::invalid_argument("send_recv: bad peer");
     if (send_bytes[i] > 0)
       check(ncclSend(reinterpret_cast<const void*>(sends[i]), (size_t)send_bytes[i], ncclUint8,
                      peers[i], c, st), "ncclSend");

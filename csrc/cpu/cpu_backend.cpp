@@ -48,7 +48,7 @@ void add_stats(LossStats* st, float p, float y) {
 u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
   const u64 mask = t.cap - 1;
   u64 s = fmix64(key) & mask;
-  for (u64 n = 0; n < t.cap; ++n) {
+  for (u64 n = 0; n < t.probe_limit; ++n) {
     u64* kp = reinterpret_cast<u64*>(t.words + s * (u64)t.L.stride);
     if (*kp == key) return (u32)s;
     if (*kp == kEmptyKey) {
@@ -59,7 +59,7 @@ u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
     }
     s = (s + 1) & mask;
   }
-  *t.overflow = 1u;
+  if (insert) *t.overflow = 1u;
   return kNoSlot;
 }
 
@@ -97,6 +97,8 @@ class CpuBackend final : public Backend {
   void synchronize() override {}
   void set_stream(void*) override {}
   void* stream() const override { return nullptr; }
+  void* host_alloc(size_t bytes) override { return alloc(bytes); }
+  void host_free(void* p) override { std::free(p); }
 
   void table_clear(const TableView& t) override {
     for (u64 s = 0; s < t.cap; ++s) {
@@ -300,7 +302,7 @@ class CpuBackend final : public Backend {
     std::vector<int64_t> cnt(a.world, 0), off(a.world, 0);
     for (int64_t i = 0; i < n; ++i) ++cnt[owner_of(a.uniq_keys[i], (u32)a.world)];
     for (int o = 1; o < a.world; ++o) off[o] = off[o - 1] + cnt[o - 1];
-    for (int o = 0; o < a.world; ++o) a.counts[o] = cnt[o];
+    for (int o = 0; o < a.world; ++o) a.counts[o] = a.seq >= 0 ? encode_count(cnt[o], a.seq) : cnt[o];
     for (int64_t i = 0; i < n; ++i) {
       int o = (int)owner_of(a.uniq_keys[i], (u32)a.world);
       int64_t d = off[o]++;
@@ -411,6 +413,18 @@ class CpuBackend final : public Backend {
       const u32 slot = probe(t, prefill_key(seed, (u64)i), true, claimed);
       if (claimed) ++*t.size;
       if (slot != kNoSlot && t.L.has_flag) t.words[(u64)slot * t.L.stride + t.L.flag_word] = 1u;
+    }
+  }
+  void table_rehash(const TableView& from, const TableView& to) override {
+    const int W = from.L.stride;
+    for (u64 s = 0; s < from.cap; ++s) {
+      const u32* sp = from.words + s * (u64)W;
+      const u64 key = *reinterpret_cast<const u64*>(sp);
+      if (key == kEmptyKey) continue;
+      bool claimed = false;
+      const u32 slot = probe(to, key, true, claimed);
+      if (claimed) ++*to.size;
+      if (slot != kNoSlot) std::memcpy(to.words + (u64)slot * W + 2, sp + 2, sizeof(u32) * (W - 2));
     }
   }
   EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {

@@ -29,6 +29,10 @@ constexpr char kMagic[8] = {'X', 'F', 'L', 'O', 'W', 'T', 'B', '1'};
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (cfg_.table_log2_cap < 4 || cfg_.table_log2_cap > 31)
     throw std::invalid_argument("table_log2_cap must be in [4, 31]");
+  if (!(cfg_.grow_load > 0.0 && cfg_.grow_load < 1.0))
+    throw std::invalid_argument("grow_load must be in (0, 1)");
+  if (cfg_.monitor_lag < 0 || cfg_.monitor_lag >= kSnaps)
+    throw std::invalid_argument("monitor_lag must be in [0, 7]");
   if (cfg_.max_slices < 1 || cfg_.max_slices > 32)
     throw std::invalid_argument("max_slices must be in [1, 32]");
   if (cfg_.model.kind != kLR && (cfg_.model.v_dim < 1 || cfg_.model.v_dim > 32))
@@ -38,15 +42,22 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 
   // persistent table
   table_.L = TableLayout::make(cfg_.model, cfg_.opt);
-  table_.cap = 1ull << cfg_.table_log2_cap;
+  log2_cap_ = cfg_.table_log2_cap;
+  max_log2_cap_ = cfg_.max_log2_cap > 0 ? (cfg_.max_log2_cap < 31 ? cfg_.max_log2_cap : 31) : 31;
+  if (max_log2_cap_ < log2_cap_) max_log2_cap_ = log2_cap_;
+  table_.cap = 1ull << log2_cap_;
+  table_.probe_limit = table_.cap < kMaxProbe ? table_.cap : kMaxProbe;
   table_bytes_ = (size_t)table_.cap * table_.L.stride * sizeof(u32);
   table_.words = static_cast<u32*>(be.alloc(table_bytes_));
-  table_.size = balloc<unsigned long long>(be, 1);
-  overflow_ = balloc<u32>(be, 2);
+  // one 16-byte block {size, overflow[2]}: a step's snapshot is one copy
+  mon_ = balloc<u32>(be, 4);
+  table_.size = reinterpret_cast<unsigned long long*>(mon_);
+  overflow_ = mon_ + 2;
   table_.overflow = overflow_ + 1;
-  be.memset(table_.size, 0, sizeof(unsigned long long));
-  be.memset(overflow_, 0, 2 * sizeof(u32));
+  be.memset(mon_, 0, 4 * sizeof(u32));
   be.table_clear(table_);
+  snaps_ = static_cast<Snap*>(be.host_alloc(sizeof(Snap) * kSnaps));
+  for (int i = 0; i < kSnaps; ++i) snap_ev_[i] = be.event_create();
 
   // per-step dedup scratch
   const int64_t nnz = cfg_.max_nnz;
@@ -143,15 +154,20 @@ Engine::~Engine() {
   Backend& be = *be_;
   be.synchronize();
   use_worker_set(cur_wb_);  // (records the current set)
-  void* ptrs[] = {table_.words, table_.size, overflow_, scratch_.keys, scratch_.stamps,
+  void* ptrs[] = {table_.words, mon_, scratch_.keys, scratch_.stamps,
                   scratch_.claims, block_counts_, uniq_keys_, uniq_slot_, wpull_, grad_, tmask_,
                   stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
-                  srv_slots_[0], srv_slots_[1], srv_nz_[0], srv_nz_[1], host_keys_dev_, host_vals_dev_,
+                  host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, own_pos_[0],
-                  own_pos_[1], own_idx_[0], own_idx_[1], srv_w_[0], srv_w_[1], fm_grad_,
+                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_,
                   lr_mask_};
   for (void* p : ptrs) be.free(p);
+  for (SrvBuf& b : srv_) {
+    void* bp[] = {b.slots, b.nz, b.w, b.own_pos, b.own_idx};
+    for (void* p : bp) be.free(p);
+  }
+  for (void* e : snap_ev_) be.event_destroy(e);
+  be.host_free(snaps_);
   for (StageSet& a : aset_) {
     void* ap[] = {a.keys, a.rowptr, a.fgid, a.labels};
     for (void* p : ap) be.free(p);
@@ -297,7 +313,7 @@ static bool lr16_disabled() {
 }
 
 void Engine::train_step(const BatchView& b) {
-  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
+  stale_stashes();  // the table changes: server stashes are stale
   use_worker_set(0);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
@@ -331,6 +347,7 @@ void Engine::train_step(const BatchView& b) {
   }
   dedup_(b, 1, nullptr, lr16 || fmu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)
+  guard_inserts(b.nnz);  // (<= nnz new keys; may grow the table first)
 
   PullArgs pa;
   pa.table = table_;
@@ -422,6 +439,7 @@ void Engine::train_step(const BatchView& b) {
     aa.gstride = 2;
   }
   be_->table_apply(aa);
+  end_step();
 }
 
 void Engine::eval_step(const BatchView& b, float* pctr) {
@@ -455,11 +473,12 @@ void Engine::eval_step(const BatchView& b, float* pctr) {
 }
 
 void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& grads) {
-  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
+  stale_stashes();  // the table changes: server stashes are stale
   const int64_t n = (int64_t)keys.size();
   const int P = cfg_.model.P();
   if ((int64_t)grads.size() != n * P) throw std::invalid_argument("push_host: grads != keys*P");
   if (n == 0) return;
+  guard_inserts(n);
   if (n > host_cap_) {
     be_->synchronize();
     be_->free(host_keys_dev_);
@@ -503,9 +522,10 @@ void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& g
 void Engine::prefill(int64_t n, uint64_t seed) {
   if (n < 0 || (uint64_t)n > table_.cap - table_.cap / 16)
     throw std::invalid_argument("prefill: at most 15/16 of the table's slots");
-  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;
+  stale_stashes();
   be_->table_prefill(table_, n, seed);
   be_->synchronize();
+  (void)table_size();  // (re-bases the capacity monitor)
 }
 
 std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
@@ -543,12 +563,18 @@ std::vector<float> Engine::pull_host(const std::vector<u64>& keys) {
 // multi-rank phases
 // ---------------------------------------------------------------------------
 void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out,
-                       int wb) {
+                       int wb, int64_t seq) {
+  if (world <= 1) seq = -1;  // (no exchange to check)
   use_worker_set(wb);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
-  if (b.nnz == 0) {  // a rank without data this step: nothing to send
-    be_->memset(counts_out, 0, sizeof(int64_t) * (world > 0 ? world : 1));
+  if (b.nnz == 0) {
+    // nothing to send; a batch without rows (a rank out of data) sends -1
+    // counts, which tell the receivers "no data from this source" (the loop
+    // ends when every source says so, ShardedEngine.train_step)
+    const int64_t c = b.rows == 0 ? -1 : 0;
+    be_->fill_u64(reinterpret_cast<u64*>(counts_out), (u64)(seq >= 0 ? encode_count(c, seq) : c),
+                  (size_t)(world > 0 ? world : 1));
     be_->memset(n_uniq_, 0, sizeof(int64_t));
     inv_valid_ = false;
     send_map_ = uniq_pos_;
@@ -561,7 +587,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
     if (red_pairs_ && (cfg_.model.kind == kLR || fm_vals_)) ensure_inv();
     dedup_(b, world, send_keys_out, true, world == 1 ? counts_out : nullptr);
     inv_valid_ = inv_ != nullptr;
-    if (world > 1) be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out);
+    if (world > 1) be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out, seq);
     send_map_ = uniq_pos_;
     return;
   }
@@ -577,21 +603,23 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
   ba.send_keys = send_keys_out;
   ba.send_pos = send_pos_;
   ba.scratch = bucket_ws_;
+  ba.seq = seq;
   be_->bucket(ba);
   send_map_ = send_pos_;
   (void)S;  // slice masks are built in w_forward_backward with the step's global S
 }
 
 void Engine::ensure_server_capacity(int64_t n, int buf) {
-  if (buf < 0 || buf > 1) throw std::invalid_argument("server buffer must be 0 or 1");
-  if (n <= srv_cap_[buf]) return;
+  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, 8)");
+  SrvBuf& sb = srv_[buf];
+  if (n <= sb.cap) return;
   be_->synchronize();
-  be_->free(srv_slots_[buf]);
-  be_->free(srv_nz_[buf]);
-  srv_nz_[buf] = nullptr;
-  srv_cap_[buf] = n + n / 4 + 1024;
-  srv_slots_[buf] = balloc<u32>(*be_, srv_cap_[buf]);
-  if (lr16_layout()) srv_nz_[buf] = balloc<float>(*be_, 2 * (size_t)srv_cap_[buf]);
+  be_->free(sb.slots);
+  be_->free(sb.nz);
+  sb.nz = nullptr;
+  sb.cap = n + n / 4 + 1024;
+  sb.slots = balloc<u32>(*be_, sb.cap);
+  if (lr16_layout()) sb.nz = balloc<float>(*be_, 2 * (size_t)sb.cap);
 }
 
 bool Engine::lr16_layout() const {
@@ -620,12 +648,18 @@ void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, 
 void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool insert, int buf,
                     const std::vector<int64_t>& src_offsets, bool keep_weights) {
   ensure_server_capacity(n, buf);
-  srv_n_[buf] = n;
-  srv_vals_[buf] = out_vals;
-  srv_w_valid_[buf] = false;
-  grp_[buf] = SrcGroups();
+  SrvBuf& sb = srv_[buf];
+  sb.n = n;
+  sb.vals = out_vals;
+  sb.w_valid = false;
+  sb.grp = SrcGroups();
+  // (kept until the buffer's s_apply: a table growth re-probes its slots)
+  sb.keys = insert && n > 0 ? recv_keys : nullptr;
   if (n == 0) return;
-  if (insert) group_entries(recv_keys, n, buf, src_offsets);
+  if (insert) {
+    guard_inserts(n);
+    group_entries(recv_keys, n, buf, src_offsets);
+  }
   PullArgs pa;
   pa.table = table_;
   pa.opt = cfg_.opt;
@@ -633,24 +667,30 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
   pa.n_host = n;
   pa.n_max = n;
   pa.insert = insert;
-  pa.out_slot = srv_slots_[buf];
+  pa.out_slot = sb.slots;
   pa.out_vals = out_vals;
   pa.pstride = pstride();
   pa.fm_vals = fm_vals_;
-  if (keep_weights && fm_vals_) {
-    // the per-parameter weights the workers' gradients refer to, for an apply
-    // that runs after other table updates (the staleness-1 step)
-    if (srv_w_cap_[buf] < n) {
+  // Compact FM value rows carry no per-parameter weights: an apply that runs
+  // after other table updates (the staleness-k step), or source by source
+  // because the owner grouping was skipped (world > kMaxGroupSources, or the
+  // other buffers' registrations were dropped on an owner-scratch resize),
+  // needs the weights the workers' gradients refer to.
+  const int nsrc = (int)src_offsets.size() - 1;
+  int active = 0;
+  for (int s2 = 0; s2 < nsrc; ++s2) active += src_offsets[s2 + 1] > src_offsets[s2];
+  if (fm_vals_ && insert && (keep_weights || (!sb.grp.oidx && active > 1))) {
+    if (sb.w_cap < n) {
       be_->synchronize();
-      be_->free(srv_w_[buf]);
-      srv_w_cap_[buf] = n + n / 4 + 1024;
-      srv_w_[buf] = balloc<float>(*be_, (size_t)srv_w_cap_[buf] * pstride());
+      be_->free(sb.w);
+      sb.w_cap = n + n / 4 + 1024;
+      sb.w = balloc<float>(*be_, (size_t)sb.w_cap * pstride());
     }
-    pa.out_w = srv_w_[buf];
-    srv_w_valid_[buf] = true;
+    pa.out_w = sb.w;
+    sb.w_valid = true;
   }
-  pa.out_nz = srv_nz_[buf];
-  srv_nz_fresh_[buf] = srv_nz_[buf] != nullptr;
+  pa.out_nz = sb.nz;
+  sb.nz_fresh = sb.nz != nullptr;
   be_->table_pull(pa);
 }
 
@@ -679,25 +719,27 @@ bool Engine::group_entries(const u64* recv_keys, int64_t n, int buf,
     be_->synchronize();
     const u64 cap = want > own_cap_ ? want : own_cap_;
     be_->free(own_keys_);
-    be_->free(own_idx_[0]);
-    be_->free(own_idx_[1]);
-    own_idx_[0] = own_idx_[1] = nullptr;
-    grp_[0] = grp_[1] = SrcGroups();
+    for (SrvBuf& b : srv_) {
+      be_->free(b.own_idx);
+      b.own_idx = nullptr;
+      b.grp = SrcGroups();
+    }
     own_cap_ = cap;
     own_nsrc_ = nsrc;
     own_keys_ = balloc<u64>(*be_, cap);
     be_->fill_u64(own_keys_, kEmptyKey, cap);
     own_fill_ = 0;
   }
-  if (!own_idx_[buf]) {
-    own_idx_[buf] = balloc<u64>(*be_, own_cap_ * (u64)own_nsrc_);
-    be_->memset(own_idx_[buf], 0, sizeof(u64) * own_cap_ * own_nsrc_);  // epoch 0: never valid
+  SrvBuf& sb = srv_[buf];
+  if (!sb.own_idx) {
+    sb.own_idx = balloc<u64>(*be_, own_cap_ * (u64)own_nsrc_);
+    be_->memset(sb.own_idx, 0, sizeof(u64) * own_cap_ * own_nsrc_);  // epoch 0: never valid
   }
-  if (n > own_pos_cap_[buf]) {
+  if (n > sb.own_pos_cap) {
     be_->synchronize();
-    be_->free(own_pos_[buf]);
-    own_pos_cap_[buf] = n + n / 4 + 1024;
-    own_pos_[buf] = balloc<u32>(*be_, own_pos_cap_[buf]);
+    be_->free(sb.own_pos);
+    sb.own_pos_cap = n + n / 4 + 1024;
+    sb.own_pos = balloc<u32>(*be_, sb.own_pos_cap);
   }
   if (own_fill_ + n > (int64_t)(own_cap_ / 2)) {
     be_->fill_u64(own_keys_, kEmptyKey, own_cap_);
@@ -710,16 +752,16 @@ bool Engine::group_entries(const u64* recv_keys, int64_t n, int buf,
   ga.n = n;
   ga.okeys = own_keys_;
   ga.ocap = own_cap_;
-  ga.opos = own_pos_[buf];
-  ga.oidx = own_idx_[buf];
+  ga.opos = sb.own_pos;
+  ga.oidx = sb.own_idx;
   ga.g.nsrc = nsrc;
   ga.g.epoch = own_epoch_;
   for (int s = 0; s <= nsrc; ++s) ga.g.offs[s] = offs[s];
   ga.overflow = overflow_;
   be_->owner_group(ga);
-  grp_[buf] = ga.g;
-  grp_[buf].opos = own_pos_[buf];
-  grp_[buf].oidx = own_idx_[buf];
+  sb.grp = ga.g;
+  sb.grp.opos = sb.own_pos;
+  sb.grp.oidx = sb.own_idx;
   return true;
 }
 
@@ -787,14 +829,16 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
 
 void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
                      const std::vector<int64_t>& src_offsets, int S, int buf) {
-  if (buf < 0 || buf > 1) throw std::invalid_argument("server buffer must be 0 or 1");
+  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, 8)");
+  SrvBuf& sb = srv_[buf];
+  sb.keys = nullptr;  // applied: no slot remap needed after a growth
   const int ps = pstride();
   const int gw = grad_width();
   // the first source applied sees the state its pull saw; a key sent by
   // several sources is updated by the earlier ones, so later sources re-read
   // (the grouped apply pushes every source of a key at once: its stash stays valid)
-  bool stash = srv_nz_fresh_[buf];
-  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;
+  bool stash = sb.nz_fresh;
+  stale_stashes();
   ApplyArgs base;
   base.table = table_;
   base.opt = cfg_.opt;
@@ -809,22 +853,22 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
   base.P = cfg_.model.P();
   base.sum_slices = cfg_.sum_slices;
   base.slice_rows = nullptr;
-  const SrcGroups& g = grp_[buf];
+  const SrcGroups& g = sb.grp;
   if (g.oidx && (int)src_offsets.size() == g.nsrc + 1) {
     bool same = true;
     for (int s = 0; s <= g.nsrc; ++s) same = same && src_offsets[s] == g.offs[s];
     if (!same) throw std::invalid_argument("s_apply: source offsets differ from the pull's");
     const int64_t n = g.offs[g.nsrc];
-    if (n > srv_n_[buf]) throw std::invalid_argument("s_apply: offsets beyond pull");
+    if (n > sb.n) throw std::invalid_argument("s_apply: offsets beyond pull");
     ApplyArgs aa = base;
     aa.keys = recv_keys;
-    aa.slots = srv_slots_[buf];
+    aa.slots = sb.slots;
     aa.n_host = n;
     aa.n_max = n;
     aa.grads = const_cast<float*>(recv_grads);
     if (aa.fm_compact) aa.pulled = pulled_weights(buf, 0);
     aa.masks = recv_masks;
-    if (stash) aa.nz_stash = srv_nz_[buf];
+    if (stash) aa.nz_stash = sb.nz;
     aa.grp = g;
     be_->table_apply(aa);
     return;
@@ -836,10 +880,10 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
     int64_t off = src_offsets[src];
     int64_t cnt = src_offsets[src + 1] - off;
     if (cnt <= 0) continue;
-    if (src_offsets[src + 1] > srv_n_[buf]) throw std::invalid_argument("s_apply: offsets beyond pull");
+    if (src_offsets[src + 1] > sb.n) throw std::invalid_argument("s_apply: offsets beyond pull");
     ApplyArgs aa = base;
     aa.keys = recv_keys + off;
-    aa.slots = srv_slots_[buf] + off;
+    aa.slots = sb.slots + off;
     aa.n_host = cnt;
     aa.n_max = cnt;
     aa.grads = const_cast<float*>(recv_grads) + off * (int64_t)S * gw;
@@ -852,7 +896,7 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
                                "apply or s_pull(keep_weights)");
     }
     aa.masks = recv_masks ? recv_masks + off : nullptr;
-    if (stash) aa.nz_stash = srv_nz_[buf] + 2 * off;
+    if (stash) aa.nz_stash = sb.nz + 2 * off;
     stash = false;
     be_->table_apply(aa);
   }
@@ -862,13 +906,135 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
 // FM apply: full pulled rows, or the owner's kept weights, or none (the apply
 // then takes the slot's current weights -- valid while no other update ran).
 const float* Engine::pulled_weights(int buf, int64_t off) const {
-  if (!fm_vals_) return srv_vals_[buf] + off * (int64_t)pstride();
-  if (srv_w_valid_[buf]) return srv_w_[buf] + off * (int64_t)pstride();
+  const SrvBuf& sb = srv_[buf];
+  if (!fm_vals_) return sb.vals + off * (int64_t)pstride();
+  if (sb.w_valid) return sb.w + off * (int64_t)pstride();
   return nullptr;
 }
 
-// The dedup scratch is epoch-stamped and persistent: nothing to release.
-void Engine::w_finish() {}
+// The dedup scratch is epoch-stamped and persistent: nothing to release; the
+// step's capacity snapshot is queued here.
+void Engine::w_finish() { end_step(); }
+
+// ---------------------------------------------------------------------------
+// table capacity management
+// ---------------------------------------------------------------------------
+// Consume the recorded snapshots in order (each event completes after the
+// older ones: one stream); wait_upto >= 0 waits for snapshots up to that
+// sequence number.  A snapshot with an overflow flag raises: keys were
+// dropped (table: no slot within the probe bound; dedup or owner scratch:
+// full), so the run is invalid -- fail within monitor_lag steps, not at
+// epoch end.
+void Engine::poll_snapshots(int64_t wait_upto) {
+  while (snap_seen_ < snap_seq_) {
+    const int i = (int)(snap_seen_ % kSnaps);
+    if (!be_->event_done(snap_ev_[i])) {
+      if (snap_seen_ > wait_upto) break;
+      be_->event_wait(snap_ev_[i]);
+      ++monitor_waits_;
+    }
+    const Snap sn = snaps_[i];
+    known_size_ = (int64_t)sn.size;
+    known_adds_ = snap_adds_[i];
+    ++snap_seen_;
+    if (sn.ovf[0] || sn.ovf[1]) {
+      char msg[320];
+      std::snprintf(msg, sizeof(msg),
+                    "xflow: %s overflow -- keys were dropped (table: %lld keys in 2^%d slots%s); "
+                    "raise the capacity (table_log2_cap / max_log2_cap, max_nnz)",
+                    sn.ovf[1] ? "parameter table" : "dedup/owner scratch", (long long)sn.size,
+                    log2_cap_, cfg_.table_grow ? "" : ", growth disabled");
+      throw std::runtime_error(msg);
+    }
+  }
+}
+
+// XFLOW_NO_MONITOR=1: no per-step snapshot (A/B of the monitor's cost only;
+// growth then relies on exact-size reads, overflow on the epoch-end check)
+static bool monitor_disabled() {
+  static const bool off = std::getenv("XFLOW_NO_MONITOR") != nullptr;
+  return off;
+}
+
+void Engine::end_step() {
+  if (monitor_disabled()) return;
+  if (snap_seq_ - snap_seen_ >= kSnaps) poll_snapshots(snap_seq_ - kSnaps);  // (ring slot reuse)
+  const int i = (int)(snap_seq_ % kSnaps);
+  be_->download_small(&snaps_[i], mon_, sizeof(Snap));
+  snap_adds_[i] = queued_adds_;
+  be_->event_record(snap_ev_[i]);
+  ++snap_seq_;
+  // bounded run-ahead: the snapshot monitor_lag steps back must be complete
+  poll_snapshots(snap_seq_ - 1 - cfg_.monitor_lag);
+}
+
+// Before an inserting pull of n keys (at most n new): make sure the table can
+// take them below grow_load.  The bound is the last snapshot's size plus
+// every insert bound queued since; only when it passes the watermark does the
+// host read the exact size (one sync), and grow if that is needed too.
+void Engine::guard_inserts(int64_t n) {
+  if (n <= 0) return;
+  poll_snapshots(-1);
+  const double lim = cfg_.grow_load * (double)table_.cap;
+  if (cfg_.table_grow && (double)(known_size_ + (queued_adds_ - known_adds_) + n) > lim) {
+    const int64_t exact = table_size();  // (syncs; re-bases the monitor)
+    ++monitor_waits_;
+    int lg = log2_cap_;
+    while ((double)(exact + n) > cfg_.grow_load * (double)(1ull << lg) && lg < max_log2_cap_) ++lg;
+    if (lg > log2_cap_) grow_table(lg);
+  }
+  queued_adds_ += n;
+}
+
+void Engine::grow_table(int lg) {
+  if (lg <= log2_cap_) return;
+  if (lg > 31) throw std::invalid_argument("grow_table: at most 2^31 slots (32-bit slot indices)");
+  be_->synchronize();
+  poll_snapshots(snap_seq_);  // (raises on a pending overflow first)
+  TableView nt = table_;
+  nt.cap = 1ull << lg;
+  nt.probe_limit = nt.cap < kMaxProbe ? nt.cap : kMaxProbe;
+  const size_t bytes = (size_t)nt.cap * table_.L.stride * sizeof(u32);
+  const size_t fr = be_->free_memory();
+  if (fr < bytes + (size_t)(256u << 20)) {
+    char msg[256];
+    std::snprintf(msg, sizeof(msg),
+                  "xflow: table growth to 2^%d slots needs %.1f GB, %.1f GB free on the device",
+                  lg, bytes / 1e9, fr / 1e9);
+    throw std::runtime_error(msg);
+  }
+  nt.words = static_cast<u32*>(be_->alloc(bytes));
+  be_->table_clear(nt);
+  be_->memset(table_.size, 0, sizeof(unsigned long long));  // counts the re-inserted keys
+  be_->table_rehash(table_, nt);
+  be_->synchronize();
+  be_->free(table_.words);
+  table_ = nt;
+  table_bytes_ = bytes;
+  log2_cap_ = lg;
+  ++growths_;
+  remap_server_slots();
+  (void)table_size();  // (re-bases the monitor)
+}
+
+// Slots of pulled-but-not-yet-applied server buffers point into the old
+// table: look their keys up again (all present, no insert).
+void Engine::remap_server_slots() {
+  for (SrvBuf& sb : srv_) {
+    if (!sb.keys || sb.n <= 0) continue;
+    PullArgs pa;
+    pa.table = table_;
+    pa.opt = cfg_.opt;
+    pa.keys = sb.keys;
+    pa.n_host = sb.n;
+    pa.n_max = sb.n;
+    pa.insert = false;
+    pa.out_slot = sb.slots;
+    pa.pstride = pstride();
+    be_->table_pull(pa);
+  }
+  be_->synchronize();
+}
 
 // ---------------------------------------------------------------------------
 LossStats Engine::read_stats(bool reset, int which) {
@@ -887,7 +1053,9 @@ int64_t Engine::n_unique() {
 
 int64_t Engine::table_size() {
   unsigned long long n = 0;
-  be_->copy_d2h(&n, table_.size, sizeof(n));
+  be_->copy_d2h(&n, table_.size, sizeof(n));  // (stream-synchronising: every queued insert is in)
+  known_size_ = (int64_t)n;
+  known_adds_ = queued_adds_;
   return (int64_t)n;
 }
 
@@ -1010,11 +1178,12 @@ void Engine::export_table(std::vector<u64>& keys, std::vector<u32>& words) {
 }
 
 void Engine::import_table(const std::vector<u64>& keys, const std::vector<u32>& words) {
-  srv_nz_fresh_[0] = srv_nz_fresh_[1] = false;  // the table changes: server stashes are stale
+  stale_stashes();  // the table changes: server stashes are stale
   const int W = state_words();
   const int64_t n = (int64_t)keys.size();
   if ((int64_t)words.size() != n * W) throw std::invalid_argument("import_table: size mismatch");
   if (n == 0) return;
+  guard_inserts(n);
   u64* dk = balloc<u64>(*be_, n);
   u32* dw = balloc<u32>(*be_, n * W);
   be_->copy_h2d(dk, keys.data(), sizeof(u64) * n);
@@ -1023,6 +1192,7 @@ void Engine::import_table(const std::vector<u64>& keys, const std::vector<u32>& 
   be_->synchronize();
   be_->free(dk);
   be_->free(dw);
+  (void)table_size();  // (re-bases the capacity monitor)
 }
 
 void Engine::save(const std::string& path) {

@@ -114,6 +114,39 @@ class HipBackend final : public Backend {
     hip::launch_upload_small(dst, src, bytes, stream_);
   }
   void synchronize() override { XF_HIP_CHECK(hipStreamSynchronize(stream_)); }
+  size_t free_memory() const override {
+    size_t fr = 0, tot = 0;
+    XF_HIP_CHECK(hipSetDevice(device_));
+    XF_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+    return fr;
+  }
+  void* host_alloc(size_t bytes) override {
+    void* p = nullptr;
+    XF_HIP_CHECK(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault));
+    std::memset(p, 0, bytes ? bytes : 16);
+    return p;
+  }
+  void host_free(void* p) override {
+    if (p) (void)hipHostFree(p);
+  }
+  void* event_create() override {
+    hipEvent_t e = nullptr;
+    XF_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
+  void event_destroy(void* e) override {
+    if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
+  }
+  void event_record(void* e) override {
+    XF_HIP_CHECK(hipEventRecord(static_cast<hipEvent_t>(e), stream_));
+  }
+  bool event_done(void* e) override {
+    const hipError_t r = hipEventQuery(static_cast<hipEvent_t>(e));
+    if (r == hipErrorNotReady) return false;
+    XF_HIP_CHECK(r);
+    return true;
+  }
+  void event_wait(void* e) override { XF_HIP_CHECK(hipEventSynchronize(static_cast<hipEvent_t>(e))); }
   // nullptr selects the null (default) stream, which is what torch reports as
   // its default current stream.
   void set_stream(void* s) override { stream_ = reinterpret_cast<hipStream_t>(s); }
@@ -135,8 +168,8 @@ class HipBackend final : public Backend {
   void bucket(const BucketArgs& a) override { hip::launch_bucket(a, stream_); }
   bool partitioned_dedup() const override { return true; }
   void partition_counts(const ScratchView& s, const u32* chunk_offsets, const int64_t* n_uniq,
-                        int64_t* counts) override {
-    hip::launch_partition_counts(s, chunk_offsets, n_uniq, counts, stream_);
+                        int64_t* counts, int64_t seq) override {
+    hip::launch_partition_counts(s, chunk_offsets, n_uniq, counts, seq, stream_);
   }
   bool owner_grouping() const override { return true; }
   void owner_group(const OwnerGroupArgs& a) override { hip::launch_owner_group(a, stream_); }
@@ -170,6 +203,9 @@ class HipBackend final : public Backend {
   }
   void table_prefill(const TableView& t, int64_t n, u64 seed) override {
     hip::launch_table_prefill(t, n, seed, stream_);
+  }
+  void table_rehash(const TableView& from, const TableView& to) override {
+    hip::launch_table_rehash(from, to, stream_);
   }
   EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {
     EvalMetrics m;

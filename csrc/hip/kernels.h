@@ -18,7 +18,7 @@ void launch_gather_grads(const GatherGradArgs& a, hipStream_t st);
 void launch_owner_group(const OwnerGroupArgs& a, hipStream_t st);
 void launch_bucket(const BucketArgs& a, hipStream_t st);
 void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
-                             const int64_t* n_uniq, int64_t* counts, hipStream_t st);
+                             const int64_t* n_uniq, int64_t* counts, int64_t seq, hipStream_t st);
 void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                          int64_t n_max, int width, float* zero_out, int zero_width,
                          hipStream_t st);
@@ -37,6 +37,7 @@ void launch_table_export(const TableView& t, u64* keys_out, u32* words_out, int6
 void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,
                          hipStream_t st);
 void launch_table_prefill(const TableView& t, int64_t n, u64 seed, hipStream_t st);
+void launch_table_rehash(const TableView& from, const TableView& to, hipStream_t st);
 void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long long* counter,
                           hipStream_t st);
 

@@ -391,7 +391,7 @@ constexpr int kPartBlock = 1024;
 
 __global__ void __launch_bounds__(kPartBlock) k_partition_counts(
     ScratchView sv, const unsigned int* __restrict__ offs, const int64_t* __restrict__ n_uniq,
-    int64_t* __restrict__ counts) {
+    int64_t* __restrict__ counts, int64_t seq) {
   __shared__ int64_t start[kMaxParts + 1];
   const u32 parts = (u32)sv.parts;
   const u64 R = batch_cap(sv) / parts;
@@ -412,15 +412,16 @@ __global__ void __launch_bounds__(kPartBlock) k_partition_counts(
   __syncthreads();
   for (u32 o = threadIdx.x; o < parts; o += kPartBlock) {
     XF_DASSERT(start[o + 1] >= start[o]);
-    counts[o] = start[o + 1] - start[o];
+    const int64_t c = start[o + 1] - start[o];
+    counts[o] = seq >= 0 ? encode_count(c, seq) : c;
   }
 }
 
 void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
-                             const int64_t* n_uniq, int64_t* counts, hipStream_t st) {
+                             const int64_t* n_uniq, int64_t* counts, int64_t seq, hipStream_t st) {
   if (s.parts < 2 || s.parts > kMaxParts) throw std::runtime_error("partition_counts: bad parts");
   hipLaunchKernelGGL(k_partition_counts, dim3(1), dim3(kPartBlock), 0, st, s, chunk_offsets,
-                     n_uniq, counts);
+                     n_uniq, counts, seq);
   XF_HIP_CHECK(hipGetLastError());
 }
 
@@ -535,7 +536,7 @@ __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, b
   const u64 mask = t.cap - 1;
   u64 s = fmix64(key) & mask;
   const int stride = t.L.stride;
-  for (u64 n = 0; n < t.cap; ++n) {
+  for (u64 n = 0; n < t.probe_limit; ++n) {
     u64* kp = reinterpret_cast<u64*>(t.words + s * (u64)stride);
     u64 cur = *kp;
     if (cur == key) return (u32)s;
@@ -548,7 +549,8 @@ __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, b
     }
     s = (s + 1) & mask;
   }
-  *t.overflow = 1u;
+  // bounded chain (TableView::probe_limit): a key is never stored further out
+  if (insert) *t.overflow = 1u;
   return kNoSlot;
 }
 
@@ -618,10 +620,12 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
 #pragma unroll
     for (int q = 0; q < kLineSlots; ++q) ln[q] = v[j];  // (only ln[q0] is read in round one)
     bool done = false;
-    for (u64 c = 0; c < t.cap && !done;) {
+    // c = slots examined so far = probe distance of the round's first slot;
+    // slots at distance >= probe_limit are never examined (bounded chains)
+    for (u64 c = 0; c < t.probe_limit && !done;) {
 #pragma unroll
       for (int q = 0; q < kLineSlots; ++q) {
-        if (q < q0 || q >= q1 || done) continue;
+        if (q < q0 || q >= q1 || done || c + (u64)(q - q0) >= t.probe_limit) continue;
         const u64 cur = (u64)ln[q].x | ((u64)ln[q].y << 32);
         const u64 sq = (sj & ~(u64)(kLineSlots - 1)) + (u64)q;
         if (cur == key[j]) {
@@ -1360,6 +1364,10 @@ __global__ void __launch_bounds__(kBlock) k_bucket_scatter(
   }
 }
 
+__global__ void k_encode_counts(int64_t* __restrict__ counts, int world, int64_t seq) {
+  for (int o = threadIdx.x; o < world; o += blockDim.x) counts[o] = encode_count(counts[o], seq);
+}
+
 void launch_bucket(const BucketArgs& a, hipStream_t st) {
   if (a.world > kMaxWorld) throw std::runtime_error("bucket: world size > 256 unsupported");
   XF_HIP_CHECK(hipMemsetAsync(a.counts, 0, sizeof(int64_t) * a.world, st));
@@ -1372,6 +1380,8 @@ void launch_bucket(const BucketArgs& a, hipStream_t st) {
                      a.n_dev, a.n_max, a.world,
                      reinterpret_cast<const unsigned long long*>(a.counts),
                      reinterpret_cast<unsigned long long*>(a.scratch), a.send_keys, a.send_pos);
+  if (a.seq >= 0)
+    hipLaunchKernelGGL(k_encode_counts, dim3(1), dim3(kBlock), 0, st, a.counts, a.world, a.seq);
   XF_HIP_CHECK(hipGetLastError());
 }
 
@@ -1505,6 +1515,32 @@ __global__ void __launch_bounds__(kBlock) k_table_import(TableView t, const u64*
     for (int w = 0; w < W; ++w) sp[2 + w] = words[i * W + w];
   }
   block_count_add<kBlock>(t.size, claims);
+}
+
+// Growth: every live slot of `from` is re-inserted into the empty, larger
+// table `to` with its state words (one lane per old slot, grid-stride).
+__global__ void __launch_bounds__(kBlock) k_table_rehash(TableView from, TableView to) {
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  const int W = from.L.stride;
+  unsigned int claims = 0;
+  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < from.cap; s += stride) {
+    const u32* sp = from.words + s * (u64)W;
+    const u64 key = *reinterpret_cast<const u64*>(sp);
+    if (key == kEmptyKey) continue;
+    bool claimed = false;
+    const u32 slot = probe(to, key, true, claimed);
+    claims += claimed;
+    if (slot == kNoSlot) continue;
+    u32* dp = to.words + (u64)slot * W;
+    for (int w = 2; w < W; ++w) dp[w] = sp[w];
+  }
+  block_count_add<kBlock>(to.size, claims);
+}
+
+void launch_table_rehash(const TableView& from, const TableView& to, hipStream_t st) {
+  hipLaunchKernelGGL(k_table_rehash, dim3(grid_for((int64_t)from.cap, kBlock, 16384)), dim3(kBlock),
+                     0, st, from, to);
+  XF_HIP_CHECK(hipGetLastError());
 }
 
 __global__ void __launch_bounds__(kBlock) k_table_prefill(TableView t, int64_t n, u64 seed) {

@@ -24,12 +24,22 @@
 
 namespace xflow {
 
+// Linear-probe chains are bounded: an insert that finds no free slot within
+// probe_limit slots of its home flags the table overflow instead of walking a
+// (nearly) full table, and a lookup stops at the same distance -- no key is
+// ever stored further from its home than an insert may probe.  The engine
+// keeps the load below EngineConfig::grow_load by growing the table (2x,
+// Backend::table_rehash), so chains stay short and the bound is never hit in
+// normal operation.
+constexpr u64 kMaxProbe = 1ull << 16;
+
 struct TableView {
   u32* words = nullptr;      // slot array
   u64 cap = 0;               // power of two
   TableLayout L;
   unsigned long long* size = nullptr;   // device counter: occupied slots
-  u32* overflow = nullptr;   // set when a probe wraps the whole table
+  u32* overflow = nullptr;   // set when an insert finds no slot within probe_limit
+  u64 probe_limit = 0;       // min(cap, kMaxProbe)
 };
 
 // Worker dedup table.  Persistent across steps: a key keeps its slot, so hot
@@ -73,6 +83,16 @@ struct ScratchView {
   int parts = 1;
 };
 constexpr int kMaxParts = 1024;
+
+// Counts of the multi-rank counts exchange (world > 1): one int64 per owner
+// carrying the count + 1 (0: the source has no data this step) in the low
+// kCountBits bits and the sender's prepare sequence number above them, so a
+// rank that skipped an exchange is detected by every peer at the next one.
+constexpr int kCountBits = 40;
+constexpr int64_t kSeqMask = (1ll << 23) - 1;
+XF_HD int64_t encode_count(int64_t count, int64_t seq) {
+  return ((seq & kSeqMask) << kCountBits) | (count + 1);
+}
 constexpr u32 kStampEpochs = 255;
 constexpr u64 kScratchHeadroom = 4;      // active cap >= 4 x max unique keys per batch (A/B: 8 and 2 slower)
 constexpr u64 kScratchMinCap = 1ull << 16;
@@ -273,6 +293,7 @@ struct BucketArgs {                // group unique keys by owning rank
   int64_t n_max = 0;
   int world = 1;
   int64_t* counts = nullptr;       // [world] (device) out
+  int64_t seq = -1;                // >= 0: write encode_count(count, seq)
   u64* send_keys = nullptr;        // [n_max] out, grouped by owner
   u32* send_pos = nullptr;         // [n_max] out
   int64_t* scratch = nullptr;      // [2*world] workspace
@@ -328,6 +349,19 @@ class Backend {
   virtual void synchronize() = 0;
   virtual void set_stream(void* stream) = 0;
   virtual void* stream() const = 0;
+  // Bytes of device memory still free (table growth checks it first).
+  virtual size_t free_memory() const { return ~(size_t)0; }
+
+  // Host-visible step snapshots (Engine's capacity monitor): pinned host
+  // memory a kernel can write (download_small), and completion events on the
+  // backend's stream.  The CPU backend is synchronous: events are always done.
+  virtual void* host_alloc(size_t bytes) = 0;
+  virtual void host_free(void* p) = 0;
+  virtual void* event_create() { return nullptr; }
+  virtual void event_destroy(void* e) { (void)e; }
+  virtual void event_record(void* e) { (void)e; }
+  virtual bool event_done(void* e) { (void)e; return true; }
+  virtual void event_wait(void* e) { (void)e; }
 
   // Asynchronous double-buffered host -> device staging (the native trainer's
   // input path).  Slot s in {0, 1}: stage_begin(s) waits on the host until
@@ -357,8 +391,8 @@ class Backend {
   // counts of the unique list from the compaction's chunk offsets.
   virtual bool partitioned_dedup() const { return false; }
   virtual void partition_counts(const ScratchView& s, const u32* chunk_offsets,
-                                const int64_t* n_uniq, int64_t* counts) {
-    (void)s, (void)chunk_offsets, (void)n_uniq, (void)counts;
+                                const int64_t* n_uniq, int64_t* counts, int64_t seq) {
+    (void)s, (void)chunk_offsets, (void)n_uniq, (void)counts, (void)seq;
     throw std::runtime_error("partitioned dedup is not supported by this backend");
   }
   // Owner grouping for the one-launch multi-source apply (HIP only).
@@ -395,6 +429,9 @@ class Backend {
   // keys a long run has accumulated but the current batches do not touch
   // (occupancy-realistic benchmarks).
   virtual void table_prefill(const TableView& t, int64_t n, u64 seed) = 0;
+  // Re-insert every live slot of `from` (key + state words) into the empty
+  // table `to` (a larger capacity); to.size counts the inserted keys.
+  virtual void table_rehash(const TableView& from, const TableView& to) = 0;
   // AUC / logloss sums of n predictions (backend memory; labels 0/1 floats)
   virtual EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) = 0;
 };

@@ -29,6 +29,21 @@ struct EngineConfig {
   bool sum_slices = false;     // apply Σ_s g_s once instead of ordered per-slice pushes
   double scratch_factor = 2.5;  // dedup scratch capacity = pow2 >= factor * max_nnz
   int device = -1;             // -1 => CPU backend, else HIP device ordinal
+  // Table capacity management (the reference's store is an unbounded
+  // unordered_map, ftrl.h:54-56,84).  Before every inserting pull the engine
+  // bounds the table's size from below-lagging device snapshots plus the
+  // inserts queued since (each at most the pull's key count); when the bound
+  // would pass grow_load * capacity the table is rehashed into 2x the slots
+  // (stream-ordered, the host is involved only then), up to 2^max_log2_cap.
+  // table_grow = false keeps the capacity fixed: an insert that finds no slot
+  // flags the overflow, and the next step start raises within monitor_lag
+  // steps of it.
+  bool table_grow = true;
+  double grow_load = 0.8;
+  int max_log2_cap = 0;        // 0 => 31, and what the device's free memory allows
+  // steps the host may run ahead of the device before it waits for a
+  // snapshot (bounds both the growth bound's slack and fail-fast latency)
+  int monitor_lag = 2;
 };
 
 class Engine {
@@ -71,8 +86,10 @@ class Engine {
   // in its forward/backward -- the pipelined sharded step.
   // worker: dedup the batch and group its unique keys by owner rank.
   // counts_out: backend int64[world]; send_keys_out: backend u64[>= n_unique].
+  // seq (world > 1): the caller's prepare sequence number, carried in the
+  // counts (encode_count) so that peers detect a rank that skipped a step.
   void w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* send_keys_out,
-                 int wb = 0);
+                 int wb = 0, int64_t seq = -1);
   // server: probe/insert n received keys, write pulled rows (pstride floats)
   // into out_vals (backend memory), remember slots for s_apply.
   // buf selects one of two server slot buffers (pipelined steps alternate).
@@ -113,6 +130,14 @@ class Engine {
   uint64_t table_capacity() const { return table_.cap; }
   size_t table_bytes() const { return table_bytes_; }
   bool overflowed();
+  // capacity management (EngineConfig::table_grow): growths so far, host
+  // waits the monitor needed, and an explicit growth to 2^log2_cap slots
+  int64_t table_growths() const { return growths_; }
+  int64_t monitor_waits() const { return monitor_waits_; }
+  void grow_table(int log2_cap);
+  // queue a snapshot of (table size, overflow flags) behind the step's
+  // work; called at the end of every training step (fused or sharded)
+  void end_step();
   // exactly non-zero (key, param) weights of this table shard (L1 sparsity)
   int64_t nonzero_weights() { return be_->table_nonzero(table_, cfg_.opt); }
   int pstride() const { return cfg_.model.pstride(); }
@@ -169,12 +194,8 @@ class Engine {
   u64* own_keys_ = nullptr;      // owner scratch [own_cap_]
   u64 own_cap_ = 0;
   int64_t own_fill_ = 0;         // entries registered since the last clear (upper bound of keys)
-  int own_nsrc_ = 0;             // row stride of own_idx_
-  u32* own_pos_[2] = {nullptr, nullptr};
-  int64_t own_pos_cap_[2] = {0, 0};
-  u64* own_idx_[2] = {nullptr, nullptr};
+  int own_nsrc_ = 0;             // row stride of SrvBuf::own_idx
   u32 own_epoch_ = 0;
-  SrcGroups grp_[2];             // grp_[buf].oidx != null: s_pull grouped this buffer
   bool group_entries(const u64* recv_keys, int64_t n, int buf,
                      const std::vector<int64_t>& src_offsets);
   const int32_t* slice_rows_dev(const BatchView& b, int S);
@@ -187,10 +208,6 @@ class Engine {
     return red_pairs_ && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference &&
            (double)scratch_.cap * cfg_.max_slices * pstride() < 4294967295.0;
   }
-  const float* srv_vals_[2] = {nullptr, nullptr};  // s_pull outputs (fm_compact apply)
-  float* srv_w_[2] = {nullptr, nullptr};           // s_pull(keep_weights) per-param weights
-  int64_t srv_w_cap_[2] = {0, 0};
-  bool srv_w_valid_[2] = {false, false};
   bool fm_vals_ = false;
   int vstride_ = 1;
   const float* pulled_weights(int buf, int64_t off) const;
@@ -208,7 +225,8 @@ class Engine {
   u32* uniq_slot_ = nullptr;    // [max_nnz]
   int64_t* n_uniq_ = nullptr;   // [1]
   u32* block_counts_ = nullptr; // dedup compaction workspace
-  u32* overflow_ = nullptr;     // [2]: scratch, table
+  u32* mon_ = nullptr;          // [4]: table size (u64), overflow_ (below)
+  u32* overflow_ = nullptr;     // [2]: scratch, table (= mon_ + 2)
   float* wpull_ = nullptr;      // [scratch_cap * pstride]
   float* grad_ = nullptr;       // [scratch_cap * max_slices * pstride]
   u32* tmask_ = nullptr;        // [scratch_cap]
@@ -255,18 +273,57 @@ class Engine {
   int32_t* st_fgid_ = nullptr;
   float* st_labels_ = nullptr;
 
-  // server buffers
-  // two server slot buffers: a pipelined (staleness-1) step applies the
-  // previous step's pushes after pulling into the other buffer
-  u32* srv_slots_[2] = {nullptr, nullptr};
-  int64_t srv_cap_[2] = {0, 0};
-  int64_t srv_n_[2] = {0, 0};
-  // LR-FTRL 16-byte slots: (n, z) as pulled into each buffer, and whether no
-  // apply has touched the table since that pull (then the first source's
-  // apply takes its state from here instead of re-reading the table)
-  float* srv_nz_[2] = {nullptr, nullptr};
-  bool srv_nz_fresh_[2] = {false, false};
+  // Server buffers: a pipelined step with staleness k applies a buffer's
+  // pushes after the next k pulls (parallel/async_p2p.py), so k + 1 are live.
+ public:
+  static constexpr int kSrvBufs = 8;
+ private:
+  struct SrvBuf {
+    u32* slots = nullptr;        // table slot of each received key (s_pull)
+    int64_t cap = 0;
+    int64_t n = 0;
+    const u64* keys = nullptr;   // the received keys (slots re-probed after a table growth)
+    // LR-FTRL 16-byte slots: (n, z) as pulled, and whether no apply has
+    // touched the table since that pull (then the first source's apply takes
+    // its state from here instead of re-reading the table)
+    float* nz = nullptr;
+    bool nz_fresh = false;
+    const float* vals = nullptr;  // s_pull outputs (fm_compact apply)
+    float* w = nullptr;           // s_pull(keep_weights) per-param weights
+    int64_t w_cap = 0;
+    bool w_valid = false;
+    u32* own_pos = nullptr;       // owner grouping of the buffer's entries
+    int64_t own_pos_cap = 0;
+    u64* own_idx = nullptr;
+    SrcGroups grp;                // grp.oidx != null: s_pull grouped this buffer
+  };
+  SrvBuf srv_[kSrvBufs];
+  void stale_stashes() {
+    for (SrvBuf& b : srv_) b.nz_fresh = false;
+  }
   bool lr16_layout() const;
+
+  // capacity monitor (EngineConfig::table_grow): a ring of pinned snapshots
+  // {table size, overflow[2]} written by a kernel at each step end, each with
+  // an event and the cumulative insert bound queued before it
+  struct Snap {
+    unsigned long long size;
+    u32 ovf[2];
+  };
+  static constexpr int kSnaps = 8;
+  Snap* snaps_ = nullptr;           // pinned host [kSnaps]
+  void* snap_ev_[kSnaps] = {};
+  int64_t snap_adds_[kSnaps] = {};
+  int64_t snap_seq_ = 0;            // snapshots recorded
+  int64_t snap_seen_ = 0;           // snapshots consumed (all older ones complete)
+  int64_t known_size_ = 0;          // table size at the last consumed snapshot (or sync)
+  int64_t known_adds_ = 0;          // cumulative insert bound queued before it
+  int64_t queued_adds_ = 0;         // cumulative insert bound queued so far
+  int64_t growths_ = 0, monitor_waits_ = 0;
+  int log2_cap_ = 0, max_log2_cap_ = 31;
+  void poll_snapshots(int64_t wait_upto);
+  void guard_inserts(int64_t n);   // before an inserting pull of <= n new keys
+  void remap_server_slots();
 
   u64* host_keys_dev_ = nullptr;   // push_host / pull_host staging
   float* host_vals_dev_ = nullptr;

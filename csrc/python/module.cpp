@@ -172,8 +172,13 @@ PYBIND11_MODULE(_xflow_native, m) {
   py::class_<Engine>(m, "Engine")
       .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,
                        int64_t max_nnz, int max_slices, bool sum_slices, double scratch_factor,
-                       int device) {
+                       int device, bool table_grow, double grow_load, int max_log2_cap,
+                       int monitor_lag) {
              EngineConfig c;
+             c.table_grow = table_grow;
+             c.grow_load = grow_load;
+             c.max_log2_cap = max_log2_cap;
+             c.monitor_lag = monitor_lag;
              c.model = model_from(model);
              c.opt = opt_from(opt);
              c.table_log2_cap = table_log2_cap;
@@ -188,7 +193,13 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("model"), py::arg("opt"), py::arg("table_log2_cap") = 20,
            py::arg("max_rows") = 1 << 16, py::arg("max_nnz") = 1 << 22,
            py::arg("max_slices") = 1, py::arg("sum_slices") = false,
-           py::arg("scratch_factor") = 2.5, py::arg("device") = -1)
+           py::arg("scratch_factor") = 2.5, py::arg("device") = -1,
+           py::arg("table_grow") = true, py::arg("grow_load") = 0.8, py::arg("max_log2_cap") = 0,
+           py::arg("monitor_lag") = 2)
+      .def_property_readonly("table_growths", &Engine::table_growths)
+      .def_property_readonly("monitor_waits", &Engine::monitor_waits)
+      .def("grow_table", &Engine::grow_table, py::call_guard<py::gil_scoped_release>())
+      .def("end_step", &Engine::end_step, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("is_gpu", &Engine::is_gpu)
       .def_property_readonly("backend_name", [](Engine& e) { return e.backend().name(); })
       .def_property_readonly("pstride", &Engine::pstride)
@@ -252,9 +263,11 @@ PYBIND11_MODULE(_xflow_native, m) {
            })
       .def("w_prepare",
            [](Engine& e, const BatchView& b, int world, uintptr_t counts, uintptr_t send_keys,
-              int wb) { e.w_prepare(b, world, P<int64_t>(counts), P<u64>(send_keys), wb); },
+              int wb, int64_t seq) {
+             e.w_prepare(b, world, P<int64_t>(counts), P<u64>(send_keys), wb, seq);
+           },
            py::arg("batch"), py::arg("world"), py::arg("counts"), py::arg("send_keys"),
-           py::arg("wb") = 0, py::call_guard<py::gil_scoped_release>())
+           py::arg("wb") = 0, py::arg("seq") = -1, py::call_guard<py::gil_scoped_release>())
       .def("s_pull",
            [](Engine& e, uintptr_t keys, int64_t n, uintptr_t out, bool insert, int buf,
               std::vector<int64_t> offsets, bool keep_weights) {
@@ -286,7 +299,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            },
            py::arg("keys"), py::arg("grads"), py::arg("masks"), py::arg("offsets"), py::arg("S"),
            py::arg("buf") = 0, py::call_guard<py::gil_scoped_release>())
-      .def("w_finish", &Engine::w_finish)
+      .def("w_finish", &Engine::w_finish, py::call_guard<py::gil_scoped_release>())
       .def("read_stats",
            [](Engine& e, bool reset, int which) { return stats_dict(e.read_stats(reset, which)); },
            py::arg("reset") = false, py::arg("which") = 0)

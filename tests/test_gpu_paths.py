@@ -26,9 +26,17 @@ def nccl_group(gpu_device):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,slices,transport", [("lr", 1, "rccl"), ("lr", 4, "rccl"),
-                                                   ("fm", 2, "rccl"), ("lr", 4, "torch")])
-def test_rccl_sharded_step_equals_fused(gpu_device, nccl_group, kind, slices, transport):
+@pytest.mark.parametrize("kind,slices,transport,self_exchange,pipelined",
+                         [("lr", 1, "rccl", "alias", False), ("lr", 4, "rccl", "alias", False),
+                          ("fm", 2, "rccl", "alias", False), ("lr", 4, "torch", "alias", False),
+                          ("lr", 1, "rccl", "comm", True), ("lr", 4, "rccl", "comm", True),
+                          ("fm", 1, "rccl", "comm", True), ("mvm", 2, "rccl", "comm", True)])
+def test_rccl_sharded_step_equals_fused(gpu_device, nccl_group, kind, slices, transport,
+                                        self_exchange, pipelined):
+    """self_exchange="comm": every exchange of the 1-rank step really goes
+    through RCCL (ncclSend/ncclRecv to self, grouped calls carrying the next
+    batch's counts with the values, masks with the gradients) -- the code
+    path of the multi-GPU step."""
     from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
     def mk():
@@ -37,14 +45,18 @@ def test_rccl_sharded_step_equals_fused(gpu_device, nccl_group, kind, slices, tr
                                    max_slices=slices), device=gpu_device)
 
     a, b = mk(), mk()
-    sh = ShardedEngine(a, transport=transport)
+    sh = ShardedEngine(a, transport=transport, self_exchange=self_exchange)
     assert sh.transport == transport
     keys = []
-    for step in range(4):
-        k, rp, fg, lab = random_csr(512, 8, 300, seed=step)
+    data = [random_csr(512, 8, 300, seed=step) for step in range(4)]
+    bs = [to_batch(*d, gpu_device, slice_rows=512 // slices) for d in data]
+    for step, (k, rp, fg, lab) in enumerate(data):
         keys.append(k)
-        sh.train_step(to_batch(k, rp, fg, lab, gpu_device, slice_rows=512 // slices))
+        nxt = bs[step + 1] if pipelined and step + 1 < len(bs) else None
+        assert sh.train_step(bs[step], next_batch=nxt)
         b.train_step(to_batch(k, rp, fg, lab, gpu_device, slice_rows=512 // slices))
+    if pipelined:
+        assert sh.inline_prepares == 1
     allk = np.unique(np.concatenate(keys))
     np.testing.assert_allclose(a.pull(allk), b.pull(allk), rtol=1e-5, atol=1e-7)
     # sharded eval == fused eval
@@ -181,33 +193,42 @@ def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind, S, pipe
     np.testing.assert_allclose(np.concatenate(allv), ref.pull(k), rtol=1e-4, atol=1e-6)
 
 
-def test_async_staleness_one_on_gpu_matches_simulation(gpu_device, nccl_group):
+@pytest.mark.parametrize("staleness,self_exchange", [(1, "alias"), (1, "comm"), (2, "comm"),
+                                                     (3, "alias")])
+def test_async_staleness_one_on_gpu_matches_simulation(gpu_device, nccl_group, staleness,
+                                                       self_exchange):
     """Config 4 on the HIP backend (1-rank RCCL group): AsyncShardedEngine ==
-    the reference step whose pulls miss exactly the previous step's pushes.
-    Also pins the owner apply's (n, z) stash: the staleness-1 step applies a
-    buffer after the other buffer's pull and apply, so it must re-read."""
+    the reference step whose pulls miss exactly the previous k steps' pushes.
+    Also pins the owner apply's (n, z) stash: the staleness-k step applies a
+    buffer after other buffers' pulls and applies, so it must re-read.  With
+    self_exchange="comm" the pushes ride in the next step's key exchange
+    through RCCL (one communicator, one stream)."""
+    from collections import deque
+
     from xflow_amd.parallel.async_p2p import AsyncShardedEngine
     from xflow_amd.testing import torch_ref
     from xflow_amd.testing.hashing import normal_init
 
-    rows, steps = 64, 4
+    rows, steps = 64, 6
     eng = Engine(ModelConfig(kind="lr", v_dim=4), OptimConfig(),
                  EngineConfig(table_log2_cap=14, max_rows=rows, max_nnz=rows * 16),
                  device=gpu_device)
-    sh = AsyncShardedEngine(eng)
+    sh = AsyncShardedEngine(eng, staleness=staleness, self_exchange=self_exchange)
     data = [random_csr(rows, 6, 80, seed=1000 * s) for s in range(steps)]
     for k, rp, fg, lab in data:
         sh.train_step(to_batch(k, rp, fg, lab, gpu_device), S=1)
     sh.flush()
     torch.cuda.synchronize()
+    assert sh.p2p_ops == steps
     ref = torch_ref.RefTable(1, 1, "ftrl", init_fn=lambda k, d: normal_init(k, d) * 1e-2)
-    pending = None
+    pending = deque()
     for k, rp, fg, lab in data:
         _, cur = torch_ref.compute_step(ref, "lr", k, lab, rp.astype(np.int32), rows)
-        if pending is not None:
-            torch_ref.apply_step(ref, pending)
-        pending = cur
-    torch_ref.apply_step(ref, pending)
+        if len(pending) == staleness:
+            torch_ref.apply_step(ref, pending.popleft())
+        pending.append(cur)
+    while pending:
+        torch_ref.apply_step(ref, pending.popleft())
     keys, _ = eng.export_table()
     np.testing.assert_allclose(eng.pull(keys), ref.weights(keys, insert=False).numpy(),
                                rtol=1e-4, atol=1e-6)

@@ -129,16 +129,39 @@ def test_checkpoint_reshard_2_to_1_and_3(tmp_path):
 
 
 def _trainer_worker(rank, world, data_dir, pred_dir):
+    import json
+
     from xflow_amd.config import TrainConfig
+    from xflow_amd.parallel import dist as xdist
     from xflow_amd.trainer import Trainer
 
+    metrics = os.path.join(pred_dir, "metrics.jsonl")
+    # 4 KB blocks: several blocks (steps) per epoch; rank 1 has fewer rows, so
+    # it runs out of data first and joins the last steps with empty batches
     cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
                       test_prefix=os.path.join(data_dir, "small_test"), epochs=3, threads=4,
-                      pred_dir=pred_dir, engine=EngineConfig(table_log2_cap=14))
+                      pred_dir=pred_dir, engine=EngineConfig(table_log2_cap=14),
+                      train_block_bytes=4096 if rank == 0 else 6144, metrics_file=metrics)
     t = Trainer(cfg, device=torch.device("cpu"))
-    res = t.train()
+    # the training loop needs no per-block collective or host sync: the end
+    # of an epoch travels in the counts exchange of the pipelined step
+    calls = []
+    orig = xdist.all_any
+    xdist.all_any = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        t.train_epochs(cfg.epochs)
+    finally:
+        xdist.all_any = orig
+    assert not calls, "per-block all_any in the training loop"
+    assert t.sharded.empty_steps == cfg.epochs
+    res = t.predict(0)
     if rank == 0:
         assert res["n"] == 200 and 0.0 < res["auc"] < 1.0
+        recs = [json.loads(x) for x in open(metrics)]
+        ep = [r for r in recs if r["event"] == "epoch"]
+        assert len(ep) == 3 and all(r["steps"] > 3 * (i + 1) for i, r in enumerate(ep))
+        # one batch per epoch is prepared in line (the first); no step waited
+        assert all(r["inline_prepares"] == 1 and r["host_waits"] == 0 for r in ep), ep
 
 
 def test_trainer_two_workers_bundled_data(tmp_path):
@@ -149,14 +172,16 @@ def test_trainer_two_workers_bundled_data(tmp_path):
     assert pred.shape == (200, 3)
 
 
-def _async_worker(rank, world, out_dir):
+def _async_worker(rank, world, out_dir, staleness=1):
     from xflow_amd.parallel.async_p2p import AsyncShardedEngine
 
     eng = _make_engine("lr", 1)
-    sh = AsyncShardedEngine(eng)
-    for step in range(STEPS + 1):
-        k, rp, fg, lab = _batches(rank, step)
-        sh.train_step(to_batch(k, rp, fg, lab, torch.device("cpu")), S=1)
+    sh = AsyncShardedEngine(eng, staleness=staleness)
+    bs = [to_batch(*_batches(rank, step), torch.device("cpu")) for step in range(STEPS + 2)]
+    for step in range(STEPS + 2):
+        # pipelined (next batch prepared inside the step) from the second step on
+        nxt = bs[step + 1] if 0 < step < STEPS + 1 else None
+        sh.train_step(bs[step], S=1, next_batch=nxt)
     sh.flush()
     keys, _ = eng.export_table()
     np.save(os.path.join(out_dir, f"akeys{rank}.npy"), keys)
@@ -164,26 +189,30 @@ def _async_worker(rank, world, out_dir):
     assert sh.p2p_ops > 0
 
 
-def test_async_p2p_staleness_one_matches_simulation(tmp_path):
+@pytest.mark.parametrize("staleness", [1, 2, 3])
+def test_async_p2p_staleness_one_matches_simulation(tmp_path, staleness):
     """AsyncShardedEngine == the reference step with pulls that miss exactly
-    the previous step's pushes (staleness 1), pushes in (source) order."""
+    the previous k steps' pushes (staleness k), pushes in (source) order."""
+    from collections import deque
+
     from xflow_amd.testing import torch_ref
     from xflow_amd.testing.hashing import normal_init
 
     world = 2
-    run_world(_async_worker, world, str(tmp_path))
+    run_world(_async_worker, world, str(tmp_path), staleness)
     ref = torch_ref.RefTable(1, 1, "ftrl", init_fn=lambda k, d: normal_init(k, d) * 1e-2)
-    pending = None
-    for step in range(STEPS + 1):
+    pending = deque()
+    for step in range(STEPS + 2):
         parts = [_batches(r, step) for r in range(world)]
         keys = np.concatenate([p[0] for p in parts])
         lab = np.concatenate([p[3] for p in parts])
         rp = np.concatenate([parts[0][1]] + [p[1][1:] + len(parts[0][0]) for p in parts[1:]])
         _, cur = torch_ref.compute_step(ref, "lr", keys, lab, rp.astype(np.int32), ROWS)
-        if pending is not None:
-            torch_ref.apply_step(ref, pending)
-        pending = cur
-    torch_ref.apply_step(ref, pending)
+        if len(pending) == staleness:
+            torch_ref.apply_step(ref, pending.popleft())
+        pending.append(cur)
+    while pending:
+        torch_ref.apply_step(ref, pending.popleft())
     k = np.concatenate([np.load(tmp_path / f"akeys{r}.npy") for r in range(world)])
     v = np.concatenate([np.load(tmp_path / f"avals{r}.npy") for r in range(world)])
     want = ref.weights(k, insert=False).numpy()

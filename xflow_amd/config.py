@@ -88,6 +88,14 @@ class EngineConfig:
     max_slices: int = 1
     sum_slices: bool = False      # one push of Σ_s g_s instead of ordered per-slice pushes
     scratch_factor: float = 2.5
+    # table capacity management (csrc/include/xflow/engine.h EngineConfig):
+    # grow 2x before the load could pass grow_load, up to 2^max_log2_cap
+    # (0: 2^31 or what free HBM allows); table_grow=False keeps it fixed and
+    # an overflow raises within monitor_lag steps
+    table_grow: bool = True
+    grow_load: float = 0.8
+    max_log2_cap: int = 0
+    monitor_lag: int = 2
 
 
 @dataclass

@@ -111,7 +111,9 @@ class Engine:
                            table_log2_cap=self.cfg.table_log2_cap, max_rows=self.cfg.max_rows,
                            max_nnz=self.cfg.max_nnz, max_slices=self.cfg.max_slices,
                            sum_slices=self.cfg.sum_slices, scratch_factor=self.cfg.scratch_factor,
-                           device=_device_index(self.device))
+                           device=_device_index(self.device), table_grow=self.cfg.table_grow,
+                           grow_load=self.cfg.grow_load, max_log2_cap=self.cfg.max_log2_cap,
+                           monitor_lag=self.cfg.monitor_lag)
         if self.is_gpu != (self.device.type == "cuda"):
             raise RuntimeError("native engine backend does not match the requested device")
 
@@ -214,10 +216,13 @@ class Engine:
     # wb: worker buffer set (0/1) holding a prepared batch's dedup state, so the
     # next batch can be prepared while the current one is still in flight.
     def w_prepare(self, batch: Batch, world: int, counts: torch.Tensor, send_keys: torch.Tensor,
-                  wb: int = 0):
+                  wb: int = 0, seq: int = -1):
+        """seq >= 0 (world > 1): counts are written encoded with the prepare
+        sequence number (csrc/include/xflow/backend.h encode_count)."""
         batch.check(self.device)
         self._sync_stream()
-        self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr(), int(wb))
+        self._e.w_prepare(batch.view(), world, counts.data_ptr(), send_keys.data_ptr(), int(wb),
+                          int(seq))
 
     def s_pull(self, recv_keys: torch.Tensor, n: int, out_vals: torch.Tensor,
                insert: bool = True, buf: int = 0, offsets=None, keep_weights: bool = False) -> None:
@@ -275,8 +280,29 @@ class Engine:
 
     @property
     def table_capacity(self) -> int:
-        """Slots of this rank's table shard."""
+        """Slots of this rank's table shard (grows, see EngineConfig.table_grow)."""
         return int(self._e.table_capacity)
+
+    @property
+    def table_growths(self) -> int:
+        """Times the table was rehashed into 2x the slots."""
+        return int(self._e.table_growths)
+
+    @property
+    def monitor_waits(self) -> int:
+        """Host waits of the capacity monitor (bounded run-ahead, exact-size reads)."""
+        return int(self._e.monitor_waits)
+
+    def grow_table(self, log2_cap: int) -> None:
+        """Rehash the table into 2^log2_cap slots now (normally automatic)."""
+        self._sync_stream()
+        self._e.grow_table(int(log2_cap))
+
+    def end_step(self) -> None:
+        """Queue the step's capacity snapshot (the sharded steps call it via
+        w_finish; raises if an earlier step overflowed)."""
+        self._sync_stream()
+        self._e.end_step()
 
     def n_unique(self) -> int:
         self._sync_stream()

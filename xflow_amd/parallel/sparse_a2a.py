@@ -7,7 +7,9 @@ fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
 
   1. w_prepare    dedup the batch's keys grouped by owner (owner-partitioned
                   scratch on the GPU, a bucket pass on the CPU backend)
-  2. a2a counts   (int64 x world); the split sizes return through pinned
+  2. a2a counts   (int64 x world; -1 = "this source has no data this step",
+                  so the loop ends when every source sent -1 -- no separate
+                  per-step collective); the split sizes return through pinned
                   memory and are read when the batch's step starts -- with
                   next_batch, one step after they were produced (see prepare)
   3. a2a keys     -> each owner receives the keys it serves
@@ -47,6 +49,10 @@ import torch.distributed as dist
 from xflow_amd.engine import Batch, Engine
 
 
+_COUNT_BITS = 40              # encode_count (csrc/include/xflow/backend.h)
+_SEQ_MASK = (1 << 23) - 1
+
+
 class _Buf:
     """Grow-only flat device buffer."""
 
@@ -76,11 +82,18 @@ class ShardedEngine:
 
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
                  world: Optional[int] = None, rank: Optional[int] = None,
-                 transport: str = "auto"):
+                 transport: str = "auto", self_exchange: Optional[str] = None):
         """world/rank default to the process group's; passing them (with _a2a
         overridden) runs the step over another transport, e.g. in-process
-        ranks in tests.  transport: see _init_transport."""
+        ranks in tests.  transport: see _init_transport.  self_exchange (world
+        1 on a GPU): "alias" (default) reads the send buffers in place;
+        "comm" sends every exchange through the transport anyway (RCCL
+        ncclSend/ncclRecv to self) -- the multi-GPU code path on one GPU
+        (XFLOW_SELF_EXCHANGE=comm)."""
         self.engine = engine
+        self.self_exchange = self_exchange or os.environ.get("XFLOW_SELF_EXCHANGE", "alias")
+        if self.self_exchange not in ("alias", "comm"):
+            raise ValueError("self_exchange must be 'alias' or 'comm'")
         self.group = group
         custom = world is not None or rank is not None
         self.world = int(world) if world is not None else dist.get_world_size(group)
@@ -105,9 +118,14 @@ class ShardedEngine:
         self.last_recv = 0
         self.bytes_moved = 0
         self.host_waits = 0        # split-size reads that found the copy still in flight
+        self.inline_prepares = 0   # steps whose batch was not prepared ahead (epoch starts)
+        self.drop_exchanges = 0    # fault injection (utils/faults.py drop_a2a): skip exchanges
+        self.empty_steps = 0       # steps every rank passed without data (loop ends)
         self._counts_host = None
         self._counts_ready = None
         self._prep = None          # (batch, worker buffer set) prepared ahead
+        self._seq = 0              # prepares so far (carried in the counts, world > 1)
+        self._prep_seq = [0, 0]    # sequence number of each worker set's batch
         self._next_wb = 0
         self._comm = None
         self.transport = "custom"
@@ -179,7 +197,10 @@ class ShardedEngine:
         return math.prod(t.shape[1:]) * t.element_size()  # bytes per split unit
 
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits) -> None:
-        if self.world == 1 and out.is_cuda:  # a self-exchange: one device copy
+        if self.drop_exchanges > 0:  # injected fault: this rank misses a collective
+            self.drop_exchanges -= 1
+            return
+        if self._self_only():  # a self-exchange: one device copy
             if out.data_ptr() != inp.data_ptr():
                 out.copy_(inp)
             return
@@ -198,7 +219,7 @@ class ShardedEngine:
         """Several all-to-alls, each (out, inp, out_splits, in_splits) with
         None splits meaning equal parts: ONE RCCL group call (one kernel)
         natively, one call each (in list order on every rank) otherwise."""
-        if self._comm is None or len(ops) == 1 or self.world == 1:
+        if self._comm is None or len(ops) == 1 or self._self_only() or self.drop_exchanges:
             for out, inp, osp, isp in ops:
                 self._a2a(out, inp, osp, isp)
             return
@@ -224,7 +245,9 @@ class ShardedEngine:
         wb = self._next_wb
         self._next_wb ^= 1
         both = self._counts_both[wb]
-        e.w_prepare(batch, W, both[:W], self._send_keys[wb], wb)
+        self._seq += 1  # (prepares are collective: every rank counts alike)
+        e.w_prepare(batch, W, both[:W], self._send_keys[wb], wb, self._seq if W > 1 else -1)
+        self._prep_seq[wb] = self._seq
         self._prep = (batch, wb)
         if self._self_only():  # receive counts = send counts (read from both[:W])
             self._counts_sent(wb)
@@ -252,9 +275,12 @@ class ShardedEngine:
             self._counts_ready[wb].record()
 
     def _take(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
-        """(worker buffer set, send splits, recv splits) of ``batch``, preparing
-        it now unless it is the batch prepared ahead."""
+        """(worker buffer set, send splits, recv splits, prefetch, any data) of
+        ``batch``, preparing it now unless it is the batch prepared ahead.
+        A count of -1 marks a source without data (Engine.w_prepare on a
+        batch of 0 rows); any data = some source (this rank included) has rows."""
         if self._prep is None or self._prep[0] is not batch:
+            self.inline_prepares += 1
             self.prepare(batch)
             if prefetch is not None:  # device work to overlap the split-size round trip
                 prefetch()
@@ -271,9 +297,24 @@ class ShardedEngine:
             both = self._counts_host[wb].tolist()
         else:
             both = both.tolist()
-        send_splits, recv_splits = both[:W], (both[:W] if self._self_only() else both[W:])
+        send, recv = both[:W], (both[:W] if self._self_only() else both[W:])
+        if W > 1:
+            # (count + 1, sender's prepare number): a peer that skipped an
+            # exchange shows up as a different number -- fail now, not later
+            mask = (1 << _COUNT_BITS) - 1
+            seqs = [int(c) >> _COUNT_BITS for c in recv]
+            want = self._prep_seq[wb] & _SEQ_MASK
+            if any(q != want for q in seqs):
+                raise RuntimeError(f"rank {self.rank}: counts exchange out of step (expected "
+                                   f"prepare {want}, peers sent {seqs}): a rank skipped or "
+                                   f"repeated a collective")
+            send = [(int(c) & mask) - 1 for c in send]
+            recv = [(int(c) & mask) - 1 for c in recv]
+        any_data = any(int(c) >= 0 for c in recv)
+        send_splits = [max(int(c), 0) for c in send]
+        recv_splits = [max(int(c), 0) for c in recv]
         self.last_send, self.last_recv = int(sum(send_splits)), int(sum(recv_splits))
-        return wb, send_splits, recv_splits, prefetch
+        return wb, send_splits, recv_splits, prefetch, any_data
 
     def _exchange_keys(self, wb: int, send_splits, recv_splits) -> torch.Tensor:
         if self._self_only():  # world 1: the owner reads the send buffer in place
@@ -284,8 +325,9 @@ class ShardedEngine:
 
     def _self_only(self) -> bool:
         """World 1 on a GPU: every exchange is a self-exchange, so the step
-        aliases send and receive buffers instead of copying through RCCL."""
-        return self.world == 1 and self.engine.is_gpu
+        aliases send and receive buffers instead of copying through RCCL
+        (unless self_exchange == "comm")."""
+        return self.world == 1 and self.engine.is_gpu and self.self_exchange == "alias"
 
     @staticmethod
     def _offsets(splits):
@@ -296,17 +338,23 @@ class ShardedEngine:
 
     def train_step(self, batch: Batch, S: Optional[int] = None,
                    prefetch: Optional[Callable[[], None]] = None,
-                   next_batch: Optional[Batch] = None) -> None:
+                   next_batch: Optional[Batch] = None) -> bool:
         """One lock-step training step.  S = slices per step, identical on every
         rank (defaults to this batch's slice count, fine when all ranks use the
         same batch shape).  ``prefetch``: device work producing the next batch
         (e.g. the synthetic generator), queued before ``next_batch`` is
-        prepared.  Every rank must pass next_batch (or not) alike."""
+        prepared.  Every rank must pass next_batch (or not) alike; a rank out
+        of data passes an empty batch (0 rows).  Returns False, having done
+        nothing, when no rank had data for ``batch`` -- every rank sees the
+        same counts, so all of them stop at the same step."""
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.value_width  # floats per pulled value row
         ordered_masks = S > 1 and not e.cfg.sum_slices
-        wb, send_splits, recv_splits, prefetch = self._take(batch, prefetch)
+        wb, send_splits, recv_splits, prefetch, any_data = self._take(batch, prefetch)
+        if not any_data:
+            self.empty_steps += 1
+            return False
         n_send, n_recv = self.last_send, self.last_recv
         recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
         offsets = self._offsets(recv_splits)
@@ -343,6 +391,7 @@ class ShardedEngine:
         e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
         e.w_finish()
         self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)  # W = S * grad_width
+        return True
 
     def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward-only sharded step (keys looked up, never inserted).  Every
@@ -350,7 +399,7 @@ class ShardedEngine:
         e = self.engine
         if pctr is None:
             pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
-        wb, send_splits, recv_splits, _ = self._take(batch)
+        wb, send_splits, recv_splits, _, _ = self._take(batch)
         recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
         ps = e.value_width  # floats per pulled value row
         vals = self._vals_out[0].get(self.last_recv * ps).view(self.last_recv, ps)

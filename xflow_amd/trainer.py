@@ -17,7 +17,11 @@ Differences by design (MI355X-first):
   the same weights, pushes applied in slice order), or one step per slice
   (serial_slices);
 * ranks advance in lock-step; a rank that ran out of blocks joins each
-  exchange with an empty batch until every rank is done with the epoch.
+  exchange with an empty batch until every rank is done with the epoch.  The
+  multi-rank loop is pipelined (each step prepares the rank's next batch) and
+  learns that the epoch is over from the counts exchange it does anyway (a
+  source without data sends -1 counts, ShardedEngine.train_step) -- no
+  per-block collective or host synchronisation.
 """
 from __future__ import annotations
 
@@ -154,11 +158,25 @@ class Trainer:
             return rows, max(1, -(-rows // self.threads))
         return ts * self.threads, ts
 
-    def _step(self, batch: Batch) -> None:
-        if self.sharded is not None:
-            self.sharded.train_step(batch, S=self.S)
-        elif batch.rows > 0:
-            self.engine.train_step(batch)
+    def _empty_batch(self) -> Batch:
+        if getattr(self, "_empty", None) is None:
+            self._empty = self._to_batch(None, 0, self.S)
+        return self._empty
+
+    def _epoch_batches(self, nxt, record):
+        """This rank's batches of one epoch: blocks from ``nxt()`` (None at
+        the end), each as one concurrent step or one step per slice."""
+        while True:
+            blk = nxt()
+            if blk is None:
+                return
+            if self._resident is not None:
+                batches = blk
+            else:
+                batches = list(self._slices_of(blk))
+                if record is not None:
+                    record.append(batches)
+            yield from batches
 
     def _slices_of(self, blk: Optional[dict]):
         """Batches of one block: one concurrent step, or one step per slice."""
@@ -198,8 +216,8 @@ class Trainer:
         for _ in range(epochs):
             stream = record = None
             if self._resident is not None:  # batches kept in HBM by the first epoch
-                it = iter(self._resident)
-                nxt = lambda: next(it, None)  # noqa: E731
+                blocks = iter(self._resident)
+                nxt = lambda: next(blocks, None)  # noqa: E731
             else:
                 xfb = binfmt.shard_file(path)
                 reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
@@ -212,28 +230,33 @@ class Trainer:
                 record = [] if cfg.resident else None
             t0 = time.perf_counter()
             ep_samples = 0
+            sh = self.sharded
+            w0 = (sh.host_waits, sh.inline_prepares) if sh is not None else (0, 0)
+            it = self._epoch_batches(nxt, record)
+            empty = self._empty_batch()
+            cur = next(it, None)
             while True:
-                blk = nxt()
-                if not xdist.all_any(blk is not None, self.device):
+                # multi-rank: the next batch is prepared inside this step and
+                # the epoch ends when no rank has data (counts of -1)
+                nb = next(it, None) if sh is not None else None
+                if sh is None and cur is None:
                     break
-                if self._resident is not None and blk is not None:
-                    batches = blk
-                else:
-                    batches = list(self._slices_of(blk))
-                    if record is not None and blk is not None:
-                        record.append(batches)
-                for b in batches:
-                    if self.watchdog is not None:
-                        self.watchdog.beat()
-                    if not self.faults.before_step(self.steps):
-                        self.steps += 1
-                        continue
-                    with self.timer.phase("step"):
-                        self._step(b)
-                    self.steps += 1
-                    ep_samples += b.rows
-                    if log_every and self.steps % log_every == 0:
-                        self._log_progress(ep_samples, t0)
+                if self.watchdog is not None:
+                    self.watchdog.beat()
+                if cur is not None and not self.faults.before_step(self.steps) and sh is not None:
+                    sh.drop_exchanges += 1  # fault injection: this rank skips an exchange
+                with self.timer.phase("step"):
+                    if sh is not None:
+                        if not sh.train_step(cur if cur is not None else empty, S=self.S,
+                                             next_batch=nb if nb is not None else empty):
+                            break
+                    elif cur.rows > 0:
+                        self.engine.train_step(cur)
+                self.steps += 1
+                ep_samples += cur.rows if cur is not None else 0
+                if log_every and self.steps % log_every == 0:
+                    self._log_progress(ep_samples, t0)
+                cur = nb if sh is not None else next(it, None)
             if stream is not None:
                 stream.close()
             if record is not None:
@@ -254,7 +277,15 @@ class Trainer:
             rec = dict(event="epoch", epoch=self.epoch, steps=self.steps,
                        train_logloss=tot[0] / max(tot[1], 1.0),
                        samples_per_s=tot[2] / max(time.perf_counter() - t0, 1e-9),
-                       table_keys=keys, table_load=keys / float(self.engine.table_capacity))
+                       table_keys=keys, table_load=keys / float(self.engine.table_capacity),
+                       table_capacity=self.engine.table_capacity,
+                       table_growths=self.engine.table_growths,
+                       monitor_waits=self.engine.monitor_waits)
+            if sh is not None:
+                # split-size reads that found the device copy in flight, and
+                # steps whose batch was not prepared ahead (the epoch's first)
+                rec["host_waits"] = sh.host_waits - w0[0]
+                rec["inline_prepares"] = sh.inline_prepares - w0[1]
             if self.cfg.optim.lambda1 > 0 and os.environ.get("XFLOW_REPORT_NNZ"):
                 rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
                                                            self.device)[0])

@@ -9,7 +9,9 @@
 * Fault injection for tests, from the environment (never set in production):
     XFLOW_FAULT=kill:<rank>:<step>      rank exits abruptly before that step
     XFLOW_FAULT=hang:<rank>:<step>      rank stops making progress (sleeps)
-    XFLOW_FAULT=drop_a2a:<rank>:<step>  rank skips the step's exchanges
+    XFLOW_FAULT=drop_a2a:<rank>:<step>  rank skips one exchange of that step (its
+                                        peers detect the out-of-step counts or
+                                        time out)
 """
 from __future__ import annotations
 
@@ -68,7 +70,7 @@ class FaultInjector:
                 self.kind, self.step = kind, int(step)
 
     def before_step(self, step: int) -> bool:
-        """Returns False when this rank must skip the step's exchanges."""
+        """Returns False when this rank must skip an exchange of the step."""
         if self.kind is None or step != self.step:
             return True
         if self.kind == "kill":
