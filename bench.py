@@ -73,6 +73,9 @@ def parse():
                          "GPU otherwise times its first steps at idle clocks (seen once in five "
                          "cold boxes: 315 vs 525 M samples/s).  Training warmup is exactly "
                          "--warmup steps, so logloss/table_keys do not depend on the box")
+    ap.add_argument("--monitor-lag", type=int, default=2,
+                    help="steps the host may run ahead of the table-capacity monitor "
+                         "(EngineConfig.monitor_lag)")
     ap.add_argument("--overlap", choices=["on", "off"], default="off",
                     help="generate batch t+1 on a side stream while step t runs (measured on "
                          "one MI355X: 2-4%% slower for the fused and the multi-rank step, the "
@@ -111,7 +114,7 @@ def main():
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
                                        v_init_scale=a.v_init_scale),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
-                                 max_slices=a.slices),
+                                 max_slices=a.slices, monitor_lag=a.monitor_lag),
                     device=device)
     if a.batch % a.slices:
         raise SystemExit("--batch must be a multiple of --slices")

@@ -98,6 +98,9 @@ class CpuBackend final : public Backend {
   void set_stream(void*) override {}
   void* stream() const override { return nullptr; }
   void* host_alloc(size_t bytes) override { return alloc(bytes); }
+  void snapshot(HostSnap* dst, const u32* mon, unsigned long long seq) override {
+    dst->word = pack_snapshot(*reinterpret_cast<const unsigned long long*>(mon), mon[2], mon[3], seq);
+  }
   void host_free(void* p) override { std::free(p); }
 
   void table_clear(const TableView& t) override {

@@ -2,8 +2,11 @@
 #include <cstdlib>
 #include "xflow/engine.h"
 
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <fstream>
 #include <stdexcept>
 
@@ -23,6 +26,14 @@ T* balloc(Backend& be, size_t n) {
 }
 
 constexpr char kMagic[8] = {'X', 'F', 'L', 'O', 'W', 'T', 'B', '1'};
+
+// XFLOW_NO_MONITOR=1: no per-step capacity snapshot (A/B of the monitor's
+// cost only; growth then relies on exact-size reads, overflow on the
+// epoch-end check)
+bool monitor_disabled() {
+  static const bool off = std::getenv("XFLOW_NO_MONITOR") != nullptr;
+  return off;
+}
 
 }  // namespace
 
@@ -56,8 +67,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   table_.overflow = overflow_ + 1;
   be.memset(mon_, 0, 4 * sizeof(u32));
   be.table_clear(table_);
-  snaps_ = static_cast<Snap*>(be.host_alloc(sizeof(Snap) * kSnaps));
-  for (int i = 0; i < kSnaps; ++i) snap_ev_[i] = be.event_create();
+  snaps_ = static_cast<HostSnap*>(be.host_alloc(sizeof(HostSnap) * kSnaps));
+  std::memset(snaps_, 0, sizeof(HostSnap) * kSnaps);
 
   // per-step dedup scratch
   const int64_t nnz = cfg_.max_nnz;
@@ -166,7 +177,6 @@ Engine::~Engine() {
     void* bp[] = {b.slots, b.nz, b.w, b.own_pos, b.own_idx};
     for (void* p : bp) be.free(p);
   }
-  for (void* e : snap_ev_) be.event_destroy(e);
   be.host_free(snaps_);
   for (StageSet& a : aset_) {
     void* ap[] = {a.keys, a.rowptr, a.fgid, a.labels};
@@ -438,6 +448,7 @@ void Engine::train_step(const BatchView& b) {
     aa.zero_after = false;
     aa.gstride = 2;
   }
+  attach_snapshot(aa);
   be_->table_apply(aa);
   end_step();
 }
@@ -870,6 +881,7 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
     aa.masks = recv_masks;
     if (stash) aa.nz_stash = sb.nz;
     aa.grp = g;
+    attach_snapshot(aa);
     be_->table_apply(aa);
     return;
   }
@@ -898,6 +910,7 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
     aa.masks = recv_masks ? recv_masks + off : nullptr;
     if (stash) aa.nz_stash = sb.nz + 2 * off;
     stash = false;
+    attach_snapshot(aa);
     be_->table_apply(aa);
   }
 }
@@ -919,53 +932,79 @@ void Engine::w_finish() { end_step(); }
 // ---------------------------------------------------------------------------
 // table capacity management
 // ---------------------------------------------------------------------------
+
 // Consume the recorded snapshots in order (each event completes after the
 // older ones: one stream); wait_upto >= 0 waits for snapshots up to that
 // sequence number.  A snapshot with an overflow flag raises: keys were
 // dropped (table: no slot within the probe bound; dedup or owner scratch:
 // full), so the run is invalid -- fail within monitor_lag steps, not at
 // epoch end.
+bool Engine::snap_ready(int64_t seq) const {
+  const volatile unsigned long long* p = &snaps_[seq % kSnaps].word;
+  const unsigned long long want = (unsigned long long)seq & ((1ull << (64 - kSnapSeqShift)) - 1);
+  return (*p >> kSnapSeqShift) == want;
+}
+
+// The next snapshot rides on this apply launch (its first wave stores it):
+// valid as long as no insert is queued between it and end_step.
+void Engine::attach_snapshot(ApplyArgs& aa) {
+  if (!be_->is_gpu() || monitor_disabled() || aa.n_max <= 0) return;
+  const int64_t seq = snap_seq_ + 1;
+  if (seq - 1 - snap_seen_ >= kSnaps) poll_snapshots(seq - kSnaps);  // (ring slot reuse)
+  aa.snap = &snaps_[seq % kSnaps];
+  aa.snap_mon = mon_;
+  aa.snap_seq = (unsigned long long)seq;
+  snap_carried_ = true;
+}
+
 void Engine::poll_snapshots(int64_t wait_upto) {
   while (snap_seen_ < snap_seq_) {
-    const int i = (int)(snap_seen_ % kSnaps);
-    if (!be_->event_done(snap_ev_[i])) {
-      if (snap_seen_ > wait_upto) break;
-      be_->event_wait(snap_ev_[i]);
+    const int64_t seq = snap_seen_ + 1;  // (sequence numbers start at 1)
+    const int i = (int)(seq % kSnaps);
+    if (!snap_ready(seq)) {
+      if (seq > wait_upto) break;
       ++monitor_waits_;
+      for (int spin = 0; !snap_ready(seq); ++spin) {
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else std::this_thread::yield();
+      }
     }
-    const Snap sn = snaps_[i];
-    known_size_ = (int64_t)sn.size;
+    const unsigned long long w = *reinterpret_cast<volatile unsigned long long*>(&snaps_[i].word);
+    const int64_t size = (int64_t)(w & 0xFFFFFFFFull);
+    const bool ovf0 = (w >> 32) & 1ull, ovf1 = (w >> 33) & 1ull;
+    known_size_ = size;
     known_adds_ = snap_adds_[i];
     ++snap_seen_;
-    if (sn.ovf[0] || sn.ovf[1]) {
+    if (ovf0 || ovf1) {
       char msg[320];
       std::snprintf(msg, sizeof(msg),
                     "xflow: %s overflow -- keys were dropped (table: %lld keys in 2^%d slots%s); "
                     "raise the capacity (table_log2_cap / max_log2_cap, max_nnz)",
-                    sn.ovf[1] ? "parameter table" : "dedup/owner scratch", (long long)sn.size,
+                    ovf1 ? "parameter table" : "dedup/owner scratch", (long long)size,
                     log2_cap_, cfg_.table_grow ? "" : ", growth disabled");
       throw std::runtime_error(msg);
     }
   }
 }
 
-// XFLOW_NO_MONITOR=1: no per-step snapshot (A/B of the monitor's cost only;
-// growth then relies on exact-size reads, overflow on the epoch-end check)
-static bool monitor_disabled() {
-  static const bool off = std::getenv("XFLOW_NO_MONITOR") != nullptr;
-  return off;
+// Close the next snapshot: it is the one an apply of this step carries, or
+// a tiny kernel writes it now; its insert bound is everything queued so far.
+void Engine::close_snapshot() {
+  const int64_t seq = snap_seq_ + 1;
+  if (!snap_carried_) {
+    if (seq - 1 - snap_seen_ >= kSnaps) poll_snapshots(seq - kSnaps);  // (ring slot reuse)
+    be_->snapshot(&snaps_[seq % kSnaps], mon_, (unsigned long long)seq);
+  }
+  snap_carried_ = false;
+  snap_adds_[seq % kSnaps] = queued_adds_;
+  snap_seq_ = seq;
 }
 
 void Engine::end_step() {
   if (monitor_disabled()) return;
-  if (snap_seq_ - snap_seen_ >= kSnaps) poll_snapshots(snap_seq_ - kSnaps);  // (ring slot reuse)
-  const int i = (int)(snap_seq_ % kSnaps);
-  be_->download_small(&snaps_[i], mon_, sizeof(Snap));
-  snap_adds_[i] = queued_adds_;
-  be_->event_record(snap_ev_[i]);
-  ++snap_seq_;
-  // bounded run-ahead: the snapshot monitor_lag steps back must be complete
-  poll_snapshots(snap_seq_ - 1 - cfg_.monitor_lag);
+  close_snapshot();
+  // bounded run-ahead: the snapshot monitor_lag steps back must be in
+  poll_snapshots(snap_seq_ - cfg_.monitor_lag);
 }
 
 // Before an inserting pull of n keys (at most n new): make sure the table can
@@ -974,6 +1013,9 @@ void Engine::end_step() {
 // host read the exact size (one sync), and grow if that is needed too.
 void Engine::guard_inserts(int64_t n) {
   if (n <= 0) return;
+  // an apply outside a step (e.g. a staleness-k flush) carried a snapshot:
+  // close it before these inserts, which it does not include
+  if (snap_carried_) close_snapshot();
   poll_snapshots(-1);
   const double lim = cfg_.grow_load * (double)table_.cap;
   if (cfg_.table_grow && (double)(known_size_ + (queued_adds_ - known_adds_) + n) > lim) {

@@ -120,9 +120,13 @@ class HipBackend final : public Backend {
     XF_HIP_CHECK(hipMemGetInfo(&fr, &tot));
     return fr;
   }
+  void snapshot(HostSnap* dst, const u32* mon, unsigned long long seq) override {
+    hip::launch_snapshot(dst, mon, seq, stream_);
+  }
+  // (coherent: the monitor polls snapshots the kernels write, no event)
   void* host_alloc(size_t bytes) override {
     void* p = nullptr;
-    XF_HIP_CHECK(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault));
+    XF_HIP_CHECK(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocCoherent));
     std::memset(p, 0, bytes ? bytes : 16);
     return p;
   }

@@ -31,6 +31,7 @@ void launch_scatter_u32(const u32* src, u32* dst, const u32* map, const int64_t*
 void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st);
 void launch_upload_small(void* dst, const void* src, size_t bytes, hipStream_t st);
 void launch_download_small(void* host_dst, const void* src, size_t bytes, hipStream_t st);
+void launch_snapshot(HostSnap* dst, const u32* mon, unsigned long long seq, hipStream_t st);
 void launch_table_clear(const TableView& t, hipStream_t st);
 void launch_table_export(const TableView& t, u64* keys_out, u32* words_out, int64_t max_rows,
                          unsigned long long* counter, hipStream_t st);

@@ -507,6 +507,30 @@ void launch_download_small(void* host_dst, const void* src, size_t bytes, hipStr
   XF_HIP_CHECK(hipGetLastError());
 }
 
+// Capacity snapshot (HostSnap): one 64-bit vector store (size, flags and
+// sequence number packed) to coherent host memory by lane 0 of the first
+// wave.  The apply kernels call it first: the step's pulls -- the only
+// inserts -- have completed, so the size and flags are final.
+__device__ __forceinline__ void store_snapshot(HostSnap* dst, const u32* mon,
+                                               unsigned long long seq) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const unsigned long long size = *reinterpret_cast<const unsigned long long*>(mon);
+  __hip_atomic_store(&dst->word, pack_snapshot(size, mon[2], mon[3], seq), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_snapshot(HostSnap* dst, const u32* mon, unsigned long long seq) {
+  store_snapshot(dst, mon, seq);
+}
+
+void launch_snapshot(HostSnap* dst, const u32* mon, unsigned long long seq, hipStream_t st) {
+  hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(64), 0, st, dst, mon, seq);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+#define XF_APPLY_SNAPSHOT(a) \
+  if ((a).snap) store_snapshot((a).snap, (a).snap_mon, (a).snap_seq)
+
 void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st) {
   if (n == 0) return;
   hipLaunchKernelGGL(k_fill_u64, dim3(grid_for((int64_t)n)), dim3(kBlock), 0, st, p, v, n);
@@ -918,6 +942,7 @@ __device__ __forceinline__ float norm_grad(float raw, const int32_t* slice_rows,
 // the dependent slot -> state chain better than per-lane ILP.
 template <bool kSlices>
 __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
+  XF_APPLY_SNAPSHOT(a);
   int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const FtrlParams fp = a.opt.ftrl;
@@ -975,6 +1000,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
 }
 
 __global__ void __launch_bounds__(kBlock) k_apply_generic(ApplyArgs a) {
+  XF_APPLY_SNAPSHOT(a);
   int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableView& t = a.table;
   const TableLayout& L = t.L;
@@ -1081,6 +1107,7 @@ void launch_owner_group(const OwnerGroupArgs& a, hipStream_t st) {
 // entry of a key takes (n, z) from its pull stash (or the table), pushes each
 // source's gradient in source order and writes the slot once.
 __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
+  XF_APPLY_SNAPSHOT(a);
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const FtrlParams fp = a.opt.ftrl;
@@ -1115,6 +1142,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
 // (7 waves per SIMD: <= 72 VGPRs without spills -- 77 at the default gave 6;
 // 8 waves spills: FM-8 +1.7 % / -1 %, profiles/r2_s3_fm_pull_apply_pipeline.txt)
 __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
+  XF_APPLY_SNAPSHOT(a);
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
   const TableLayout& L = a.table.L;
   const int S = a.S, ps = a.pstride, gs = a.gstride ? a.gstride : ps;

@@ -227,8 +227,29 @@ struct OwnerGroupArgs {
   u32* overflow = nullptr;
 };
 
+// A step's capacity snapshot (Engine's monitor) in coherent pinned host
+// memory, packed into ONE 64-bit word so a single store publishes it whole:
+// bits [0, 32) table size (<= 2^31 slots), bit 32/33 the scratch/table
+// overflow flags, bits [34, 64) the snapshot's sequence number.  No fence is
+// needed (a system-scope release would write back the L2 every step).
+struct HostSnap {
+  unsigned long long word;
+};
+constexpr int kSnapSeqShift = 34;
+XF_HD unsigned long long pack_snapshot(unsigned long long size, u32 ovf0, u32 ovf1,
+                                              unsigned long long seq) {
+  return (seq << kSnapSeqShift) | ((unsigned long long)(ovf1 != 0u) << 33) |
+         ((unsigned long long)(ovf0 != 0u) << 32) | (size & 0xFFFFFFFFull);
+}
+
 struct ApplyArgs {
   TableView table;
+  // optional: the kernel's first wave writes the capacity snapshot (size,
+  // overflow flags -- final once the step's pulls ran) before its work, so a
+  // step needs no extra launch or event for the monitor
+  HostSnap* snap = nullptr;
+  const u32* snap_mon = nullptr;   // device {size u64, overflow[2]}
+  unsigned long long snap_seq = 0;
   OptSpec opt;
   const u64* keys = nullptr;       // needed for latent init of un-pushed slots
   const u32* slots = nullptr;
@@ -351,6 +372,10 @@ class Backend {
   virtual void* stream() const = 0;
   // Bytes of device memory still free (table growth checks it first).
   virtual size_t free_memory() const { return ~(size_t)0; }
+  // Write a capacity snapshot {mon: size u64, overflow[2]} with sequence seq
+  // into pinned host memory, queued on the stream (a tiny kernel on HIP; the
+  // apply kernels do the same through ApplyArgs::snap when a step has one).
+  virtual void snapshot(HostSnap* dst, const u32* mon, unsigned long long seq) = 0;
 
   // Host-visible step snapshots (Engine's capacity monitor): pinned host
   // memory a kernel can write (download_small), and completion events on the

@@ -304,16 +304,17 @@ class Engine {
   bool lr16_layout() const;
 
   // capacity monitor (EngineConfig::table_grow): a ring of pinned snapshots
-  // {table size, overflow[2]} written by a kernel at each step end, each with
-  // an event and the cumulative insert bound queued before it
-  struct Snap {
-    unsigned long long size;
-    u32 ovf[2];
-  };
+  // (HostSnap: table size, overflow flags, sequence number), one per step,
+  // written by the step's apply kernel (or a tiny kernel when the step has
+  // none) and polled by the host -- no event, no extra launch; each comes
+  // with the cumulative insert bound queued before it
   static constexpr int kSnaps = 8;
-  Snap* snaps_ = nullptr;           // pinned host [kSnaps]
-  void* snap_ev_[kSnaps] = {};
+  HostSnap* snaps_ = nullptr;       // pinned host [kSnaps]
   int64_t snap_adds_[kSnaps] = {};
+  bool snap_carried_ = false;       // an apply since the last inserts carries the next snapshot
+  bool snap_ready(int64_t seq) const;
+  void close_snapshot();
+  void attach_snapshot(ApplyArgs& aa);
   int64_t snap_seq_ = 0;            // snapshots recorded
   int64_t snap_seen_ = 0;           // snapshots consumed (all older ones complete)
   int64_t known_size_ = 0;          // table size at the last consumed snapshot (or sync)

@@ -17,6 +17,7 @@ for i in 1 2; do
   XFLOW_NO_MONITOR=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_bench_nomon_$i.log 2>&1 || { echo "bench failed"; exit 1; }
   grep metric gpurun_out/${TAG}_bench_nomon_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('bench nomon', d['value']/1e6, d['ms_per_step'])"
 done
+[ -n "$SKIP_W8" ] && exit 0
 timeout -k 10 600 python tools/w8_emulate.py --out gpurun_out/${TAG}_w8.json > gpurun_out/${TAG}_w8.log 2>&1 || { echo "w8 failed"; tail -30 gpurun_out/${TAG}_w8.log; exit 1; }
 cat gpurun_out/${TAG}_w8.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_w8prof -o run -- python3 tools/w8_emulate.py > gpurun_out/${TAG}_w8prof.log 2>&1 || { echo "w8 profile failed"; tail -30 gpurun_out/${TAG}_w8prof.log; exit 1; }
