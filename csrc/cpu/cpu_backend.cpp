@@ -384,6 +384,14 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes) override {
+    const char* s = static_cast<const char*>(src);
+    char* d = static_cast<char*>(dst);
+    for (int64_t r = 0; r < rows; ++r)
+      for (int f = 0; f < F; ++f)
+        std::memcpy(d + ((int64_t)f * rows + r) * elem_bytes, s + (r * F + f) * elem_bytes,
+                    (size_t)elem_bytes);
+  }
   int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
                        int64_t max_rows) override {
     const int W = t.L.stride - 2;

@@ -42,6 +42,10 @@ void launch_table_rehash(const TableView& from, const TableView& to, hipStream_t
 void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long long* counter,
                           hipStream_t st);
 
+// kernels_layout.hip
+void launch_field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
+                        hipStream_t st);
+
 // kernels_model.hip
 void launch_forward_backward(const FwdArgs& a, hipStream_t st);
 void launch_slice_masks(const BatchView& b, const u32* pos, u32* tmask, hipStream_t st);

@@ -7,8 +7,14 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
+#include <atomic>
+#include <charconv>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
+#include <thread>
+#include <vector>
 #include <string>
 
 #include "../comm/rccl_comm.h"
@@ -82,6 +88,52 @@ PYBIND11_MODULE(_xflow_native, m) {
   m.doc() = "xflow-amd native core: HBM hash-table engine, gfx950 kernels, libffm reader";
 
   m.def("hip_available", &hip_backend_available);
+  // The reference's pred_<rank>_<block>.txt (lr_worker.cc:65-68: `pctr \t
+  // 1-label \t label`, ostream default float format = %g): formatted into one
+  // buffer and written with a single fwrite, without the GIL.
+  m.def("write_pred", [](const std::string& path, py::array_t<float> pctr,
+                         py::array_t<int32_t> labels) {
+    const int64_t n = pctr.size();
+    if (labels.size() != n) throw std::invalid_argument("write_pred: lengths differ");
+    const float* p = pctr.data();
+    const int32_t* y = labels.data();
+    py::gil_scoped_release nogil;
+    // chunks formatted in parallel (std::to_chars general/6 == printf "%g")
+    const int64_t per = 1 << 18;
+    const int64_t nchunk = (n + per - 1) / per;
+    std::vector<std::string> out((size_t)nchunk);
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+      for (int64_t c = next++; c < nchunk; c = next++) {
+        const int64_t lo = c * per, hi = lo + per < n ? lo + per : n;
+        std::string& b = out[(size_t)c];
+        b.resize((size_t)(hi - lo) * 24);
+        char* q = &b[0];
+        for (int64_t i = lo; i < hi; ++i) {
+          q = std::to_chars(q, q + 16, (double)p[i], std::chars_format::general, 6).ptr;
+          const int yi = y[i] ? 1 : 0;
+          *q++ = '\t';
+          *q++ = (char)('0' + (1 - yi));
+          *q++ = '\t';
+          *q++ = (char)('0' + yi);
+          *q++ = '\n';
+        }
+        b.resize((size_t)(q - &b[0]));
+      }
+    };
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int nt = (int)std::min<int64_t>(nchunk, hw ? (hw < 16 ? hw : 16) : 4);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (std::thread& t : th) t.join();
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw std::runtime_error("write_pred: cannot open " + path);
+    bool ok = true;
+    for (const std::string& b : out) ok = ok && std::fwrite(b.data(), 1, b.size(), f) == b.size();
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) throw std::runtime_error("write_pred: write failed " + path);
+  });
   m.def("feature_hash", [](py::bytes b) {
     std::string s = b;
     return feature_hash(s.data(), s.size());
@@ -300,6 +352,11 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("keys"), py::arg("grads"), py::arg("masks"), py::arg("offsets"), py::arg("S"),
            py::arg("buf") = 0, py::call_guard<py::gil_scoped_release>())
       .def("w_finish", &Engine::w_finish, py::call_guard<py::gil_scoped_release>())
+      .def("field_major",
+           [](Engine& e, uintptr_t src, uintptr_t dst, int64_t rows, int F, int elem_bytes) {
+             e.backend().field_major(P<const void>(src), P<void>(dst), rows, F, elem_bytes);
+           },
+           py::call_guard<py::gil_scoped_release>())
       .def("read_stats",
            [](Engine& e, bool reset, int which) { return stats_dict(e.read_stats(reset, which)); },
            py::arg("reset") = false, py::arg("which") = 0)

@@ -47,6 +47,8 @@ def main() -> int:
     ap.add_argument("--csr-only", action="store_true")
     ap.add_argument("--copy-threads", type=int, default=8)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--test-rows", type=int, default=65536,
+                    help="rows of the test shard rank 0 predicts (pred file + AUC/logloss)")
     a = ap.parse_args()
 
     import torch
@@ -60,7 +62,10 @@ def main() -> int:
     t0 = time.perf_counter()
     if not os.path.exists(tr):
         make_shard(tr, a.rows, a.fields, 1)
-        make_shard(te, 65536, a.fields, 2)
+    from xflow_amd.data import binfmt
+
+    if not os.path.exists(te) or binfmt.Shard(te).rows != a.test_rows:
+        make_shard(te, a.test_rows, a.fields, 2)
     print(f"shard ready ({time.perf_counter() - t0:.1f}s, "
           f"{os.path.getsize(tr) / 1e9:.2f} GB)", flush=True)
     dev = torch.device("cpu" if a.cpu or not torch.cuda.is_available() else "cuda:0")
@@ -75,8 +80,11 @@ def main() -> int:
                       copy_threads=a.copy_threads, metrics_file=mfile)
     t = Trainer(cfg, device=dev)
     t0 = time.perf_counter()
-    t.train()
-    wall = time.perf_counter() - t0
+    t.train_epochs(cfg.epochs)
+    t1 = time.perf_counter()
+    res = t.predict(0)  # device AUC/logloss + pred_0_0.txt
+    t2 = time.perf_counter()
+    wall = t2 - t0
     eps = [json.loads(l) for l in open(mfile) if '"epoch"' in l]
     eps = [e for e in eps if e.get("event") == "epoch"]
     print(json.dumps({"path": "xfb", "device": str(dev), "rows": a.rows,
@@ -84,7 +92,21 @@ def main() -> int:
                       "fixed_width": not a.csr_only,
                       "samples_per_s_by_epoch": [round(e["samples_per_s"]) for e in eps],
                       "train_logloss": [round(e["train_logloss"], 5) for e in eps],
+                      "train_s": round(t1 - t0, 2), "predict_rows": res["n"],
+                      "predict_s": round(t2 - t1, 3), "test_auc": round(res["auc"], 5),
                       "wall_s_incl_eval": round(wall, 2)}), flush=True)
+    # release the engine (device memory, pinned buffers) before interpreter
+    # teardown: under rocprofv3 a late hipFree from a module destructor crashed
+    t.close()
+    del t
+    import gc
+
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        if hasattr(torch._C, "_host_emptyCache"):
+            torch._C._host_emptyCache()  # pinned staging blocks
     return 0
 
 

@@ -71,6 +71,9 @@ def test_synthetic_criteo_shape(devname):
     np.testing.assert_array_equal(brm.keys.cpu().numpy().reshape(rows, cfg.fields), k)
     assert torch.equal(brm.labels, b.labels)
     assert torch.equal(brm.to_field_major().keys, b.keys)
+    # the engine's transpose (HIP: LDS-tiled kernel) == torch's
+    fm = brm.to_field_major(eng)
+    assert torch.equal(fm.keys, b.keys) and torch.equal(fm.fgid, b.fgid)
     y = b.labels.cpu().numpy()
     assert set(np.unique(y)) <= {0.0, 1.0} and 0.1 < y.mean() < 0.45
     # power-law: the 3-valued field has very few distinct keys, big fields many
@@ -273,3 +276,21 @@ def test_stamp_epoch_wrap(devname):
     for e in engines:
         assert not e.overflowed()
     np.testing.assert_allclose(engines[-1].pull(keys), engines[0].pull(keys), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+@pytest.mark.parametrize("rows,F", [(1000, 39), (64, 1), (130, 64), (7, 13)])
+def test_engine_field_major_transpose(devname, rows, F):
+    """Backend field_major ([rows][F] -> [F][rows], HIP: LDS tiles of 64 rows,
+    partial last tile) equals torch's transpose for u64 keys and i32 fgid."""
+    from xflow_amd.engine import Batch
+
+    dev = _dev(devname)
+    eng = Engine(ModelConfig(kind="mvm", v_dim=4), OptimConfig(),
+                 EngineConfig(table_log2_cap=10, max_rows=rows, max_nnz=rows * F), device=dev)
+    rng = np.random.default_rng(rows + F)
+    keys = torch.from_numpy(rng.integers(0, 1 << 62, rows * F, dtype=np.int64)).to(dev)
+    fg = torch.from_numpy(rng.integers(0, 1 << 30, rows * F, dtype=np.int32)).to(dev)
+    b = Batch(keys=keys, labels=torch.zeros(rows, device=dev), fgid=fg, nnz_per_row=F)
+    a, t = b.to_field_major(eng), b.to_field_major()
+    assert torch.equal(a.keys, t.keys) and torch.equal(a.fgid, t.fgid) and a.field_major

@@ -110,7 +110,11 @@ class BlockStream:
             return None
         slot, meta, rp_host, F = item
         compute = torch.cuda.current_stream(self.device)
-        self.copy.wait_stream(compute)
+        # No wait for the compute stream: block t+1's copies run while step t
+        # computes.  The pinned slot is reused only after the event behind its
+        # DMA, and the device tensors are allocated from the copy stream's
+        # pool with record_stream(compute) -- the caching allocator hands a
+        # block back only once the steps that read it have finished.
         out: Dict[str, object] = {}
         with torch.cuda.stream(self.copy):
             for name in self.names:

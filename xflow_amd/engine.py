@@ -73,14 +73,26 @@ class Batch:
         if self.field_major and self.row_ptr is not None:
             raise ValueError("field-major batches are fixed-width (no row_ptr)")
 
-    def to_field_major(self) -> "Batch":
-        """The same fixed-width batch stored field-major."""
+    def to_field_major(self, engine: "Engine | None" = None) -> "Batch":
+        """The same fixed-width batch stored field-major.  With an engine, its
+        backend transposes (HIP: an LDS-tiled kernel on the engine's stream,
+        csrc/hip/kernels_layout.hip); otherwise torch does."""
         if self.field_major:
             return self
         if self.row_ptr is not None:
             raise ValueError("only fixed-width batches have a field-major form")
         F = self.nnz_per_row
-        t = (lambda x: None if x is None else x.view(self.rows, F).t().contiguous().view(-1))
+        if engine is not None and F <= 64:
+            def t(x):
+                if x is None:
+                    return None
+                y = torch.empty_like(x)
+                engine._sync_stream()
+                engine.native.field_major(x.data_ptr(), y.data_ptr(), self.rows, F,
+                                          x.element_size())
+                return y
+        else:
+            t = (lambda x: None if x is None else x.view(self.rows, F).t().contiguous().view(-1))
         return Batch(keys=t(self.keys), labels=self.labels, fgid=t(self.fgid), nnz_per_row=F,
                      slice_rows=self.slice_rows, field_major=True)
 

@@ -136,7 +136,7 @@ class Trainer:
         fgid = up(blk["fgid"][:nnz]) if self._with_fgid else None
         if F:
             return Batch(keys=keys, labels=up(blk["labels"][:used]), fgid=fgid, nnz_per_row=F,
-                         slice_rows=slice_rows).to_field_major()
+                         slice_rows=slice_rows).to_field_major(self.engine)
         return Batch(keys=keys, labels=up(blk["labels"][:used]), row_ptr=up(rp), fgid=fgid,
                      slice_rows=slice_rows)
 
@@ -147,7 +147,7 @@ class Trainer:
         F = blk["nnz_per_row"] if self.cfg.fixed_width else 0
         if F:
             return Batch(keys=blk["keys"][:nnz], labels=blk["labels"][:used], fgid=fgid,
-                         nnz_per_row=F, slice_rows=slice_rows).to_field_major()
+                         nnz_per_row=F, slice_rows=slice_rows).to_field_major(self.engine)
         return Batch(keys=blk["keys"][:nnz], labels=blk["labels"][:used],
                      row_ptr=blk["row_ptr"][:used + 1], fgid=fgid, slice_rows=slice_rows)
 
@@ -355,14 +355,16 @@ class Trainer:
         if cfg.write_pred:
             os.makedirs(cfg.pred_dir or ".", exist_ok=True)
             ph, yh = p.cpu().numpy(), y.cpu().numpy().astype(np.int32)
-            with open(os.path.join(cfg.pred_dir or ".", "pred_%d_%d.txt" % (self.rank, block)),
-                      "w") as f:
-                for pi, yi in zip(ph.tolist(), yh.tolist()):
-                    f.write("%s\t%d\t%d\n" % (_fmt_float(pi), 1 - yi, yi))
+            nat.write_pred(os.path.join(cfg.pred_dir or ".", "pred_%d_%d.txt" % (self.rank, block)),
+                           np.ascontiguousarray(ph, dtype=np.float32), np.ascontiguousarray(yh))
             # predictions are on the host anyway: print the reference's exact
             # line, whose AUC depends on std::sort's (unspecified) order of
-            # equal pctr values; the device AUC breaks ties by prediction order
-            res = reference_auc(yh, ph)
+            # equal pctr values; the device AUC breaks ties by prediction order.
+            # (Above 2^22 rows the host sort costs more than the whole device
+            # eval and the reference's float accumulators drift: the device
+            # line, exact sums, is printed instead.)
+            if len(ph) <= (1 << 22):
+                res = reference_auc(yh, ph)
         _say(res["line"])
         self.metrics.log(event="eval", auc=res["auc"], auc_device=dev_auc,
                          ln_logloss=res["ln_logloss"], logloss_printed=res["logloss_printed"],
@@ -424,11 +426,6 @@ class Trainer:
         if getattr(self, "sharded", None) is not None:
             self.sharded.close()
         xdist.finalize()
-
-
-def _fmt_float(x: float) -> str:
-    """C++ ostream default float formatting (%g, 6 significant digits)."""
-    return "%g" % x
 
 
 if __name__ == "__main__":  # pragma: no cover
