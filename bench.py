@@ -41,6 +41,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=262144, help="rows per GPU per step")
     ap.add_argument("--model", default="lr", choices=["lr", "fm", "mvm"])
     ap.add_argument("--v-dim", type=int, default=8)
+    ap.add_argument("--fm-math", default="reference", choices=["reference", "standard"],
+                    help="FM interaction: the reference's (fm_worker.cc:159-202) or Rendle's "
+                         "standard 1/2 sum_k[(sum v)^2 - sum v^2] (BASELINE config 5)")
+    ap.add_argument("--fm-mfma", action="store_true",
+                    help="standard-math FM forward on the matrix cores (A/B option; measured "
+                         "slower than the VALU form, docs/DESIGN.md section 6)")
     ap.add_argument("--slices", type=int, default=1,
                     help="Hogwild slices per step (lr_worker.cc:190-199): every slice reads the "
                          "same weights, gradients normalised per slice, pushes applied per key in "
@@ -110,7 +116,7 @@ def main():
         a.batch = min(a.batch, 4096)
     synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed)
     nnz = a.batch * synth.fields
-    model = ModelConfig(kind=a.model, v_dim=a.v_dim)
+    model = ModelConfig(kind=a.model, v_dim=a.v_dim, fm_math=a.fm_math, fm_mfma=a.fm_mfma)
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
                                        v_init_scale=a.v_init_scale),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
@@ -234,13 +240,21 @@ def main():
                        "hashed_features": a.features, "table_slots_per_gpu": 2 ** log2_cap,
                        "backend": engine.backend_name,
                        "a2a_transport": sharded.transport if sharded is not None else "none",
-                       "input_overlap": overlap, "v_init_scale": a.v_init_scale},
+                       "input_overlap": overlap, "v_init_scale": a.v_init_scale,
+                       "table_growths": engine.table_growths},
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
             "table_load": table_keys / float(world * 2 ** log2_cap),
             "prefilled_keys": int(prefill_tot),
             "host_waits": int(sharded.host_waits) if sharded is not None else 0,
         }
+        if a.model == "fm":
+            out["config"]["v_dim"] = a.v_dim
+            out["config"]["fm_math"] = a.fm_math
+            # the path the interaction actually ran on (VALU per-row sums; the
+            # MFMA form is an A/B option, slower on this sparse gather shape)
+            out["config"]["fm_interaction"] = ("mfma" if a.fm_mfma and a.fm_math == "standard"
+                                               else "valu")
         if a.async_p2p:
             out["config"]["parallelism"] += "+async-p2p(staleness=1)"
             out["config"]["lambda1"] = a.lambda1

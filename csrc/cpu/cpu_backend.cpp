@@ -267,6 +267,7 @@ class CpuBackend final : public Backend {
       float loss = p - lab;
       if (a.pctr) a.pctr[r] = p;
       add_stats(a.stats, p, lab);
+      if (a.fx_bad && !(p >= 0.0f && p <= 1.0f)) *a.fx_bad |= 2u;
       if (!a.grad) continue;
       const int s = slice_of(b, r, a.S);
       for (int64_t j = 0, o = rs.base; j < rs.len; ++j, o += rs.step) {

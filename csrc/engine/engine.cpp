@@ -392,6 +392,7 @@ void Engine::train_step(const BatchView& b) {
   fa.model = cfg_.model;
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
+  fa.fx_bad = overflow_;
   set_reduction(fa);
   // slice bits from the reduction (LR / reference FM), else per occurrence
   if (masks && lr16) fa.red_masks = lr_mask_;
@@ -803,6 +804,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.model = cfg_.model;
   fa.S = S;
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
+  fa.fx_bad = overflow_;
   set_reduction(fa);
   if (masks && reduction_masks()) fa.red_masks = tmask_;
   else if (masks) be_->slice_masks(b, pos_, tmask_);
@@ -971,10 +973,14 @@ void Engine::poll_snapshots(int64_t wait_upto) {
     }
     const unsigned long long w = *reinterpret_cast<volatile unsigned long long*>(&snaps_[i].word);
     const int64_t size = (int64_t)(w & 0xFFFFFFFFull);
-    const bool ovf0 = (w >> 32) & 1ull, ovf1 = (w >> 33) & 1ull;
+    const bool ovf0 = (w >> 32) & 1ull, ovf1 = (w >> 33) & 1ull, bad = (w >> 34) & 1ull;
     known_size_ = size;
     known_adds_ = snap_adds_[i];
     ++snap_seen_;
+    if (bad && !ovf0 && !ovf1)
+      throw std::runtime_error(
+          "xflow: non-finite or out-of-range prediction / gradient sum (the model diverged); "
+          "the step's values were clamped");
     if (ovf0 || ovf1) {
       char msg[320];
       std::snprintf(msg, sizeof(msg),

@@ -165,6 +165,17 @@ template <int FX>
 __device__ __forceinline__ long long fx_from(float v) {
   return (long long)__builtin_rint((double)v * (double)(1ull << FX));
 }
+// Largest |v| a fixed-point input may have: 2^(62-FX-16), i.e. 2^16 such
+// inputs still sum inside int64 (LR: |loss| <= 1 << 2^10; FM: loss*vsum).
+// Out-of-range or non-finite inputs (a diverged model) are clamped -- NaN to
+// 0 -- so the conversion stays defined, and the caller flags them.
+template <int FX>
+__device__ __forceinline__ float fx_clamp(float v, u32& bad) {
+  constexpr float kLim = (float)(1ull << (62 - FX - 16));
+  if (fabsf(v) <= kLim) return v;
+  bad = 1u;
+  return v == v ? copysignf(kLim, v) : 0.0f;
+}
 template <int FX>
 __device__ __forceinline__ double fx_to_double(long long a) {
   return (double)a * (1.0 / (double)(1ull << FX));

@@ -58,7 +58,9 @@ __device__ __forceinline__ int red_active(const FwdArgs& a, int base) {
 // Per-row loss statistics, reduced per workgroup then one f64 atomic each.
 struct StatAcc {
   double ln = 0, l2 = 0, rows = 0, pos = 0;
+  u32 bad = 0;  // a non-finite / out-of-range prediction or gradient input (FwdArgs::fx_bad)
   __device__ void add(float p, float y) {
+    bad |= !(p >= 0.0f && p <= 1.0f) ? 1u : 0u;
     float pc = fminf(fmaxf(p, 1e-7f), 1.0f - 1e-7f);
     ln += (y > 0.5f) ? -(double)logf(pc) : -(double)logf(1.0f - pc);
     l2 += (y > 0.5f) ? (double)log2f(p) : (double)log2f(1.0f - p);
@@ -68,7 +70,8 @@ struct StatAcc {
 };
 
 template <int BLOCK>
-__device__ void flush_stats(StatAcc a, LossStats* out) {
+__device__ void flush_stats(StatAcc a, LossStats* out, u32* bad_flag = nullptr) {
+  if (bad_flag && __ballot(a.bad != 0u) && threadIdx.x % kWave == 0) atomicOr(bad_flag, 2u);
   if (!out) return;
   __shared__ double red[4][BLOCK / kWave];
   a.ln = wave_sum(a.ln);
@@ -198,6 +201,7 @@ struct ListAgg {
   u64* region;  // this workgroup's pair region
   u32 written;  // pairs written so far (workgroup-uniform)
   int shift = kShift;  // bucket = dest >> shift (RedGeom: runtime, >= kShift)
+  u32 bad = 0;   // a clamped fixed-point input (see fx_clamp), OR-ed into the stats flag
 
   __device__ __forceinline__ void init(int nb) {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
@@ -238,10 +242,10 @@ struct ListAgg {
     if (has) {
       h = insert(t, j, dest, claimed);
       atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV]),
-                (unsigned long long)fx_from<kFx>(loss));
+                (unsigned long long)fx_from<kFx>(fx_clamp<kFx>(loss, bad)));
       if constexpr (NV > 1)
         atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV + 1]),
-                  (unsigned long long)fx_from<kFx>(loss2));
+                  (unsigned long long)fx_from<kFx>(fx_clamp<kFx>(loss2, bad)));
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -423,7 +427,8 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
     for (int i = threadIdx.x, n = red_active(a, red_shift(1)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
-  flush_stats<BLOCK>(st, a.stats);
+  st.bad |= lagg.bad;
+  flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -547,7 +552,7 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
       }
     }
   }
-  flush_stats<BLOCK>(st, a.stats);
+  flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
 
@@ -997,7 +1002,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
   for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
     a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
-  flush_stats<BLOCK>(st, a.stats);
+  st.bad |= lagg.bad;
+  flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
@@ -1085,7 +1091,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
     for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
-  flush_stats<BLOCK>(st, a.stats);
+  st.bad |= lagg.bad;
+  flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -1172,7 +1179,7 @@ __global__ void __launch_bounds__(256) k_fm_fwd_mfma(FwdArgs a) {
       st.add(p, lab);
     }
   }
-  flush_stats<256>(st, a.stats);
+  flush_stats<256>(st, a.stats, a.fx_bad);
 }
 
 template <bool kGrad>
@@ -1475,7 +1482,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
       }
     }
   }
-  flush_stats<BLOCK>(st, a.stats);
+  flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
 // MVM bucket sums.  A bucket's 2^kRedShift destinations x D floats do not fit

@@ -166,6 +166,11 @@ struct FwdArgs {
   // loss*M_k/(1+v_ik), so records are (dest | row << 32), red_rowv[row] holds
   // T = loss*M ([rows][pstride]) and the sum divides Σ T by (1 + v) per key.
   float* red_rowv = nullptr;
+  // set to 2 (OR) when a row's prediction is non-finite or out of [0, 1], or
+  // a fixed-point input is out of range (a diverged model): the values are
+  // clamped before the fixed-point conversion and the capacity monitor
+  // raises (Engine::poll_snapshots)
+  u32* fx_bad = nullptr;
 };
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
@@ -230,16 +235,18 @@ struct OwnerGroupArgs {
 // A step's capacity snapshot (Engine's monitor) in coherent pinned host
 // memory, packed into ONE 64-bit word so a single store publishes it whole:
 // bits [0, 32) table size (<= 2^31 slots), bit 32/33 the scratch/table
-// overflow flags, bits [34, 64) the snapshot's sequence number.  No fence is
-// needed (a system-scope release would write back the L2 every step).
+// overflow flags, bit 34 the non-finite-loss flag (FwdArgs::fx_bad), bits
+// [35, 64) the snapshot's sequence number.  No fence is needed (a
+// system-scope release would write back the L2 every step).
 struct HostSnap {
   unsigned long long word;
 };
-constexpr int kSnapSeqShift = 34;
+constexpr int kSnapSeqShift = 35;
 XF_HD unsigned long long pack_snapshot(unsigned long long size, u32 ovf0, u32 ovf1,
                                               unsigned long long seq) {
-  return (seq << kSnapSeqShift) | ((unsigned long long)(ovf1 != 0u) << 33) |
-         ((unsigned long long)(ovf0 != 0u) << 32) | (size & 0xFFFFFFFFull);
+  return (seq << kSnapSeqShift) | ((unsigned long long)((ovf0 & 2u) != 0u) << 34) |
+         ((unsigned long long)(ovf1 != 0u) << 33) | ((unsigned long long)((ovf0 & 1u) != 0u) << 32) |
+         (size & 0xFFFFFFFFull);
 }
 
 struct ApplyArgs {

@@ -10,10 +10,13 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 500 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { echo "pytest gpu failed"; tail -40 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
   tail -1 gpurun_out/pytest_gpu_$TAG.log
 fi
-for m in "lr" "lr --slices 8" "lr --sharded" "lr --async" "fm --v-dim 8" "fm --v-dim 10" "mvm --v-dim 10" "lr --optimizer sgd"; do
+MODELS=${MODELS:-"lr|lr --slices 8|lr --sharded|lr --async|fm --v-dim 8|fm --v-dim 8 --fm-math standard|fm --v-dim 10|mvm --v-dim 10|lr --optimizer sgd"}
+IFS='|' read -ra MLIST <<< "$MODELS"
+for m in "${MLIST[@]}"; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --model $m > gpurun_out/bench_${TAG}.log 2>&1 || { echo "bench $m failed"; tail -20 gpurun_out/bench_${TAG}.log; exit 1; }
   python3 -c "import json,sys; d=json.loads(open('gpurun_out/bench_${TAG}.log').read().strip().splitlines()[-1]); print('$m', round(d['value']/1e6,1), 'M samples/s', round(d['ms_per_step'],3), 'ms/step logloss', round(d['logloss'],4))"
 done
+[ -n "$SKIP_PROF" ] && exit 0
 for m in "fm --v-dim 8" "mvm --v-dim 10"; do
   mt=$(echo $m | tr -d ' -')
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_$mt -o run -- python3 bench.py --steps 5 --warmup 2 --model $m > gpurun_out/prof_${TAG}_$mt.log 2>&1 || { echo "profile failed"; tail -20 gpurun_out/prof_${TAG}_$mt.log; exit 1; }

@@ -129,3 +129,21 @@ def test_growth_with_pending_staleness_buffers(tmp_path):
         np.testing.assert_array_equal(ka[oa], kb[ob])
         va, vb = np.load(tmp_path / f"v{r}_10.npy"), np.load(tmp_path / f"v{r}_16.npy")
         np.testing.assert_array_equal(va[oa].view(np.uint32), vb[ob].view(np.uint32))
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+def test_diverged_model_is_flagged(devname):
+    """A non-finite weight makes the forward's predictions non-finite: the
+    values are clamped before the fixed-point gradient sums (no undefined
+    conversion) and the capacity monitor raises within monitor_lag steps."""
+    dev = _dev(devname)
+    e = Engine(ModelConfig(kind="lr"), OptimConfig(),
+               EngineConfig(table_log2_cap=16, max_rows=512, max_nnz=512 * 12, monitor_lag=1),
+               device=dev)
+    k, rp, fg, lab = _fresh_csr(512, 8, seed=3, reuse=0.9)
+    e.train_step(to_batch(k, rp, fg, lab, dev))
+    e.push(np.unique(k)[:50], np.full(50, np.nan, np.float32))  # poison some weights
+    with pytest.raises(RuntimeError, match="non-finite"):
+        for _ in range(4):
+            e.train_step(to_batch(k, rp, fg, lab, dev))
+    assert e.overflowed()

@@ -25,6 +25,7 @@ import json
 import os
 import shutil
 import struct
+import warnings
 from typing import Callable, Optional
 
 import numpy as np
@@ -101,16 +102,28 @@ def save(engine, ckpt_dir: str, rank: int, world: int, meta: Optional[dict] = No
     return path
 
 
+# Fields that define what the table's state means: a resume must match them.
+# Everything else (fm_mfma picks a kernel; lr/alpha/beta/lambda1/lambda2 are
+# a schedule the user may change on resume) only warns.
+_LAYOUT_FIELDS = {"model": ("kind", "v_dim", "fm_math", "mvm_math"),
+                  "optim": ("kind", "v_init_scale", "sgd_v_init", "seed")}
+
+
 def check_compatible(engine, meta: dict) -> None:
-    """The checkpoint's model/optimizer config must equal the running one."""
+    """The checkpoint's layout-defining model/optimizer fields must equal the
+    running ones; other differences (hyperparameters, kernel choices) are
+    reported as warnings."""
     want = {"model": dataclasses.asdict(engine.model), "optim": dataclasses.asdict(engine.optim)}
     for k, cur in want.items():
         saved = meta.get(k)
         if saved is None:
             continue
         diff = {f: (saved.get(f), v) for f, v in cur.items() if f in saved and saved[f] != v}
+        hard = {f: d for f, d in diff.items() if f in _LAYOUT_FIELDS[k]}
+        if hard:
+            raise ValueError(f"checkpoint {k} config differs from the running one: {hard}")
         if diff:
-            raise ValueError(f"checkpoint {k} config differs from the running one: {diff}")
+            warnings.warn(f"resuming with a changed {k} config (saved, now): {diff}")
 
 
 def _check_header(engine, path: str, hdr) -> None:
