@@ -66,7 +66,9 @@ def parse():
     ap.add_argument("--sharded", action="store_true",
                     help="force the multi-rank (all-to-all) step even at 1 GPU (overhead probe)")
     ap.add_argument("--async", dest="async_p2p", action="store_true",
-                    help="config 4: staleness-1 pipelined steps, pushes over RCCL point-to-point")
+                    help="config 4: bounded-staleness steps, pushes over RCCL send/recv riding in "
+                         "the next step's key exchange")
+    ap.add_argument("--staleness", type=int, default=1, help="--async: staleness in steps")
     ap.add_argument("--v-init-scale", type=float, default=1e-2,
                     help="latent init N(0,1)*scale (ftrl.h:114-120: 1e-2).  MVM on 39 fields "
                          "at 1e-2 has a field product that underflows to 0 (no gradient "
@@ -139,7 +141,8 @@ def main():
         from xflow_amd.parallel.async_p2p import AsyncShardedEngine
         from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
-        sharded = AsyncShardedEngine(engine) if a.async_p2p else ShardedEngine(engine)
+        sharded = (AsyncShardedEngine(engine, staleness=a.staleness) if a.async_p2p
+                   else ShardedEngine(engine))
     overlap = a.overlap == "on"
     if not overlap and sharded is not None:
         # double-buffered batches on the compute stream
@@ -256,7 +259,7 @@ def main():
             out["config"]["fm_interaction"] = ("mfma" if a.fm_mfma and a.fm_math == "standard"
                                                else "valu")
         if a.async_p2p:
-            out["config"]["parallelism"] += "+async-p2p(staleness=1)"
+            out["config"]["parallelism"] += "+async-p2p(staleness=%d)" % a.staleness
             out["config"]["lambda1"] = a.lambda1
             out["nonzero_weights"] = int(nonzero)
         print(json.dumps(out), flush=True)

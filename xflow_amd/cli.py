@@ -47,8 +47,16 @@ def build_parser() -> argparse.ArgumentParser:
                     help="one FTRL push of the summed slice gradients per step")
     ap.add_argument("--no-init-push", action="store_true")
     ap.add_argument("--async", dest="async_p2p", action="store_true",
-                    help="multi-rank: staleness-1 pipelined steps, pushes over RCCL P2P")
-    ap.add_argument("--log2-cap", type=int, default=22, help="table slots per rank = 2^N")
+                    help="multi-rank: bounded-staleness steps, pushes over RCCL send/recv riding "
+                         "in the next exchange (BASELINE config 4)")
+    ap.add_argument("--staleness", type=int, default=1,
+                    help="--async: pulls miss the previous N steps' pushes (1..7)")
+    ap.add_argument("--log2-cap", type=int, default=22,
+                    help="initial table slots per rank = 2^N (the table grows)")
+    ap.add_argument("--max-log2-cap", type=int, default=0,
+                    help="growth limit 2^N slots per rank (0: 2^31, or what free HBM allows)")
+    ap.add_argument("--no-table-grow", action="store_true",
+                    help="fixed table capacity: an overflow raises within two steps")
     ap.add_argument("--train-block-bytes", type=int, default=2 << 20)
     ap.add_argument("--test-block-bytes", type=int, default=0)
     ap.add_argument("--resident", action="store_true",
@@ -88,12 +96,13 @@ def config_from_args(a) -> TrainConfig:
         init_push=not a.no_init_push, pred_dir=a.pred_dir, write_pred=not a.no_pred_file,
         checkpoint_dir=a.save,
         save_every=a.save_every, resume_dir=a.resume,
-        metrics_file=a.metrics, async_p2p=a.async_p2p,
+        metrics_file=a.metrics, async_p2p=a.async_p2p, staleness=a.staleness,
         model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math,
                           fm_mfma=a.fm_mfma),
         optim=OptimConfig(kind=a.optimizer, alpha=a.alpha, beta=a.beta, lambda1=a.lambda1,
                           lambda2=a.lambda2, lr=a.lr),
-        engine=EngineConfig(table_log2_cap=a.log2_cap, sum_slices=a.sum_slices))
+        engine=EngineConfig(table_log2_cap=a.log2_cap, sum_slices=a.sum_slices,
+                            max_log2_cap=a.max_log2_cap, table_grow=not a.no_table_grow))
 
 
 def main(argv=None) -> int:

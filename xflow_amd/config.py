@@ -120,7 +120,8 @@ class TrainConfig:
     save_every: int = 0          # versioned checkpoint every N epochs (checkpoint.publish)
     resume_dir: str = ""         # versioned checkpoint root: resume from LATEST, save there
     metrics_file: str = ""
-    async_p2p: bool = False      # staleness-1 pipelined steps, pushes over RCCL point-to-point
+    async_p2p: bool = False      # bounded-staleness steps, pushes over RCCL point-to-point
+    staleness: int = 1           # async_p2p: pulls miss the previous N steps' pushes
     model: ModelConfig = field(default_factory=ModelConfig)
     optim: OptimConfig = field(default_factory=OptimConfig)
     engine: EngineConfig = field(default_factory=EngineConfig)

@@ -92,7 +92,7 @@ class Trainer:
         if self.world > 1 and cfg.async_p2p:
             from xflow_amd.parallel.async_p2p import AsyncShardedEngine
 
-            self.sharded = AsyncShardedEngine(self.engine)
+            self.sharded = AsyncShardedEngine(self.engine, staleness=cfg.staleness)
         elif self.world > 1:
             from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
