@@ -117,10 +117,16 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // atomic-free gradient reduction (FwdArgs::red_*): LR (1 value per key) and
   // reference-math FM (2 values per key, 16-byte records)
   const bool fm_ref = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference;
+  // standard FM: vector records (dest, 1 + D sums) per (key, slice, column)
+  // and workgroup (k_fm_std_red), at most one per occurrence
+  const bool fm_std = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard;
   const bool mvm = cfg_.model.kind == kMVM;
-  if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref || mvm)) {
-    const int nv = fm_ref ? 2 : 1, shift = red_shift(nv);
-    const int group_rows = fm_ref ? kFmGroupRows : (mvm ? kMvmGroupRows : kLrGroupRows);
+  if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref || fm_std || mvm)) {
+    const int nv = fm_ref ? 2 : (fm_std ? 1 + cfg_.model.v_dim : 1), shift = red_shift(nv);
+    // u64 words per record slot: nv for LR / reference FM, the vector record for standard FM
+    const int recw = fm_std ? vec_rec_words(nv) / 2 : nv;
+    const int group_rows = fm_ref ? kFmGroupRows
+                                  : (mvm ? kMvmGroupRows : (fm_std ? kFmStdMinGroupRows : kLrGroupRows));
     // (the trash slot's occurrences are never reduced: FwdArgs::trash_pos)
     // Buckets of 2^shift dests at the allocated capacity; beyond
     // kRedMaxBuckets the device widens the buckets (FwdArgs::red_bcap) and
@@ -136,8 +142,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     if (nb <= kRedMaxBuckets && dests < (1ull << 32)) {
       const int64_t groups = (cfg_.max_rows + group_rows - 1) / group_rows;
       red_nb_ = nb;
-      red_pairs_ = balloc<u64>(be, (size_t)nnz * nv);  // nv u64 words per record
-      red_sorted_ = balloc<u64>(be, (size_t)nnz * nv);
+      red_pairs_ = balloc<u64>(be, (size_t)nnz * recw);
+      red_sorted_ = balloc<u64>(be, (size_t)nnz * recw);
       red_hist_ = balloc<u32>(be, (size_t)nb * groups);
       red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
       red_count_ = balloc<u32>(be, groups);

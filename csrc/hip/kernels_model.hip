@@ -239,13 +239,18 @@ struct ListAgg {
     if (threadIdx.x == 0) nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
     bool claimed = false;
     int h = 0;
+    long long v[NV];
+    v[0] = 0ll;
+    if constexpr (NV > 1) v[1] = 0ll;
     if (has) {
       h = insert(t, j, dest, claimed);
-      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV]),
-                (unsigned long long)fx_from<kFx>(fx_clamp<kFx>(loss, bad)));
-      if constexpr (NV > 1)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV + 1]),
-                  (unsigned long long)fx_from<kFx>(fx_clamp<kFx>(loss2, bad)));
+      v[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
+      if constexpr (NV > 1) v[1] = fx_from<kFx>(fx_clamp<kFx>(loss2, bad));
+    }
+    if (has) {
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV + c]), (unsigned long long)v[c]);
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -588,7 +593,16 @@ __global__ void __launch_bounds__(kBlock) k_red_scan(u32* __restrict__ hist, int
 constexpr int kRedBlock = 1024;
 constexpr int kRedUnroll = 4;
 
-// record of one (dest, NV values) partial sum
+// record of one (dest, NV values) partial sum; NV >= 3: standard-FM vector
+// records (dest, v_0 .. v_{NV-1}, pad) of vec_rec_words(NV) words
+template <int W>
+struct VecRec {
+  uint4 q[W / 4];
+};
+template <int NV> struct VecRedRec {
+  using T = VecRec<vec_rec_words(NV)>;
+  __device__ static u32 dest(const T& r) { return r.q[0].x; }
+};
 template <int NV> struct RedRec;
 template <> struct RedRec<1> {
   using T = u64;
@@ -599,7 +613,7 @@ template <> struct RedRec<2> {
   __device__ static u32 dest(T r) { return r.x; }
 };
 
-template <int NV>
+template <int NV, typename R = RedRec<NV>>
 __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows_per_group,
                                                            const void* __restrict__ pairs,
                                                            const u32* __restrict__ count,
@@ -608,7 +622,6 @@ __global__ void __launch_bounds__(kRedBlock) k_red_scatter(BatchView b, int rows
                                                            u32* __restrict__ start, int nb,
                                                            void* __restrict__ sorted,
                                                            RedGeom geom) {
-  using R = RedRec<NV>;
   using T = typename R::T;
   const int kShift = geom.shift(red_shift(NV));
   __shared__ u32 cur[kRedMaxBuckets];
@@ -1006,6 +1019,280 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
+// Standard-math FM (Rendle) on the atomic-free reduction.  The occurrence
+// gradient has 1+D components (loss; loss*(vs_k - v_k)), all of them needed
+// per key.  Each column's contributions are summed per (key, slice) in an LDS
+// table with 1+D fixed-point accumulators per slot (one insert, 1+D integer
+// atomics per occurrence; deterministic), and the flush emits one vector
+// record (dest, 1+D sums) per (key, slice, column) -- 48 bytes at D = 8 --
+// which k_red_scan / k_red_scatter partition by dest bucket and
+// k_red_sum_vec sums into the slot-indexed gradient rows.  Before: LDS column
+// tables flushed with (1+D) global float atomics per (key, column,
+// workgroup), 1.15 ms of a 1.6 ms FM-8 step.
+// One LDS table (flushed, then a barrier, per column): 2x the rows of a
+// double-buffered table for the same LDS -- larger workgroups aggregate hot
+// keys over more rows (A/B: 128 rows per workgroup -21 %, 256 -> 512 below)
+constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128); }
+
+template <int D, int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
+  constexpr int PS = fm_ps(D);
+  constexpr int NV = 1 + D;
+  constexpr int LOG2 = ilog2c(2 * BLOCK);
+  constexpr int kSlots = 1 << LOG2;
+  constexpr int kFx = FxBits<1>::kFx;
+  __shared__ u64 s_tag[1][kSlots];
+  __shared__ long long s_acc[1][kSlots * NV];
+  __shared__ unsigned short s_list[1][BLOCK];
+  __shared__ u32 s_hist[kRedMaxBuckets];
+  __shared__ u32 s_nlist[3];
+  __shared__ int s_wmax[BLOCK / kWave];
+  const BatchView& b = a.batch;
+  const u32* __restrict__ pos = a.pos;
+  const float4* __restrict__ wp4 = reinterpret_cast<const float4*>(a.wpull);
+  const int64_t r = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool active = r < b.rows;
+  RowSpan rs;
+  if (active) rs = row_span(b, r);
+  const int len = rs.len;
+  const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
+  using Rec = typename VecRedRec<NV>::T;
+  constexpr int W = vec_rec_words(NV);
+  Rec* region = reinterpret_cast<Rec*>(a.red_pairs) +
+                (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
+  const RedGeom geom = red_geom(a);
+  const int shift = geom.shift(red_shift(NV));
+  for (int i = threadIdx.x; i < kSlots; i += BLOCK) {
+    s_tag[0][i] = ~0ull;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = 0ll;
+  }
+  for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) s_hist[i] = 0u;
+  if (threadIdx.x < 3) s_nlist[threadIdx.x] = 0u;
+  int maxlen;
+  if (!b.row_ptr) {
+    maxlen = b.nnz_per_row;
+    __syncthreads();
+  } else {
+    const int m = wave_max(len);
+    if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
+    __syncthreads();
+    maxlen = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
+  }
+  StatAcc st;
+  float loss = 0.0f;
+  float vs[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+  if (active) {
+    float wx = 0.0f, vp = 0.0f;
+    for (int j = 0; j < len; ++j) {
+      const float4* src = wp4 + (size_t)pos[rs.at(j)] * (PS / 4);
+      float w[PS];
+#pragma unroll
+      for (int q = 0; q < PS / 4; ++q) {
+        const float4 v4 = src[q];
+        w[4 * q] = v4.x;
+        w[4 * q + 1] = v4.y;
+        w[4 * q + 2] = v4.z;
+        w[4 * q + 3] = v4.w;
+      }
+      wx += w[0];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        vs[k] += w[1 + k];
+        vp += w[1 + k] * w[1 + k];
+      }
+    }
+    float sq = 0.0f;
+#pragma unroll
+    for (int k = 0; k < D; ++k) sq += vs[k] * vs[k];
+    const float p = sigmoid_ref(wx + 0.5f * (sq - vp));
+    const float lab = b.labels[r];
+    loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+  }
+  const u32 sl = active ? (u32)slice_of(b, r, a.S) : 0u;
+  const u32 S = (u32)a.S;
+  const int lane = lane_id();
+  u32 written = 0, bad = 0;
+  for (int j = 0; j < maxlen; ++j) {
+    const int t = 0;
+    if (threadIdx.x == 0) s_nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
+    const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
+    const bool has = pj != a.trash_pos;
+    bool claimed = false;
+    u32 h = 0;
+    long long vals[NV];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) vals[c] = 0ll;
+    if (has) {
+      const u32 dest = pj * S + sl;
+      const u64 key = ((u64)(u32)j << 32) | dest;
+      h = (dest * 0x9E3779B1u) >> (32 - LOG2);
+      while (true) {  // <= BLOCK keys per column in 2 * BLOCK slots: terminates
+        const u64 cur = s_tag[t][h];
+        if (cur == key) break;
+        if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
+          const u64 old = atomicCAS((unsigned long long*)&s_tag[t][h], (unsigned long long)cur,
+                                    (unsigned long long)key);
+          if (old == cur) {
+            claimed = true;
+            break;
+          }
+          if (old == key) break;
+        }
+        h = (h + 1) & (kSlots - 1);
+      }
+      float w[PS];
+      {
+        const float4* src = wp4 + (size_t)pj * (PS / 4);
+#pragma unroll
+        for (int q = 0; q < PS / 4; ++q) {
+          const float4 v4 = src[q];
+          w[4 * q] = v4.x;
+          w[4 * q + 1] = v4.y;
+          w[4 * q + 2] = v4.z;
+          w[4 * q + 3] = v4.w;
+        }
+      }
+      vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
+#pragma unroll
+      for (int k = 0; k < D; ++k)
+        vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(loss * (vs[k] - w[1 + k]), bad));
+    }
+    if (has) {
+      long long* acc = &s_acc[t][h * NV];
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)vals[c]);
+    }
+    const unsigned long long m = __ballot(claimed);
+    if (m) {
+      const int leader = __ffsll((long long)m) - 1;
+      u32 base = 0;
+      if (lane == leader) base = atomicAdd(&s_nlist[j % 3], (u32)__popcll(m));
+      base = __shfl(base, leader);
+      if (claimed) s_list[t][base + (u32)__popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)h;
+    }
+    lds_barrier();
+    const u32 n = s_nlist[j % 3];
+    for (u32 i = threadIdx.x; i < n; i += BLOCK) {
+      const int hh = s_list[t][i];
+      const u32 d = (u32)s_tag[t][hh];
+      u32 wv[W];
+      wv[0] = d;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        long long* ap = &s_acc[t][hh * NV + c];
+        wv[1 + c] = __float_as_uint((float)fx_to_double<kFx>(*ap));
+        *ap = 0ll;
+      }
+#pragma unroll
+      for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
+      Rec rec;
+#pragma unroll
+      for (int q = 0; q < W / 4; ++q)
+        rec.q[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
+      region[written + i] = rec;
+      atomicAdd(&s_hist[d >> shift], 1u);
+    }
+    written += n;
+    lds_barrier();  // (one table: flushed before the next column inserts)
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.red_count[blockIdx.x] = written;
+  for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK)
+    a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
+  st.bad |= bad;
+  flush_stats<BLOCK>(st, a.stats, a.fx_bad);
+}
+
+// Sums of a bucket's vector records: units of kR dests (as k_red_sum) with
+// (1+D) int64 accumulators per dest in LDS; every dest a record reached gets
+// its whole gradient row (pad components 0) -- the rows are the step's
+// (slot, slice) gradients the apply reads.
+template <int D>
+__global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restrict__ sorted,
+                                                           const u32* __restrict__ start,
+                                                           float* __restrict__ grad,
+                                                           RedGeom geom, int nb) {
+  constexpr int NV = 1 + D;
+  constexpr int PS = fm_ps(D);
+  constexpr int kShift = red_shift(NV);
+  constexpr u32 kR = 1u << kShift;
+  constexpr int kFx = FxBits<1>::kFx;
+  constexpr int W = vec_rec_words(NV);
+  using Rec = typename VecRedRec<NV>::T;
+  __shared__ long long acc[kR * NV];
+  __shared__ u32 seen[kR / 32];
+  const Rec* src = static_cast<const Rec*>(sorted);
+  const int shift = geom.shift(kShift);
+  const u32 act = (u32)geom.active(shift, nb);
+  const u32 units = act << (shift - kShift);
+  for (u32 id = blockIdx.x; id < units; id += gridDim.x) {
+    const u32 bk = id % act, sub = id / act;
+    const u32 beg = start[bk], end = start[bk + 1];
+    if (beg == end) continue;  // (block-uniform)
+    const u64 lo = ((u64)bk << shift) + ((u64)sub << kShift);
+    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
+    for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) seen[i] = 0u;
+    lds_barrier();
+    for (u32 i = beg + threadIdx.x; i < end; i += kRedBlock) {
+      const Rec r = src[i];
+      const u64 l = (u64)r.q[0].x - lo;
+      if (l >= kR) continue;  // (another sub-unit's dest)
+      u32 wv[W];
+#pragma unroll
+      for (int q = 0; q < W / 4; ++q) {
+        wv[4 * q] = r.q[q].x;
+        wv[4 * q + 1] = r.q[q].y;
+        wv[4 * q + 2] = r.q[q].z;
+        wv[4 * q + 3] = r.q[q].w;
+      }
+      long long* ap = acc + l * NV;
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
+                  (unsigned long long)fx_from<kFx>(__uint_as_float(wv[1 + c])));
+      atomicOr(&seen[l >> 5], 1u << (l & 31));
+    }
+    lds_barrier();
+    for (u32 l = threadIdx.x; l < kR; l += kRedBlock) {
+      if (!((seen[l >> 5] >> (l & 31)) & 1u)) continue;
+      float o[PS];
+#pragma unroll
+      for (int c = 0; c < PS; ++c) o[c] = c < NV ? (float)fx_to_double<kFx>(acc[l * NV + c]) : 0.0f;
+      float4* g4 = reinterpret_cast<float4*>(grad + (lo + l) * PS);
+#pragma unroll
+      for (int q = 0; q < PS / 4; ++q) g4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    }
+    lds_barrier();  // (the next unit reinitialises what this one read)
+  }
+}
+
+template <int D>
+static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
+  constexpr int BLOCK = fmstd_block(D);
+  constexpr int NV = 1 + D;
+  const int groups = (int)((a.batch.rows + BLOCK - 1) / BLOCK);
+  hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
+  const RedGeom geom = red_geom(a);
+  hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
+                     a.red_tot, geom, red_shift(NV));
+  u32* start = a.red_tot + a.red_nb + 1;
+  hipLaunchKernelGGL((k_red_scatter<NV, VecRedRec<NV>>), dim3(groups), dim3(kRedBlock), 0, st,
+                     a.batch, BLOCK, static_cast<const void*>(a.red_pairs), a.red_count,
+                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
+                     geom);
+  const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
+  hipLaunchKernelGGL(k_red_sum_vec<D>, dim3(grid), dim3(kRedBlock), 0, st,
+                     static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb);
+}
+
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
 // pulled row is (w, Σ_k v_k, Σ_k v_k^2, 0), one dwordx4 -- the reference's
 // y = Σ w + (Σ_f Σ_k v)^2 - Σ_f Σ_k v^2 (fm_worker.cc:159-202) needs nothing
@@ -1182,6 +1469,13 @@ __global__ void __launch_bounds__(256) k_fm_fwd_mfma(FwdArgs a) {
   flush_stats<256>(st, a.stats, a.fx_bad);
 }
 
+// XFLOW_FMSTD_ATOMICS=1 keeps standard-math FM on the column-table + global
+// float atomic backward (A/B)
+static bool fmstd_atomics_forced() {
+  static const bool forced = std::getenv("XFLOW_FMSTD_ATOMICS") != nullptr;
+  return forced;
+}
+
 template <bool kGrad>
 static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
@@ -1213,12 +1507,17 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     }
     return;
   }
+  // standard math: per-component records through the LR reduction pipeline
+  const bool red_std = agg && a.model.fm_math == kFmStandard && a.red_pairs && a.red_nb > 0 &&
+                       a.red_nb <= kRedMaxBuckets && !a.red_masks && !fmstd_atomics_forced();
   switch (a.model.v_dim) {
 #define XF_FM_CASE(DD)                                                                   \
   case DD: {                                                                             \
     constexpr int B = fm_block(DD);                                                      \
     int g = (int)((a.batch.rows + B - 1) / B);                                           \
-    if (red) {                                                                           \
+    if (red_std) {                                                                       \
+      launch_fmstd_reduction<DD>(a, st);                                                 \
+    } else if (red) {                                                                    \
       constexpr int R = kFmGroupRows;                                                    \
       const int gr = (int)((a.batch.rows + R - 1) / R);                                  \
       hipLaunchKernelGGL((k_fm_red<DD, R>), dim3(gr), dim3(R), 0, st, a);                \

@@ -175,9 +175,18 @@ struct FwdArgs {
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
 // destinations per bucket for NV aggregated values per key (NV x 2^shift x 4 B <= 64 KB)
-constexpr int red_shift(int nv) { return nv == 1 ? kRedShift : kRedShift - 1; }
+// (nv >= 3: standard-FM vector records, 1 + D values: 2^shift x nv int64 in
+// at most ~114 KB of LDS)
+constexpr int red_shift(int nv) {
+  return nv == 1 ? kRedShift : (nv == 2 ? kRedShift - 1 : (nv <= 14 ? 10 : (nv <= 28 ? 9 : 8)));
+}
+// 32-bit words of a standard-FM vector record (dest + nv values), 16-B padded
+constexpr int vec_rec_words(int nv) { return (1 + nv + 3) & ~3; }
 constexpr int kLrGroupRows = 1024;  // rows per LR workgroup on the reduction path
 constexpr int kFmGroupRows = 1024;  // rows per reference-FM workgroup on the reduction path (A/B: 512 -1.8 %)
+// smallest rows per standard-FM producer workgroup (v_dim > 16; 256 up to
+// v_dim 10): sizes the reduction's per-workgroup histogram
+constexpr int kFmStdMinGroupRows = 128;
 constexpr int kMvmGroupRows = 512;  // rows per MVM workgroup on the reduction path (A/B: 256 -1.5 %, 1024 same)
 
 struct PullArgs {

@@ -196,3 +196,24 @@ def test_c_api_gpu_matches_cpu(tmp_path):
             os.chdir(cwd)
     (la, aa), (lb, ab) = res
     assert abs(la - lb) <= 1e-4 * abs(la) and abs(aa - ab) <= 2e-3
+
+
+def test_cli_async_staleness_and_fixed_table_flags(tmp_path):
+    """--async --staleness 2 on 2 gloo ranks trains and predicts; with a
+    fixed tiny table (--no-table-grow) the run fails fast with an overflow."""
+    env = dict(os.environ, PYTHONPATH=ROOT, HIP_VISIBLE_DEVICES="")
+    base = ["bash", os.path.join(ROOT, "run_ps_local.sh"), "0", "2", "2"]
+    r = subprocess.run(base, cwd=tmp_path, capture_output=True, text=True, timeout=240,
+                       env=dict(env, XFLOW_FLAGS="--threads 4 --cpu --async --staleness 2"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "logloss:" in r.stdout
+    r = subprocess.run([sys.executable, "-m", "xflow_amd.cli", os.path.join(DATA, "small_train"),
+                        os.path.join(DATA, "small_test"), "0", "1", "--threads", "4", "--cpu",
+                        "--log2-cap", "6", "--no-table-grow"], cwd=tmp_path, capture_output=True,
+                       text=True, timeout=240, env=env)
+    assert r.returncode != 0 and "overflow" in r.stderr, r.stderr[-2000:]
+    r = subprocess.run([sys.executable, "-m", "xflow_amd.cli", os.path.join(DATA, "small_train"),
+                        os.path.join(DATA, "small_test"), "0", "1", "--threads", "4", "--cpu",
+                        "--log2-cap", "6"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]

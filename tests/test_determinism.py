@@ -21,7 +21,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _train(kind, dev, rows, small, steps_small, steps, v_dim=8, gpu_batches=None, S=1):
-    eng = Engine(ModelConfig(kind=kind, v_dim=v_dim), OptimConfig(),
+    fm_math = "standard" if kind == "fm-std" else "reference"
+    kind = "fm" if kind == "fm-std" else kind
+    eng = Engine(ModelConfig(kind=kind, v_dim=v_dim, fm_math=fm_math), OptimConfig(),
                  EngineConfig(table_log2_cap=23, max_rows=rows, max_nnz=rows * 39, max_slices=S),
                  device=dev)
     caps = []
@@ -54,11 +56,13 @@ def _batches(rows, small, steps_small, steps, S=1):
 
 @pytest.mark.parametrize("kind,rows,small,steps_small,steps,S",
                          [("lr", 262144, 32768, 4, 22, 1), ("fm", 65536, 8192, 3, 8, 1),
-                          ("lr", 262144, 32768, 3, 10, 8), ("fm", 65536, 8192, 2, 6, 4)])
+                          ("lr", 262144, 32768, 3, 10, 8), ("fm", 65536, 8192, 2, 6, 4),
+                          ("fm-std", 65536, 8192, 2, 6, 1), ("fm-std", 65536, 8192, 2, 6, 4)])
 def test_bench_scale_deterministic_and_matches_cpu(gpu_device, kind, rows, small, steps_small,
                                                    steps, S):
     """S > 1: the reference's Hogwild slices (lr_worker.cc:190-199) at bench
-    scale stay on the atomic-free fixed-point reduction."""
+    scale stay on the atomic-free fixed-point reduction.  fm-std: standard-math
+    FM, per-component records through the same reduction (k_fm_std_red)."""
     batches = _batches(rows, small, steps_small, steps, S)
     k1, w1, caps1, st1 = _train(kind, gpu_device, rows, small, steps_small, steps,
                                 gpu_batches=batches, S=S)
