@@ -720,7 +720,10 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
 // 4x the step's entries, so the load stays below 0.75.
 bool Engine::group_entries(const u64* recv_keys, int64_t n, int buf,
                            const std::vector<int64_t>& offs) {
+  // (EngineConfig::owner_group: grouping is opt-in; XFLOW_OWNER_GROUP=1 too, for A/Bs)
+  static const bool env_group = std::getenv("XFLOW_OWNER_GROUP") != nullptr;
   const int nsrc = (int)offs.size() - 1;
+  if (cfg_.owner_group != 1 && !env_group) return false;
   if (!be_->owner_grouping() || nsrc < 2 || nsrc > kMaxGroupSources) return false;
   if (offs.front() != 0 || offs.back() != n) throw std::invalid_argument("s_pull: source offsets");
   int active = 0;

@@ -8,6 +8,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "xflow/backend.h"
 #include "xflow/common.h"
 
 #define XF_HIP_CHECK(expr)                                                        \
@@ -91,6 +92,19 @@ __device__ __forceinline__ T wave_append(T* counter, bool pred) {
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
+
+// Capacity snapshot (HostSnap): one 64-bit vector store (size, flags and
+// sequence number packed) to coherent host memory by lane 0 of the first
+// wave.  The apply kernels call it first: the step's pulls -- the only
+// inserts -- have completed, so the size and flags are final.
+__device__ __forceinline__ void store_snapshot(HostSnap* dst, const u32* mon,
+                                               unsigned long long seq) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const unsigned long long size = *reinterpret_cast<const unsigned long long*>(mon);
+  __hip_atomic_store(&dst->word, pack_snapshot(size, mon[2], mon[3], seq), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 
 __device__ __forceinline__ int wave_max(int v) {
 #pragma unroll

@@ -507,18 +507,6 @@ void launch_download_small(void* host_dst, const void* src, size_t bytes, hipStr
   XF_HIP_CHECK(hipGetLastError());
 }
 
-// Capacity snapshot (HostSnap): one 64-bit vector store (size, flags and
-// sequence number packed) to coherent host memory by lane 0 of the first
-// wave.  The apply kernels call it first: the step's pulls -- the only
-// inserts -- have completed, so the size and flags are final.
-__device__ __forceinline__ void store_snapshot(HostSnap* dst, const u32* mon,
-                                               unsigned long long seq) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  const unsigned long long size = *reinterpret_cast<const unsigned long long*>(mon);
-  __hip_atomic_store(&dst->word, pack_snapshot(size, mon[2], mon[3], seq), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 __global__ void k_snapshot(HostSnap* dst, const u32* mon, unsigned long long seq) {
   store_snapshot(dst, mon, seq);
 }
@@ -1305,8 +1293,8 @@ __global__ void __launch_bounds__(kBlock) k_gather_grads(GatherGradArgs a) {
   const int S = a.S, ps = a.pstride, W = S * ps, wd = a.width ? a.width : ps;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     u32 row = a.map[i];
-    float* src = a.grad_rw + (size_t)row * W;
-    float* dst = a.out + (size_t)i * S * wd;
+    float* __restrict__ src = a.grad_rw + (size_t)row * W;
+    float* __restrict__ dst = a.out + (size_t)i * S * wd;
     for (int s = 0; s < S; ++s)
       for (int p = 0; p < wd; ++p) {
         dst[s * wd + p] = norm_grad(src[s * ps + p], a.slice_rows, s);
@@ -1319,9 +1307,48 @@ __global__ void __launch_bounds__(kBlock) k_gather_grads(GatherGradArgs a) {
   }
 }
 
+// The same with one thread per 16-byte unit (width and pstride multiples of
+// 4): every unit's load is independent -- the row-per-thread loop above
+// serialises a load -> store round trip per float (the stores may alias the
+// next loads for the compiler), 225 us per MVM-10 rank-step in the emulated
+// 8-GPU step.
+__global__ void __launch_bounds__(kBlock) k_gather_grads4(GatherGradArgs a) {
+  const int64_t n = dev_count(a.n_dev, a.n_max, a.n_max);
+  const u32 S = (u32)a.S, ps4 = (u32)a.pstride / 4, wd4 = (u32)(a.width ? a.width : a.pstride) / 4;
+  const u32 per = S * wd4;  // units per entry
+  const u32 units = (u32)n * per;  // (< 2^32: checked by the launcher)
+  const u32 stride = gridDim.x * blockDim.x;
+  float4* __restrict__ g4 = reinterpret_cast<float4*>(a.grad_rw);
+  float4* __restrict__ o4 = reinterpret_cast<float4*>(a.out);
+  for (u32 u = blockIdx.x * blockDim.x + threadIdx.x; u < units; u += stride) {
+    const u32 i = u / per;
+    const u32 r = u - i * per, s = r / wd4, q = r - s * wd4;
+    const u32 row = a.map[i];
+    float4* sp = g4 + (u64)row * S * ps4 + (u64)s * ps4 + q;
+    const float4 v = *sp;
+    o4[u] = make_float4(norm_grad(v.x, a.slice_rows, (int)s), norm_grad(v.y, a.slice_rows, (int)s),
+                        norm_grad(v.z, a.slice_rows, (int)s), norm_grad(v.w, a.slice_rows, (int)s));
+    *sp = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (r == 0 && a.tmask_rw) {
+      a.out_mask[i] = a.tmask_rw[row];
+      a.tmask_rw[row] = 0u;
+    }
+  }
+}
+
 void launch_gather_grads(const GatherGradArgs& a, hipStream_t st) {
   if (a.n_max <= 0) return;
-  hipLaunchKernelGGL(k_gather_grads, dim3(grid_for(a.n_max)), dim3(kBlock), 0, st, a);
+  const int wd = a.width ? a.width : a.pstride;
+  const bool vec = a.pstride % 4 == 0 && wd % 4 == 0 &&
+                   (double)a.n_max * a.S * (wd / 4) < 4294967295.0 &&
+                   (reinterpret_cast<uintptr_t>(a.grad_rw) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+  if (vec) {
+    const int64_t units = a.n_max * (int64_t)a.S * (wd / 4);
+    hipLaunchKernelGGL(k_gather_grads4, dim3(grid_for(units)), dim3(kBlock), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_gather_grads, dim3(grid_for(a.n_max)), dim3(kBlock), 0, st, a);
+  }
   XF_HIP_CHECK(hipGetLastError());
 }
 
@@ -1416,6 +1443,26 @@ void launch_bucket(const BucketArgs& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // row gather / scatter helpers
 // ---------------------------------------------------------------------------
+// width a multiple of 4: one thread per 16-byte unit, 32-bit index math (the
+// element loop's 64-bit division per float dominated at MVM widths)
+__global__ void k_scatter_rows4(const float4* __restrict__ src, float4* __restrict__ dst,
+                                const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
+                                u32 w4, float* __restrict__ zero_out, int zero_width) {
+  const int64_t rows = dev_count(n_dev, n_max, n_max);
+  const u32 n = (u32)rows * w4;  // (< 2^32: checked by the launcher)
+  const u32 stride = gridDim.x * blockDim.x;
+  for (u32 e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+    const u32 i = e / w4;
+    const u32 c = e - i * w4;
+    const u64 r = map ? (u64)map[i] : (u64)i;
+    dst[r * w4 + c] = src[e];
+  }
+  if (zero_out)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * zero_width;
+         i += (int64_t)stride)
+      zero_out[i] = 0.0f;
+}
+
 __global__ void k_scatter_rows(const float* __restrict__ src, float* __restrict__ dst,
                                const u32* __restrict__ map, const int64_t* n_dev, int64_t n_max,
                                int width, float* __restrict__ zero_out, int zero_width) {
@@ -1470,6 +1517,15 @@ void launch_scatter_rows(const float* src, float* dst, const u32* map, const int
                          int64_t n_max, int width, float* zero_out, int zero_width,
                          hipStream_t st) {
   if (n_max <= 0) return;
+  if (width % 4 == 0 && (double)n_max * width < 4294967295.0 &&
+      (reinterpret_cast<uintptr_t>(src) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    hipLaunchKernelGGL(k_scatter_rows4, dim3(grid_for(n_max * width / 4)), dim3(kBlock), 0, st,
+                       reinterpret_cast<const float4*>(src), reinterpret_cast<float4*>(dst), map,
+                       n_dev, n_max, (u32)(width / 4), zero_out, zero_width);
+    XF_HIP_CHECK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(k_scatter_rows, dim3(grid_for(n_max * width)), dim3(kBlock), 0, st, src, dst,
                      map, n_dev, n_max, width, zero_out, zero_width);
   XF_HIP_CHECK(hipGetLastError());

@@ -44,6 +44,13 @@ struct EngineConfig {
   // steps the host may run ahead of the device before it waits for a
   // snapshot (bounds both the growth bound's slack and fail-fast latency)
   int monitor_lag = 2;
+  // Owner apply of a multi-source sharded step (GPU): 0 = one launch per
+  // source in source order (default), 1 = one grouped launch (k_owner_group
+  // registration + leader apply).  Per source measured faster for every
+  // model in the emulated 8-GPU step (device us per rank-step, LR 617 vs
+  // 687, FM-8 846 vs 893, MVM-10 1082 vs 1184:
+  // profiles/r3s3_w8_owner_apply_ab.txt).
+  int owner_group = 0;
 };
 
 class Engine {

@@ -123,17 +123,19 @@ def _local_sharded(bus, rank, engine):
     return LocalSharded(engine, world=bus.world, rank=rank)
 
 
-@pytest.mark.parametrize("world,kind,S,pipelined",
-                         [(2, "lr", 1, False), (3, "lr", 1, False), (2, "fm", 1, False),
-                          (8, "lr", 1, True), (8, "lr", 2, True), (4, "fm", 2, True),
-                          (4, "mvm", 1, True), (8, "fm", 1, False)])
-def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind, S, pipelined):
+@pytest.mark.parametrize("world,kind,S,pipelined,og",
+                         [(2, "lr", 1, False, 0), (3, "lr", 1, False, 1), (2, "fm", 1, False, 0),
+                          (8, "lr", 1, True, 0), (8, "lr", 1, True, 1), (8, "lr", 2, True, 0),
+                          (4, "fm", 2, True, 0), (4, "fm", 1, True, 1), (4, "mvm", 1, True, 0),
+                          (4, "mvm", 1, True, 1), (8, "fm", 1, False, 0)])
+def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind, S, pipelined, og):
     """W in-process ranks on one GPU (threads + a local all-to-all) train the
     owner-partitioned sharded step; the union of their shards equals one
     engine trained on the concatenated batches (same check as the gloo
     multi-rank test, here through the HIP partitioned dedup, the owner
-    grouping and the one-launch multi-source apply; pipelined: each step
-    prepares the next batch into the other worker buffer set)."""
+    grouping and the one-launch multi-source apply or the per-source applies
+    -- og: EngineConfig.owner_group; pipelined: each step prepares the next
+    batch into the other worker buffer set)."""
     import threading
 
     from xflow_amd.testing.hashing import owner_of
@@ -143,7 +145,8 @@ def test_owner_partitioned_multirank_on_one_gpu(gpu_device, world, kind, S, pipe
     def mk():
         return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
                       EngineConfig(table_log2_cap=16, max_rows=world * rows,
-                                   max_nnz=world * rows * 16, max_slices=world * S),
+                                   max_nnz=world * rows * 16, max_slices=world * S,
+                                   owner_group=og),
                       device=gpu_device)
 
     def data(r, s):

@@ -96,6 +96,9 @@ class EngineConfig:
     grow_load: float = 0.8
     max_log2_cap: int = 0
     monitor_lag: int = 2
+    # owner apply of a multi-source sharded step on the GPU: 0 one launch per
+    # source (default), 1 one grouped launch (csrc/include/xflow/engine.h)
+    owner_group: int = 0
 
 
 @dataclass

@@ -125,7 +125,7 @@ class Engine:
                            sum_slices=self.cfg.sum_slices, scratch_factor=self.cfg.scratch_factor,
                            device=_device_index(self.device), table_grow=self.cfg.table_grow,
                            grow_load=self.cfg.grow_load, max_log2_cap=self.cfg.max_log2_cap,
-                           monitor_lag=self.cfg.monitor_lag)
+                           monitor_lag=self.cfg.monitor_lag, owner_group=self.cfg.owner_group)
         if self.is_gpu != (self.device.type == "cuda"):
             raise RuntimeError("native engine backend does not match the requested device")
 

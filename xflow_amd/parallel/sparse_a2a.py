@@ -20,8 +20,8 @@ fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
   7. a2a grads    (+ slice masks when slices are applied in order)
   8. s_apply      owner applies every (source, slice) contribution of a key in
                   source order (deterministic, the analogue of ps-lite's
-                  serialized handler) -- one launch for all sources on the GPU,
-                  grouped by key during the pull
+                  serialized handler) -- one launch per source (optionally one
+                  grouped launch, EngineConfig.owner_group)
 
 On GPUs the all-to-alls go through the native RCCL communicator on the
 engine's stream (csrc/comm/rccl_comm.h; xGMI peer links between the node's
