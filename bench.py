@@ -100,7 +100,15 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run")
     use_gpu = torch.cuda.is_available() and not a.cpu
+    shared_gpu = False
     if use_gpu:
+        from xflow_amd.parallel.dist import shared_gpu_setup
+
+        # (XFLOW_SHARED_GPU=1: all ranks on this host's GPU 0 -- the
+        # multi-process RCCL path rehearsed on a 1-GPU box, not a measurement)
+        shared_gpu = world > 1 and shared_gpu_setup(rank)
+        if shared_gpu:
+            local = 0
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -245,6 +253,7 @@ def main():
                        "a2a_transport": sharded.transport if sharded is not None else "none",
                        "input_overlap": overlap, "v_init_scale": a.v_init_scale,
                        "table_growths": engine.table_growths},
+            **({"shared_gpu_rehearsal": True} if shared_gpu else {}),
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
             "table_load": table_keys / float(world * 2 ** log2_cap),

@@ -1,0 +1,161 @@
+"""Multi-process RCCL tests on ONE GPU (XFLOW_SHARED_GPU=1, dist_utils.run_world_gpu).
+
+Several processes share GPU 0 and exchange keys, values, gradients and
+async pushes through the native RCCL communicator (csrc/comm/rccl_comm.cpp)
+and torch's RCCL process group -- real RCCL kernels moving bytes between
+processes over its socket transport (each rank presents its own NCCL_HOSTID,
+since RCCL refuses two ranks of one host on one device).  This is the code
+path of a multi-GPU run minus xGMI: the group calls, the counts exchange with
+sequence numbers, the pipelined step, the async send/recv.  Each test checks
+the result against a single-process replay, as the gloo tests do
+(tests/test_multirank.py); reference call sites: lr_worker.cc:170,175
+(Pull/Push), ftrl.h:54-80 (server apply)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_world_gpu
+from helpers import random_csr, to_batch
+from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+from xflow_amd.engine import Engine
+from xflow_amd.testing.hashing import owner_of
+
+pytestmark = pytest.mark.gpu
+
+ROWS, FIELDS, VOCAB, STEPS = 512, 8, 300, 4
+
+
+def _batches(rank, step):
+    return random_csr(ROWS, FIELDS, VOCAB, seed=7000 * step + rank)
+
+
+def _make_engine(kind, world, dev):
+    return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
+                  EngineConfig(table_log2_cap=16, max_rows=world * ROWS,
+                               max_nnz=world * ROWS * 16, max_slices=world),
+                  device=dev)
+
+
+def _sharded_worker(rank, world, kind, out_dir):
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    dev = torch.device("cuda", 0)
+    eng = _make_engine(kind, world, dev)
+    sh = ShardedEngine(eng)
+    assert sh.transport == "rccl", sh.transport
+    bs = [to_batch(*_batches(rank, s), dev) for s in range(STEPS)]
+    for s in range(STEPS):
+        sh.train_step(bs[s], next_batch=bs[s + 1] if s + 1 < STEPS else None)
+    torch.cuda.synchronize(dev)
+    assert not eng.overflowed()
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"k{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"v{rank}.npy"), eng.pull(keys))
+    np.save(os.path.join(out_dir, f"b{rank}.npy"), np.array([sh.bytes_moved]))
+
+
+@pytest.mark.parametrize("world,kind", [(2, "lr"), (4, "lr"), (2, "fm"), (3, "mvm")])
+def test_rccl_processes_sharded_equals_single_engine(gpu_device, tmp_path, world, kind):
+    """W processes on one GPU, pipelined sharded step over RCCL: the union of
+    their table shards equals one engine trained on the concatenated batches
+    as W ordered slices."""
+    run_world_gpu(_sharded_worker, world, kind, str(tmp_path))
+    ref = _make_engine(kind, world, gpu_device)
+    for s in range(STEPS):
+        parts = [_batches(r, s) for r in range(world)]
+        keys = np.concatenate([p[0] for p in parts])
+        fg = np.concatenate([p[2] for p in parts])
+        lab = np.concatenate([p[3] for p in parts])
+        rp = np.concatenate([parts[0][1]] + [p[1][1:] + sum(len(q[0]) for q in parts[:i + 1])
+                                             for i, p in enumerate(parts[1:])])
+        ref.train_step(to_batch(keys, rp.astype(np.int32), fg, lab, gpu_device,
+                                slice_rows=ROWS))
+    k = np.concatenate([np.load(tmp_path / f"k{r}.npy") for r in range(world)])
+    v = np.concatenate([np.load(tmp_path / f"v{r}.npy") for r in range(world)])
+    for r in range(world):
+        kr = np.load(tmp_path / f"k{r}.npy")
+        assert (owner_of(kr, world) == r).all(), "a rank holds keys it does not own"
+        assert np.load(tmp_path / f"b{r}.npy")[0] > 0
+    assert len(np.unique(k)) == len(k) == ref.table_size()
+    np.testing.assert_allclose(v, ref.pull(k), rtol=1e-4, atol=1e-6)
+
+
+def _async_worker(rank, world, out_dir, staleness):
+    from xflow_amd.parallel.async_p2p import AsyncShardedEngine
+
+    dev = torch.device("cuda", 0)
+    eng = _make_engine("lr", world, dev)
+    sh = AsyncShardedEngine(eng, staleness=staleness)
+    bs = [to_batch(*_batches(rank, s), dev) for s in range(STEPS + 2)]
+    for s in range(STEPS + 2):
+        nxt = bs[s + 1] if 0 < s < STEPS + 1 else None
+        sh.train_step(bs[s], S=1, next_batch=nxt)
+    sh.flush()
+    torch.cuda.synchronize(dev)
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"ak{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"av{rank}.npy"), eng.pull(keys))
+    assert sh.p2p_ops > 0
+
+
+@pytest.mark.parametrize("staleness", [1, 2])
+def test_rccl_processes_async_staleness_matches_simulation(gpu_device, tmp_path, staleness):
+    """Config 4 over RCCL between processes: pushes ride in the key exchange
+    k steps later; equals the reference step whose pulls miss exactly the
+    previous k steps' pushes."""
+    from collections import deque
+
+    from xflow_amd.testing import torch_ref
+    from xflow_amd.testing.hashing import normal_init
+
+    world = 2
+    run_world_gpu(_async_worker, world, str(tmp_path), staleness)
+    ref = torch_ref.RefTable(1, 1, "ftrl", init_fn=lambda k, d: normal_init(k, d) * 1e-2)
+    pending = deque()
+    for s in range(STEPS + 2):
+        parts = [_batches(r, s) for r in range(world)]
+        keys = np.concatenate([p[0] for p in parts])
+        lab = np.concatenate([p[3] for p in parts])
+        rp = np.concatenate([parts[0][1]] + [p[1][1:] + len(parts[0][0]) for p in parts[1:]])
+        _, cur = torch_ref.compute_step(ref, "lr", keys, lab, rp.astype(np.int32), ROWS)
+        if len(pending) == staleness:
+            torch_ref.apply_step(ref, pending.popleft())
+        pending.append(cur)
+    while pending:
+        torch_ref.apply_step(ref, pending.popleft())
+    k = np.concatenate([np.load(tmp_path / f"ak{r}.npy") for r in range(world)])
+    v = np.concatenate([np.load(tmp_path / f"av{r}.npy") for r in range(world)])
+    np.testing.assert_allclose(v, ref.weights(k, insert=False).numpy(), rtol=1e-4, atol=1e-6)
+
+
+def _trainer_worker(rank, world, data_dir, pred_dir, gpu):
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
+                      test_prefix=os.path.join(data_dir, "small_test"), epochs=3, threads=4,
+                      pred_dir=pred_dir, engine=EngineConfig(table_log2_cap=14),
+                      train_block_bytes=4096 if rank == 0 else 6144)
+    t = Trainer(cfg, device=torch.device("cuda", 0) if gpu else torch.device("cpu"))
+    if gpu:
+        assert t.sharded.transport == "rccl", t.sharded.transport
+    t.train()
+
+
+def test_rccl_processes_trainer_equals_cpu_gloo(gpu_device, tmp_path):
+    """The Trainer (CLI path) on 2 GPU processes over RCCL writes the same
+    predictions as the same 2-rank job on the CPU backend over gloo."""
+    from conftest import DATA
+    from dist_utils import run_world
+
+    gdir, cdir = tmp_path / "gpu", tmp_path / "cpu"
+    gdir.mkdir()
+    cdir.mkdir()
+    run_world_gpu(_trainer_worker, 2, DATA, str(gdir), True)
+    run_world(_trainer_worker, 2, DATA, str(cdir), False)
+    g = np.loadtxt(gdir / "pred_0_0.txt")
+    c = np.loadtxt(cdir / "pred_0_0.txt")
+    assert g.shape == c.shape == (200, 3)
+    np.testing.assert_allclose(g, c, rtol=1e-5, atol=1e-6)

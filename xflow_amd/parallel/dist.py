@@ -57,6 +57,23 @@ def _env_rank_world():
     return 0, 1
 
 
+def shared_gpu_setup(rank: int) -> bool:
+    """XFLOW_SHARED_GPU=1: several ranks of one job share a GPU (e.g. a 2- or
+    4-rank run on a 1-GPU box, to exercise the multi-process RCCL path where
+    no multi-GPU node is at hand).  RCCL refuses two ranks on one device of
+    one host ("Duplicate GPU detected"), so each rank presents its own host id
+    (NCCL_HOSTID) and RCCL connects the ranks through its socket transport on
+    the loopback interface.  Correctness only: no xGMI, and the ranks share
+    the GPU's CUs.  Must run before the first RCCL communicator is created.
+    Returns whether the mode is on."""
+    if os.environ.get("XFLOW_SHARED_GPU", "0") in ("", "0"):
+        return False
+    os.environ["NCCL_HOSTID"] = f"xflow-shared-gpu-rank{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    return True
+
+
 def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", os.environ.get("DMLC_WORKER_ID", "0")))
 
@@ -87,6 +104,7 @@ def start(device: Optional[torch.device] = None, backend: Optional[str] = None) 
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     kw = dict(backend=backend, rank=rank, world_size=world, timeout=timeout)
     if backend == "nccl":
+        shared_gpu_setup(rank)
         kw["device_id"] = device
     dist.init_process_group(**kw)
     _started_here = True
