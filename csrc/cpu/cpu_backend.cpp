@@ -385,7 +385,16 @@ class CpuBackend final : public Backend {
     }
   }
 
-  void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes) override {
+  void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
+                   bool widen) override {
+    if (widen) {
+      if (elem_bytes != 4) throw std::invalid_argument("field_major: widen needs 4-byte elements");
+      const u32* s = static_cast<const u32*>(src);
+      u64* d = static_cast<u64*>(dst);
+      for (int64_t r = 0; r < rows; ++r)
+        for (int f = 0; f < F; ++f) d[(int64_t)f * rows + r] = (u64)s[r * F + f];
+      return;
+    }
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
     for (int64_t r = 0; r < rows; ++r)

@@ -16,9 +16,11 @@ namespace hip {
 constexpr int kTileRows = 64;
 constexpr int kMaxTileFields = 64;  // LDS: 64 x 65 x 8 B = 33 KB per workgroup
 
-template <typename T>
+// TO != T: zero-extending copy (compact u32 .xfb keys -> u64 engine keys:
+// half the H2D bytes of the streamed input path, widened in this pass)
+template <typename T, typename TO = T>
 __global__ void __launch_bounds__(kBlock) k_field_major(const T* __restrict__ src,
-                                                        T* __restrict__ dst, int64_t rows, int F) {
+                                                        TO* __restrict__ dst, int64_t rows, int F) {
   // (+1 column of padding: consecutive rows of one field land in different banks)
   __shared__ T tile[kTileRows * (kMaxTileFields + 1)];
   const int64_t r0 = (int64_t)blockIdx.x * kTileRows;
@@ -32,16 +34,21 @@ __global__ void __launch_bounds__(kBlock) k_field_major(const T* __restrict__ sr
   __syncthreads();
   for (int i = threadIdx.x; i < F * kTileRows; i += kBlock) {
     const int f = i / kTileRows, r = i - f * kTileRows;
-    if (r < nr) dst[(int64_t)f * rows + r0 + r] = tile[r * (kMaxTileFields + 1) + f];
+    if (r < nr) dst[(int64_t)f * rows + r0 + r] = (TO)tile[r * (kMaxTileFields + 1) + f];
   }
 }
 
 void launch_field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
-                        hipStream_t st) {
+                        bool widen, hipStream_t st) {
   if (rows <= 0 || F <= 0) return;
   if (F > kMaxTileFields) throw std::runtime_error("field_major: at most 64 fields");
   const int64_t g = (rows + kTileRows - 1) / kTileRows;
-  if (elem_bytes == 8) {
+  if (widen) {
+    if (elem_bytes != 4) throw std::runtime_error("field_major: widen needs 4-byte elements");
+    hipLaunchKernelGGL((k_field_major<u32, unsigned long long>), dim3((unsigned)g), dim3(kBlock),
+                       0, st, static_cast<const u32*>(src), static_cast<unsigned long long*>(dst),
+                       rows, F);
+  } else if (elem_bytes == 8) {
     hipLaunchKernelGGL(k_field_major<unsigned long long>, dim3((unsigned)g), dim3(kBlock), 0, st,
                        static_cast<const unsigned long long*>(src),
                        static_cast<unsigned long long*>(dst), rows, F);

@@ -458,7 +458,11 @@ class Backend {
                            const int64_t* n_dev, int64_t n_max) = 0;
   virtual void synth_batch(const SynthArgs& a) = 0;
   // [rows][F] -> [F][rows] of 4- or 8-byte elements (field-major batches)
-  virtual void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes) = 0;
+  // widen (elem_bytes 4 only): u32 source elements zero-extended to u64 --
+  // compact .xfb keys (data/binfmt.py) become the engine's u64 keys in the
+  // same pass
+  virtual void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
+                           bool widen = false) = 0;
   // count occupied slots / dump table rows (checkpointing); returns rows written
   virtual int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
                                int64_t max_rows) = 0;

@@ -354,10 +354,12 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("buf") = 0, py::call_guard<py::gil_scoped_release>())
       .def("w_finish", &Engine::w_finish, py::call_guard<py::gil_scoped_release>())
       .def("field_major",
-           [](Engine& e, uintptr_t src, uintptr_t dst, int64_t rows, int F, int elem_bytes) {
-             e.backend().field_major(P<const void>(src), P<void>(dst), rows, F, elem_bytes);
+           [](Engine& e, uintptr_t src, uintptr_t dst, int64_t rows, int F, int elem_bytes,
+              bool widen) {
+             e.backend().field_major(P<const void>(src), P<void>(dst), rows, F, elem_bytes, widen);
            },
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("src"), py::arg("dst"), py::arg("rows"), py::arg("F"), py::arg("elem_bytes"),
+           py::arg("widen") = false, py::call_guard<py::gil_scoped_release>())
       .def("read_stats",
            [](Engine& e, bool reset, int which) { return stats_dict(e.read_stats(reset, which)); },
            py::arg("reset") = false, py::arg("which") = 0)

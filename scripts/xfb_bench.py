@@ -22,7 +22,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def make_shard(path: str, rows: int, fields: int, seed: int) -> None:
+def make_shard(path: str, rows: int, fields: int, seed: int, hash_space: int = 0) -> None:
     from xflow_amd.data import binfmt
 
     rng = np.random.default_rng(seed)
@@ -30,7 +30,10 @@ def make_shard(path: str, rows: int, fields: int, seed: int) -> None:
     mult = np.uint64(0x9E3779B97F4A7C15)
     for f in range(fields):
         v = rng.zipf(1.1 + 0.02 * f, size=rows).astype(np.uint64)
-        keys[f::fields] = (v + np.uint64(f << 40)) * mult
+        h = (v + np.uint64(f << 40)) * mult
+        if hash_space:  # hashed into [0, hash_space): multiply-high of the 64-bit hash
+            h = ((h >> np.uint64(32)) * np.uint64(hash_space)) >> np.uint64(32)
+        keys[f::fields] = h
     labels = (rng.random(rows) < 0.25).astype(np.float32)
     fg = np.tile(np.arange(fields, dtype=np.int32), rows)
     binfmt.write(path, labels, np.arange(rows + 1, dtype=np.int64) * fields, keys, fg)
@@ -47,6 +50,9 @@ def main() -> int:
     ap.add_argument("--csr-only", action="store_true")
     ap.add_argument("--copy-threads", type=int, default=8)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--hash-space", type=int, default=0,
+                    help="features hashed into [0, N) (Criteo-1TB: 1e9); N <= 2^32 makes the "
+                         "shard compact (u32 keys, half the streamed bytes); 0 = 64-bit keys")
     ap.add_argument("--test-rows", type=int, default=65536,
                     help="rows of the test shard rank 0 predicts (pred file + AUC/logloss)")
     a = ap.parse_args()
@@ -60,12 +66,15 @@ def main() -> int:
     tr = os.path.join(a.dir, "train-00000.xfb")
     te = os.path.join(a.dir, "test-00000.xfb")
     t0 = time.perf_counter()
-    if not os.path.exists(tr):
-        make_shard(tr, a.rows, a.fields, 1)
     from xflow_amd.data import binfmt
 
-    if not os.path.exists(te) or binfmt.Shard(te).rows != a.test_rows:
-        make_shard(te, a.test_rows, a.fields, 2)
+    want_compact = 0 < a.hash_space <= (1 << 32)
+    if (not os.path.exists(tr) or binfmt.Shard(tr).rows != a.rows
+            or binfmt.Shard(tr).compact != want_compact):
+        make_shard(tr, a.rows, a.fields, 1, a.hash_space)
+    if (not os.path.exists(te) or binfmt.Shard(te).rows != a.test_rows
+            or binfmt.Shard(te).compact != want_compact):
+        make_shard(te, a.test_rows, a.fields, 2, a.hash_space)
     print(f"shard ready ({time.perf_counter() - t0:.1f}s, "
           f"{os.path.getsize(tr) / 1e9:.2f} GB)", flush=True)
     dev = torch.device("cpu" if a.cpu or not torch.cuda.is_available() else "cuda:0")
@@ -88,13 +97,18 @@ def main() -> int:
     eps = [json.loads(l) for l in open(mfile) if '"epoch"' in l]
     eps = [e for e in eps if e.get("event") == "epoch"]
     print(json.dumps({"path": "xfb", "device": str(dev), "rows": a.rows,
+                      "compact_keys": binfmt.Shard(tr).compact,
                       "block_rows": a.block_rows, "resident": a.resident,
                       "fixed_width": not a.csr_only,
                       "samples_per_s_by_epoch": [round(e["samples_per_s"]) for e in eps],
                       "train_logloss": [round(e["train_logloss"], 5) for e in eps],
                       "train_s": round(t1 - t0, 2), "predict_rows": res["n"],
                       "predict_s": round(t2 - t1, 3), "test_auc": round(res["auc"], 5),
-                      "wall_s_incl_eval": round(wall, 2)}), flush=True)
+                      "wall_s_incl_eval": round(wall, 2),
+                      # XFLOW_STREAM_TIMELINE=1: per epoch, H2D time and the part of it
+                      # that ran while a step was executing (HIP events)
+                      **({"timeline_by_epoch": [e["timeline"] for e in eps]}
+                         if eps and "timeline" in eps[0] else {})}), flush=True)
     # release the engine (device memory, pinned buffers) before interpreter
     # teardown: under rocprofv3 a late hipFree from a module destructor crashed
     t.close()

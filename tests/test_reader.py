@@ -211,17 +211,27 @@ def test_trainer_on_xfb_equals_text(tmp_path, kind):
     np.testing.assert_array_equal(preds[0], preds[1])
 
 
-def _fixed_width_shards(d, rows=300, F=12, seed=0):
-    """Uniform-width train/test .xfb shards (every row holds F features)."""
+def _fixed_width_shards(d, rows=300, F=12, seed=0, hash32=False, compact="auto", csr=False):
+    """Uniform-width train/test .xfb shards (every row holds F features);
+    hash32: keys below 2^32 (stored compact unless compact="off"); csr: rows
+    of F-1 or F features."""
     from xflow_amd.data import binfmt
 
     rng = np.random.default_rng(seed)
     for name, n in (("tr-00000.xfb", rows), ("te-00000.xfb", rows // 3)):
         keys = (rng.zipf(1.3, size=n * F).astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)
                 + np.tile(np.arange(F, dtype=np.uint64), n))
+        if hash32:
+            keys = keys >> np.uint64(32)
         fg = np.tile(np.arange(F, dtype=np.int32), n)
-        binfmt.write(str(d / name), (rng.random(n) < 0.3).astype(np.float32),
-                     np.arange(n + 1) * F, keys, fg)
+        rp = np.arange(n + 1) * F
+        if csr:  # drop the last feature of every third row
+            keep = np.ones(n * F, bool)
+            keep[np.arange(0, n, 3) * F + F - 1] = False
+            keys, fg = keys[keep], fg[keep]
+            rp = np.concatenate([[0], np.cumsum(np.where(np.arange(n) % 3 == 0, F - 1, F))])
+        binfmt.write(str(d / name), (rng.random(n) < 0.3).astype(np.float32), rp, keys, fg,
+                     compact=compact)
 
 
 def _train_preds(d, tag, device="cpu", **kw):
@@ -272,3 +282,57 @@ def test_block_stream_trainer_gpu_matches_cpu(gpu_device, tmp_path, fixed):
                      block_rows=512, resident=True)
     np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(b, c, rtol=1e-4, atol=1e-5)  # float atomics: not bitwise
+
+
+def test_xfb_compact_keys_roundtrip(tmp_path):
+    """Keys below 2^32 are stored as u32 (version 2, flag bit 1): same values,
+    half the key bytes; compact=False keeps the u64 layout."""
+    from xflow_amd.data import binfmt
+
+    rp = np.array([0, 2, 2, 5])
+    keys = np.array([7, 2**32 - 1, 0, 123456789, 99], dtype=np.uint64)
+    binfmt.write(str(tmp_path / "c.xfb"), np.array([1, 0, 1]), rp, keys, np.arange(5))
+    binfmt.write(str(tmp_path / "w.xfb"), np.array([1, 0, 1]), rp, keys, np.arange(5),
+                 compact=False)
+    c, w = binfmt.Shard(str(tmp_path / "c.xfb")), binfmt.Shard(str(tmp_path / "w.xfb"))
+    assert c.compact and not w.compact and c.keys.dtype == np.uint32
+    np.testing.assert_array_equal(c.keys.astype(np.uint64), w.keys)
+    np.testing.assert_array_equal(c.fgid, w.fgid)
+    assert os.path.getsize(tmp_path / "c.xfb") < os.path.getsize(tmp_path / "w.xfb")
+    with pytest.raises(ValueError):
+        binfmt.write(str(tmp_path / "x.xfb"), np.array([1]), np.array([0, 1]),
+                     np.array([2**32], dtype=np.uint64), compact=True)
+
+
+@pytest.mark.parametrize("kind,csr", [("lr", False), ("fm", False), ("lr", True)])
+def test_compact_xfb_trains_like_wide(tmp_path, kind, csr):
+    """A compact-key shard (u32 keys widened by the engine: in the
+    field-major transpose, or by widen_keys for CSR blocks) trains exactly
+    like the same shard stored with u64 keys."""
+    (tmp_path / "c").mkdir()
+    (tmp_path / "w").mkdir()
+    _fixed_width_shards(tmp_path / "c", hash32=True, csr=csr)
+    _fixed_width_shards(tmp_path / "w", hash32=True, compact="off", csr=csr)
+    from xflow_amd.data import binfmt
+
+    assert binfmt.Shard(str(tmp_path / "c" / "tr-00000.xfb")).compact
+    a = _train_preds(tmp_path / "c", "p", kind=kind)
+    b = _train_preds(tmp_path / "w", "p", kind=kind)
+    assert len(a) == 100
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("csr", [False, True])
+def test_compact_xfb_gpu_streamed_equals_wide(gpu_device, tmp_path, csr):
+    """GPU: compact keys go over the host link as int32 (BlockStream) and are
+    widened on the device (k_field_major<u32, u64> / widen_keys); training
+    equals the u64-key shard bit for bit."""
+    (tmp_path / "c").mkdir()
+    (tmp_path / "w").mkdir()
+    _fixed_width_shards(tmp_path / "c", rows=3000, hash32=True, csr=csr)
+    _fixed_width_shards(tmp_path / "w", rows=3000, hash32=True, compact="off", csr=csr)
+    a = _train_preds(tmp_path / "c", "p", device="cuda", block_rows=512)
+    b = _train_preds(tmp_path / "w", "p", device="cuda", block_rows=512)
+    assert len(a) == 1000
+    np.testing.assert_array_equal(a, b)

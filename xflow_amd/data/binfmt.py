@@ -11,11 +11,18 @@ path), field ids -- so an epoch maps the arrays instead of parsing them.
 Layout (little endian):
 
     b"XFLOWCSR"                                   magic, 8 B
-    u64 version (1), rows, nnz, flags (bit 0: fgid present)
+    u64 version (1; 2 = compact keys), rows, nnz,
+        flags (bit 0: fgid present, bit 1: compact keys)
     f32 labels[rows]   (padded to 8 B)
     i64 row_ptr[rows + 1]
-    u64 keys[nnz]
+    u64 keys[nnz]      (compact: u32 keys[nnz], padded to 8 B)
     i32 fgid[nnz]      (flag bit 0)
+
+Compact keys: when every key of a shard is below 2^32 (features hashed into
+a space of at most 2^32, e.g. Criteo-1TB's 1e9), the writer stores them as
+u32 (``compact="auto"``).  The streamed input path then moves half the key
+bytes over the host link -- the bound of that path -- and the device widens
+them to u64 inside its field-major transpose (csrc/hip/kernels_layout.hip).
 
     python -m xflow_amd.data.binfmt convert data/small_train-00000 /tmp/small_train-00000.xfb
 
@@ -35,6 +42,8 @@ import numpy as np
 
 MAGIC = b"XFLOWCSR"
 VERSION = 1
+VERSION_COMPACT = 2
+FLAG_FGID, FLAG_COMPACT = 1, 2
 _HDR = struct.Struct("<8sQQQQ")
 
 
@@ -42,29 +51,46 @@ def _pad8(n: int) -> int:
     return (n + 7) & ~7
 
 
+def _compact_ok(keys: np.ndarray, compact) -> bool:
+    if compact == "auto":
+        return len(keys) > 0 and int(keys.max()) < (1 << 32)
+    return bool(compact)
+
+
 def write(dst: str, labels: np.ndarray, row_ptr: np.ndarray, keys: np.ndarray,
-          fgid: Optional[np.ndarray] = None) -> None:
-    """Write one shard from whole arrays (row_ptr starts at 0, ends at nnz)."""
+          fgid: Optional[np.ndarray] = None, compact="auto") -> None:
+    """Write one shard from whole arrays (row_ptr starts at 0, ends at nnz).
+    compact: store u32 keys -- "auto" when every key is below 2^32."""
     labels = np.ascontiguousarray(labels, dtype=np.float32)
     row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int64)
     keys = np.ascontiguousarray(keys).view(np.uint64)
     rows, nnz = len(labels), len(keys)
     if len(row_ptr) != rows + 1 or row_ptr[0] != 0 or row_ptr[-1] != nnz:
         raise ValueError("row_ptr must have rows+1 offsets from 0 to nnz")
+    cmp = _compact_ok(keys, compact)
+    if cmp and nnz and int(keys.max()) >= (1 << 32):
+        raise ValueError("compact keys must be below 2^32")
+    flags = (FLAG_FGID if fgid is not None else 0) | (FLAG_COMPACT if cmp else 0)
     with open(dst + ".tmp", "wb") as f:
-        f.write(_HDR.pack(MAGIC, VERSION, rows, nnz, 1 if fgid is not None else 0))
+        f.write(_HDR.pack(MAGIC, VERSION_COMPACT if cmp else VERSION, rows, nnz, flags))
         f.write(labels.tobytes())
         f.write(b"\0" * (_pad8(4 * rows) - 4 * rows))
         f.write(row_ptr.tobytes())
-        f.write(keys.tobytes())
+        if cmp:
+            f.write(keys.astype(np.uint32).tobytes())
+            f.write(b"\0" * (_pad8(4 * nnz) - 4 * nnz))
+        else:
+            f.write(keys.tobytes())
         if fgid is not None:
             f.write(np.ascontiguousarray(fgid, dtype=np.int32).tobytes())
     os.replace(dst + ".tmp", dst)
 
 
-def convert(src: str, dst: str, block_bytes: int = 64 << 20, threads: int = 0) -> dict:
+def convert(src: str, dst: str, block_bytes: int = 64 << 20, threads: int = 0,
+            compact="auto") -> dict:
     """libffm text -> .xfb, streaming block by block through the native reader
-    (parallel parse); arrays are staged in temporary files next to dst."""
+    (parallel parse); arrays are staged in temporary files next to dst.
+    compact="auto" stores u32 keys when every key is below 2^32."""
     from xflow_amd import native
 
     r = native.load().BlockReader(src, block_bytes)
@@ -73,6 +99,7 @@ def convert(src: str, dst: str, block_bytes: int = 64 << 20, threads: int = 0) -
     d = os.path.dirname(os.path.abspath(dst)) or "."
     parts = {k: tempfile.TemporaryFile(dir=d) for k in ("labels", "row_ptr", "keys", "fgid")}
     rows = nnz = 0
+    kmax = 0
     parts["row_ptr"].write(np.zeros(1, np.int64).tobytes())
     while True:
         b = r.next()
@@ -80,12 +107,19 @@ def convert(src: str, dst: str, block_bytes: int = 64 << 20, threads: int = 0) -
             break
         parts["labels"].write(np.asarray(b["labels"], np.float32).tobytes())
         parts["row_ptr"].write((np.asarray(b["row_ptr"][1:], np.int64) + nnz).tobytes())
-        parts["keys"].write(np.asarray(b["keys"]).view(np.uint64).tobytes())
+        k = np.asarray(b["keys"]).view(np.uint64)
+        if len(k):
+            kmax = max(kmax, int(k.max()))
+        parts["keys"].write(k.tobytes())
         parts["fgid"].write(np.asarray(b["fgid"], np.int32).tobytes())
         rows += len(b["labels"])
         nnz += len(b["keys"])
+    cmp = (nnz > 0 and kmax < (1 << 32)) if compact == "auto" else bool(compact)
+    if cmp and kmax >= (1 << 32):
+        raise ValueError("compact keys must be below 2^32")
     with open(dst + ".tmp", "wb") as f:
-        f.write(_HDR.pack(MAGIC, VERSION, rows, nnz, 1))
+        f.write(_HDR.pack(MAGIC, VERSION_COMPACT if cmp else VERSION, rows, nnz,
+                          FLAG_FGID | (FLAG_COMPACT if cmp else 0)))
         for k in ("labels", "row_ptr", "keys", "fgid"):
             fp = parts[k]
             fp.seek(0)
@@ -93,9 +127,13 @@ def convert(src: str, dst: str, block_bytes: int = 64 << 20, threads: int = 0) -
                 chunk = fp.read(64 << 20)
                 if not chunk:
                     break
+                if k == "keys" and cmp:
+                    chunk = np.frombuffer(chunk, np.uint64).astype(np.uint32).tobytes()
                 f.write(chunk)
             if k == "labels":
                 f.write(b"\0" * (_pad8(4 * rows) - 4 * rows))
+            if k == "keys" and cmp:
+                f.write(b"\0" * (_pad8(4 * nnz) - 4 * nnz))
             fp.close()
     os.replace(dst + ".tmp", dst)
     return {"rows": rows, "nnz": nnz}
@@ -107,17 +145,19 @@ class Shard:
     def __init__(self, path: str):
         with open(path, "rb") as f:
             magic, ver, rows, nnz, flags = _HDR.unpack(f.read(_HDR.size))
-        if magic != MAGIC or ver != VERSION:
+        if magic != MAGIC or ver not in (VERSION, VERSION_COMPACT):
             raise ValueError(f"{path}: not an xflow CSR shard")
         self.path, self.rows, self.nnz = path, rows, nnz
+        self.compact = bool(flags & FLAG_COMPACT)
         off = _HDR.size
         self.labels = np.memmap(path, np.float32, "r", off, (rows,))
         off += _pad8(4 * rows)
         self.row_ptr = np.memmap(path, np.int64, "r", off, (rows + 1,))
         off += 8 * (rows + 1)
-        self.keys = np.memmap(path, np.uint64, "r", off, (nnz,)) if nnz else np.zeros(0, np.uint64)
-        off += 8 * nnz
-        self.fgid = (np.memmap(path, np.int32, "r", off, (nnz,)) if (flags & 1) and nnz
+        kt = np.uint32 if self.compact else np.uint64  # (compact: u32, widened on use)
+        self.keys = np.memmap(path, kt, "r", off, (nnz,)) if nnz else np.zeros(0, kt)
+        off += _pad8(4 * nnz) if self.compact else 8 * nnz
+        self.fgid = (np.memmap(path, np.int32, "r", off, (nnz,)) if (flags & FLAG_FGID) and nnz
                      else np.zeros(nnz, np.int32))
 
 
@@ -171,8 +211,11 @@ def main(argv=None) -> int:
     c.add_argument("dst")
     c.add_argument("--block-bytes", type=int, default=64 << 20)
     c.add_argument("--threads", type=int, default=0)
+    c.add_argument("--compact", choices=["auto", "on", "off"], default="auto",
+                   help="u32 keys (all keys below 2^32): half the streamed H2D bytes")
     a = ap.parse_args(argv)
-    info = convert(a.src, a.dst, a.block_bytes, a.threads)
+    info = convert(a.src, a.dst, a.block_bytes, a.threads,
+                   {"auto": "auto", "on": True, "off": False}[a.compact])
     print(f"{a.dst}: {info['rows']} rows, {info['nnz']} features")
     return 0
 

@@ -35,7 +35,9 @@ _CHUNK = 4 << 20  # bytes per host-copy task
 
 def _np(a) -> np.ndarray:
     a = np.asarray(a)
-    return a.view(np.int64) if a.dtype == np.uint64 else a
+    if a.dtype == np.uint64:
+        return a.view(np.int64)
+    return a.view(np.int32) if a.dtype == np.uint32 else a  # (compact .xfb keys)
 
 
 class BlockStream:
@@ -44,8 +46,9 @@ class BlockStream:
     by ``source()`` returning host blocks (dicts of numpy arrays) or None."""
 
     def __init__(self, source: Callable[[], Optional[dict]], device: torch.device,
-                 with_fgid: bool, nbuf: int = 3, copy_threads: int = 8):
+                 with_fgid: bool, nbuf: int = 3, copy_threads: int = 8, timeline=None):
         self.device = device
+        self.timeline = timeline  # utils.trace.StreamTimeline: "h2d" intervals
         self.names = ["keys", "labels", "row_ptr"] + (["fgid"] if with_fgid else [])
         self.copy = torch.cuda.Stream(device)
         self.pool = ThreadPoolExecutor(max(1, copy_threads))
@@ -60,10 +63,10 @@ class BlockStream:
         self.thread.start()
 
     # ------------------------------------------------------------ producer
-    def _buf(self, slot: int, name: str, n: int) -> torch.Tensor:
+    def _buf(self, slot: int, name: str, n: int, dtype: torch.dtype) -> torch.Tensor:
         t = self.pinned[slot].get(name)
-        if t is None or t.numel() < n:
-            t = torch.empty(max(n, 1) + (max(n, 1) >> 3), dtype=_DTYPES[name], pin_memory=True)
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(max(n, 1) + (max(n, 1) >> 3), dtype=dtype, pin_memory=True)
             self.pinned[slot][name] = t
         return t
 
@@ -89,7 +92,10 @@ class BlockStream:
                 meta = {}
                 for name in self.names:
                     a = _np(blk[name])
-                    buf = self._buf(slot, name, len(a))
+                    # compact u32 keys travel as int32: half the H2D bytes, widened
+                    # on the device (Batch.to_field_major / engine.widen_keys)
+                    dt = torch.int32 if name == "keys" and a.dtype == np.int32 else _DTYPES[name]
+                    buf = self._buf(slot, name, len(a), dt)
                     self._fill(buf.numpy()[:len(a)], a)
                     meta[name] = len(a)
                 rp = _np(blk["row_ptr"])
@@ -117,8 +123,12 @@ class BlockStream:
         # block back only once the steps that read it have finished.
         out: Dict[str, object] = {}
         with torch.cuda.stream(self.copy):
+            if self.timeline is not None:
+                self.timeline.begin("h2d", self.copy)
             for name in self.names:
                 out[name] = self.pinned[slot][name][:meta[name]].to(self.device, non_blocking=True)
+            if self.timeline is not None:
+                self.timeline.end("h2d", self.copy)
             ev = torch.cuda.Event()
             ev.record(self.copy)
         self.free.put((slot, ev))

@@ -83,18 +83,35 @@ class Batch:
             raise ValueError("only fixed-width batches have a field-major form")
         F = self.nnz_per_row
         if engine is not None and F <= 64:
-            def t(x):
+            def t(x, widen=False):
                 if x is None:
                     return None
-                y = torch.empty_like(x)
+                y = (torch.empty(x.numel(), dtype=torch.int64, device=x.device) if widen
+                     else torch.empty_like(x))
                 engine._sync_stream()
                 engine.native.field_major(x.data_ptr(), y.data_ptr(), self.rows, F,
-                                          x.element_size())
+                                          x.element_size(), widen)
                 return y
         else:
-            t = (lambda x: None if x is None else x.view(self.rows, F).t().contiguous().view(-1))
-        return Batch(keys=t(self.keys), labels=self.labels, fgid=t(self.fgid), nnz_per_row=F,
-                     slice_rows=self.slice_rows, field_major=True)
+            def t(x, widen=False):
+                if x is None:
+                    return None
+                y = x.view(self.rows, F).t().contiguous().view(-1)
+                return widen_keys(y) if widen else y
+        # compact (u32) keys of an .xfb shard are widened in the same pass
+        return Batch(keys=t(self.keys, self.keys.dtype == torch.int32), labels=self.labels,
+                     fgid=t(self.fgid), nnz_per_row=F, slice_rows=self.slice_rows,
+                     field_major=True)
+
+
+def widen_keys(keys: torch.Tensor) -> torch.Tensor:
+    """Engine keys (int64 u64 bit patterns) from compact u32 keys held in an
+    int32 tensor (data/binfmt.py compact shards); int64 keys pass through."""
+    if keys.dtype == torch.int64:
+        return keys
+    if keys.dtype != torch.int32:
+        raise TypeError(f"keys must be int64 or compact int32, got {keys.dtype}")
+    return keys.to(torch.int64) & 0xFFFFFFFF
 
 
 def _device_index(device: torch.device) -> int:

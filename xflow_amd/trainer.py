@@ -39,12 +39,12 @@ from xflow_amd import native as _native
 from xflow_amd.config import TrainConfig, model_kind
 from xflow_amd.data import binfmt
 from xflow_amd.data.upload import BlockStream
-from xflow_amd.engine import Batch, Engine
+from xflow_amd.engine import Batch, Engine, widen_keys
 from xflow_amd.metrics import MetricsLogger, reference_auc
 from xflow_amd.parallel import dist as xdist
 from xflow_amd.testing.hashing import owner_of
 from xflow_amd.utils.faults import injector_from_env, watchdog_from_env
-from xflow_amd.utils.trace import PhaseTimer
+from xflow_amd.utils.trace import PhaseTimer, StreamTimeline
 
 
 def shard_path(prefix: str, rank: int) -> str:
@@ -132,13 +132,15 @@ class Trainer:
             return t.to(dev, non_blocking=True)
 
         F = _uniform_width(rp) if self.cfg.fixed_width else 0
-        keys = up(np.asarray(blk["keys"][:nnz]).view(np.int64))
+        k = np.asarray(blk["keys"][:nnz])
+        # (compact u32 .xfb keys upload as int32 and widen on the device)
+        keys = up(k.view(np.int32) if k.dtype == np.uint32 else k.view(np.int64))
         fgid = up(blk["fgid"][:nnz]) if self._with_fgid else None
         if F:
             return Batch(keys=keys, labels=up(blk["labels"][:used]), fgid=fgid, nnz_per_row=F,
                          slice_rows=slice_rows).to_field_major(self.engine)
-        return Batch(keys=keys, labels=up(blk["labels"][:used]), row_ptr=up(rp), fgid=fgid,
-                     slice_rows=slice_rows)
+        return Batch(keys=widen_keys(keys), labels=up(blk["labels"][:used]), row_ptr=up(rp),
+                     fgid=fgid, slice_rows=slice_rows)
 
     def _device_batch(self, blk: dict, used: int, slice_rows: int) -> Batch:
         """Batch over a block already on the device (data.upload.BlockStream)."""
@@ -148,7 +150,7 @@ class Trainer:
         if F:
             return Batch(keys=blk["keys"][:nnz], labels=blk["labels"][:used], fgid=fgid,
                          nnz_per_row=F, slice_rows=slice_rows).to_field_major(self.engine)
-        return Batch(keys=blk["keys"][:nnz], labels=blk["labels"][:used],
+        return Batch(keys=widen_keys(blk["keys"][:nnz]), labels=blk["labels"][:used],
                      row_ptr=blk["row_ptr"][:used + 1], fgid=fgid, slice_rows=slice_rows)
 
     def _split(self, rows: int):
@@ -224,8 +226,12 @@ class Trainer:
                           else nat.PrefetchReader(path, cfg.train_block_bytes))
                 nxt = reader.next
                 if self.device.type == "cuda" and self.concurrent:
+                    # XFLOW_STREAM_TIMELINE=1: H2D vs step intervals from HIP
+                    # events, reported in the epoch record (overlap evidence)
+                    tl = (StreamTimeline(self.device)
+                          if os.environ.get("XFLOW_STREAM_TIMELINE") else None)
                     stream = BlockStream(reader.next, self.device, self._with_fgid,
-                                         copy_threads=cfg.copy_threads)
+                                         copy_threads=cfg.copy_threads, timeline=tl)
                     nxt = stream.next
                 record = [] if cfg.resident else None
             t0 = time.perf_counter()
@@ -245,6 +251,9 @@ class Trainer:
                     self.watchdog.beat()
                 if cur is not None and not self.faults.before_step(self.steps) and sh is not None:
                     sh.drop_exchanges += 1  # fault injection: this rank skips an exchange
+                tl = stream.timeline if stream is not None else None
+                if tl is not None:
+                    tl.begin("step")
                 with self.timer.phase("step"):
                     if sh is not None:
                         if not sh.train_step(cur if cur is not None else empty, S=self.S,
@@ -252,13 +261,18 @@ class Trainer:
                             break
                     elif cur.rows > 0:
                         self.engine.train_step(cur)
+                if tl is not None:
+                    tl.end("step")
                 self.steps += 1
                 ep_samples += cur.rows if cur is not None else 0
                 if log_every and self.steps % log_every == 0:
                     self._log_progress(ep_samples, t0)
                 cur = nb if sh is not None else next(it, None)
+            timeline = None
             if stream is not None:
                 stream.close()
+                if stream.timeline is not None:
+                    timeline = stream.timeline.overlap("h2d", "step")
             if record is not None:
                 self._resident = record
             if hasattr(self.sharded, "flush"):
@@ -281,6 +295,8 @@ class Trainer:
                        table_capacity=self.engine.table_capacity,
                        table_growths=self.engine.table_growths,
                        monitor_waits=self.engine.monitor_waits)
+            if timeline is not None:
+                rec["timeline"] = {k: round(v, 3) for k, v in timeline.items()}
             if sh is not None:
                 # split-size reads that found the device copy in flight, and
                 # steps whose batch was not prepared ahead (the epoch's first)

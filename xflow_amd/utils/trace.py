@@ -93,6 +93,58 @@ class PhaseTimer:
         return out
 
 
+class StreamTimeline:
+    """Device-side intervals of named activities on their own streams (HIP
+    timing events), for overlap evidence without a profiler: e.g. the H2D
+    copies of the streamed input path (copy stream) against the training
+    steps (compute stream).  ``begin(kind, stream)`` / ``end(...)`` bracket
+    one interval; ``overlap(a, b)`` = time of kind a that ran while some
+    interval of kind b was running (intervals read back after a sync).
+    Enabled by XFLOW_STREAM_TIMELINE=1 in the trainer."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.base = torch.cuda.Event(enable_timing=True)
+        self.base.record(torch.cuda.current_stream(device))
+        self.events = defaultdict(list)  # kind -> [(start, end)]
+        self._open = {}
+
+    def begin(self, kind: str, stream=None) -> None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream if stream is not None else torch.cuda.current_stream(self.device))
+        self._open[kind] = ev
+
+    def end(self, kind: str, stream=None) -> None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream if stream is not None else torch.cuda.current_stream(self.device))
+        self.events[kind].append((self._open.pop(kind), ev))
+
+    def intervals(self, kind: str):
+        torch.cuda.synchronize(self.device)
+        return sorted((self.base.elapsed_time(a), self.base.elapsed_time(b))
+                      for a, b in self.events.get(kind, []))
+
+    @staticmethod
+    def _union(iv):
+        out = []
+        for a, b in iv:
+            if out and a <= out[-1][1]:
+                out[-1][1] = max(out[-1][1], b)
+            else:
+                out.append([a, b])
+        return out
+
+    def overlap(self, a: str, b: str) -> dict:
+        ia, ub = self.intervals(a), self._union(self.intervals(b))
+        tot = sum(y - x for x, y in ia)
+        ov = 0.0
+        for x, y in ia:
+            for u, v in ub:
+                ov += max(0.0, min(y, v) - max(x, u))
+        return {f"{a}_ms": tot, f"{a}_during_{b}_ms": ov,
+                f"{b}_busy_ms": sum(v - u for u, v in ub), f"{a}_n": len(ia)}
+
+
 @contextlib.contextmanager
 def torch_profile(trace_dir: Optional[str]):
     if not trace_dir:
