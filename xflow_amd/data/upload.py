@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Callable, Dict, Optional
 
@@ -58,6 +59,7 @@ class BlockStream:
             self.free.put((i, None))
         self.ready: "queue.Queue" = queue.Queue()
         self.error: Optional[BaseException] = None
+        self.stage_s = 0.0  # host time spent filling pinned slots (the timeline reports it)
         self.stop = False
         self.thread = threading.Thread(target=self._produce, args=(source,), daemon=True)
         self.thread.start()
@@ -90,6 +92,7 @@ class BlockStream:
                 if ev is not None:
                     ev.synchronize()  # the previous H2D from this slot has read it
                 meta = {}
+                t0 = time.perf_counter()
                 for name in self.names:
                     a = _np(blk[name])
                     # compact u32 keys travel as int32: half the H2D bytes, widened
@@ -98,6 +101,7 @@ class BlockStream:
                     buf = self._buf(slot, name, len(a), dt)
                     self._fill(buf.numpy()[:len(a)], a)
                     meta[name] = len(a)
+                self.stage_s += time.perf_counter() - t0
                 rp = _np(blk["row_ptr"])
                 lens = np.diff(rp) if len(rp) > 1 else np.zeros(0, rp.dtype)
                 F = int(lens[0]) if len(lens) and lens[0] > 0 and np.all(lens == lens[0]) else 0

@@ -273,6 +273,7 @@ class Trainer:
                 stream.close()
                 if stream.timeline is not None:
                     timeline = stream.timeline.overlap("h2d", "step")
+                    timeline["host_stage_ms"] = 1000.0 * stream.stage_s
             if record is not None:
                 self._resident = record
             if hasattr(self.sharded, "flush"):
