@@ -205,6 +205,7 @@ def main():
         step()
     if hasattr(sharded, "flush"):
         sharded.flush()  # the last pushes are part of the timed work
+    t_issue = time.perf_counter() - t0  # host time to queue the steps (bounded by monitor lag)
     sync()
     elapsed = time.perf_counter() - t0
     st = engine.read_stats(reset=True)
@@ -259,6 +260,8 @@ def main():
             "table_load": table_keys / float(world * 2 ** log2_cap),
             "prefilled_keys": int(prefill_tot),
             "host_waits": int(sharded.host_waits) if sharded is not None else 0,
+            "host_issue_ms_per_step": 1000.0 * t_issue / a.steps,
+            "monitor_lag": a.monitor_lag,
         }
         if a.model == "fm":
             out["config"]["v_dim"] = a.v_dim
