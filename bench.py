@@ -81,9 +81,12 @@ def parse():
                          "GPU otherwise times its first steps at idle clocks (seen once in five "
                          "cold boxes: 315 vs 525 M samples/s).  Training warmup is exactly "
                          "--warmup steps, so logloss/table_keys do not depend on the box")
-    ap.add_argument("--monitor-lag", type=int, default=2,
+    ap.add_argument("--monitor-lag", type=int, default=7,
                     help="steps the host may run ahead of the table-capacity monitor "
-                         "(EngineConfig.monitor_lag)")
+                         "(EngineConfig.monitor_lag).  The host queues a step in ~40 us of "
+                         "the device's ~470: 7 steps of run-ahead (~3 ms) absorb host "
+                         "scheduling hiccups; 2, 7 and 32 measured the same throughput "
+                         "(profiles/r3s3_monitor_lag.txt)")
     ap.add_argument("--overlap", choices=["on", "off"], default="off",
                     help="generate batch t+1 on a side stream while step t runs (measured on "
                          "one MI355X: 2-4%% slower for the fused and the multi-rank step, the "

@@ -43,7 +43,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (!(cfg_.grow_load > 0.0 && cfg_.grow_load < 1.0))
     throw std::invalid_argument("grow_load must be in (0, 1)");
   if (cfg_.monitor_lag < 0 || cfg_.monitor_lag >= kSnaps)
-    throw std::invalid_argument("monitor_lag must be in [0, 7]");
+    throw std::invalid_argument("monitor_lag must be in [0, 63]");
   if (cfg_.max_slices < 1 || cfg_.max_slices > 32)
     throw std::invalid_argument("max_slices must be in [1, 32]");
   if (cfg_.model.kind != kLR && (cfg_.model.v_dim < 1 || cfg_.model.v_dim > 32))

@@ -315,7 +315,7 @@ class Engine {
   // written by the step's apply kernel (or a tiny kernel when the step has
   // none) and polled by the host -- no event, no extra launch; each comes
   // with the cumulative insert bound queued before it
-  static constexpr int kSnaps = 8;
+  static constexpr int kSnaps = 64;
   HostSnap* snaps_ = nullptr;       // pinned host [kSnaps]
   int64_t snap_adds_[kSnaps] = {};
   bool snap_carried_ = false;       // an apply since the last inserts carries the next snapshot
