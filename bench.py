@@ -263,6 +263,9 @@ def main():
             "table_load": table_keys / float(world * 2 ** log2_cap),
             "prefilled_keys": int(prefill_tot),
             "host_waits": int(sharded.host_waits) if sharded is not None else 0,
+            # multi-rank: steps whose next batch's keys rode with the gradient
+            # exchange (2 RCCL group calls per step instead of 3)
+            "early_key_exchanges": int(getattr(sharded, "early_key_exchanges", 0)),
             "host_issue_ms_per_step": 1000.0 * t_issue / a.steps,
             "monitor_lag": a.monitor_lag,
         }

@@ -105,7 +105,14 @@ class ShardedEngine:
         self._counts_both = [torch.zeros(2 * W, dtype=torch.int64, device=dev) for _ in range(2)]
         self._send_keys = [torch.empty(max(engine.cfg.max_nnz, 1), dtype=torch.int64, device=dev)
                            for _ in range(2)]
+        # two receive-key buffers: the next batch's keys arrive (with this
+        # step's gradients) while this step's apply still reads its own
         self._recv_keys = _Buf(torch.int64, dev)
+        self._recv_keys_ahead = [_Buf(torch.int64, dev), _Buf(torch.int64, dev)]
+        self._ahead = None         # the prepared batch whose keys already arrived
+        self._ahead_no = 0
+        self.early_key_exchanges = 0  # steps whose next keys rode with the gradients
+        self.mid_step_waits = 0       # of those, split-size reads that waited
         # one per server buffer: compact-FM applies read the values served
         # by their step's pull (the async step applies after the next pull)
         self._vals_out = [_Buf(torch.float32, dev), _Buf(torch.float32, dev)]
@@ -120,6 +127,9 @@ class ShardedEngine:
         self.host_waits = 0        # split-size reads that found the copy still in flight
         self.inline_prepares = 0   # steps whose batch was not prepared ahead (epoch starts)
         self.drop_exchanges = 0    # fault injection (utils/faults.py drop_a2a): skip exchanges
+        # the next batch's key exchange joins this step's gradient exchange
+        # (XFLOW_EARLY_KEYS=0: its own exchange at the next step's start)
+        self.early_keys = os.environ.get("XFLOW_EARLY_KEYS", "1") != "0"
         self.empty_steps = 0       # steps every rank passed without data (loop ends)
         self._counts_host = None
         self._counts_ready = None
@@ -274,11 +284,14 @@ class ShardedEngine:
             self.engine.download_small(self._counts_host[wb], both)
             self._counts_ready[wb].record()
 
-    def _take(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None):
+    def _take(self, batch: Batch, prefetch: Optional[Callable[[], None]] = None,
+              mid_step: bool = False):
         """(worker buffer set, send splits, recv splits, prefetch, any data) of
         ``batch``, preparing it now unless it is the batch prepared ahead.
         A count of -1 marks a source without data (Engine.w_prepare on a
-        batch of 0 rows); any data = some source (this rank included) has rows."""
+        batch of 0 rows); any data = some source (this rank included) has rows.
+        mid_step: read for the early key exchange (a wait is expected there
+        and counted in mid_step_waits)."""
         if self._prep is None or self._prep[0] is not batch:
             self.inline_prepares += 1
             self.prepare(batch)
@@ -292,7 +305,10 @@ class ShardedEngine:
         if both.is_cuda:
             ev = self._counts_ready[wb]
             if not ev.query():
-                self.host_waits += 1
+                if mid_step:
+                    self.mid_step_waits += 1
+                else:
+                    self.host_waits += 1
                 ev.synchronize()
             both = self._counts_host[wb].tolist()
         else:
@@ -351,12 +367,24 @@ class ShardedEngine:
         S = int(S) if S else e.slices_of(batch)
         ps = e.value_width  # floats per pulled value row
         ordered_masks = S > 1 and not e.cfg.sum_slices
-        wb, send_splits, recv_splits, prefetch, any_data = self._take(batch, prefetch)
+        ahead = self._ahead
+        self._ahead = None
+        if ahead is not None and ahead["batch"] is batch:
+            # prepared AND its keys received during the previous step
+            wb, send_splits, recv_splits, any_data = (ahead["wb"], ahead["send"], ahead["recv"],
+                                                      ahead["any"])
+            self.last_send, self.last_recv = ahead["n_send"], ahead["n_recv"]
+        else:
+            if ahead is not None:
+                raise RuntimeError("train_step: the batch whose keys were exchanged ahead was "
+                                   "not trained next (pass the next_batch of the previous step)")
+            wb, send_splits, recv_splits, prefetch, any_data = self._take(batch, prefetch)
         if not any_data:
             self.empty_steps += 1
             return False
         n_send, n_recv = self.last_send, self.last_recv
-        recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
+        recv_keys = (ahead["keys"] if ahead is not None
+                     else self._exchange_keys(wb, send_splits, recv_splits))
         offsets = self._offsets(recv_splits)
         vals = self._vals_out[0].get(n_recv * ps).view(n_recv, ps)
         e.s_pull(recv_keys, n_recv, vals, insert=True, buf=0, offsets=offsets)
@@ -387,6 +415,20 @@ class ShardedEngine:
             ops = [(grads_in, grads_out, recv_splits, send_splits)]
             if ordered_masks:  # slice masks in the same group call
                 ops.append((masks_in, masks_out, recv_splits, send_splits))
+            if next_batch is not None and self.early_keys:
+                # the next batch's keys ride in this group call: its split sizes
+                # came with the values exchange above, so the host reads them
+                # now -- while the device still runs this step's forward/backward
+                # -- and a steady-state step makes two exchanges, not three
+                wb2, ss2, rs2, _, any2 = self._take(next_batch, mid_step=True)
+                n2s, n2r = self.last_send, self.last_recv
+                self._ahead_no ^= 1
+                rk2 = self._recv_keys_ahead[self._ahead_no].get(n2r)
+                ops.append((rk2, self._send_keys[wb2][:n2s], rs2, ss2))
+                self._ahead = dict(batch=next_batch, wb=wb2, send=ss2, recv=rs2, any=any2,
+                                   n_send=n2s, n_recv=n2r, keys=rk2)
+                self.early_key_exchanges += 1
+                self.last_send, self.last_recv = n_send, n_recv
             self._a2a_ops(ops)
         e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
         e.w_finish()
@@ -399,6 +441,9 @@ class ShardedEngine:
         e = self.engine
         if pctr is None:
             pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
+        # (keys exchanged ahead for a training batch no step will take now:
+        # every rank drops them at the same point)
+        self._ahead = None
         wb, send_splits, recv_splits, _, _ = self._take(batch)
         recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
         ps = e.value_width  # floats per pulled value row

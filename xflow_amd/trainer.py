@@ -303,6 +303,7 @@ class Trainer:
                 # steps whose batch was not prepared ahead (the epoch's first)
                 rec["host_waits"] = sh.host_waits - w0[0]
                 rec["inline_prepares"] = sh.inline_prepares - w0[1]
+                rec["early_key_exchanges"] = getattr(sh, "early_key_exchanges", 0)
             if self.cfg.optim.lambda1 > 0 and os.environ.get("XFLOW_REPORT_NNZ"):
                 rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
                                                            self.device)[0])
