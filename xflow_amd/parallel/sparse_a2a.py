@@ -375,9 +375,9 @@ class ShardedEngine:
                                                       ahead["any"])
             self.last_send, self.last_recv = ahead["n_send"], ahead["n_recv"]
         else:
-            if ahead is not None:
-                raise RuntimeError("train_step: the batch whose keys were exchanged ahead was "
-                                   "not trained next (pass the next_batch of the previous step)")
+            # (a batch other than the announced next one: the keys exchanged
+            # ahead are dropped -- every rank drops them at the same step, as a
+            # prepared batch that is not trained next always was)
             wb, send_splits, recv_splits, prefetch, any_data = self._take(batch, prefetch)
         if not any_data:
             self.empty_steps += 1
