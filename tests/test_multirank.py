@@ -162,6 +162,8 @@ def _trainer_worker(rank, world, data_dir, pred_dir):
         assert len(ep) == 3 and all(r["steps"] > 3 * (i + 1) for i, r in enumerate(ep))
         # one batch per epoch is prepared in line (the first); no step waited
         assert all(r["inline_prepares"] == 1 and r["host_waits"] == 0 for r in ep), ep
+        # steady state: the next batch's keys ride in the gradient exchange
+        assert ep[-1]["early_key_exchanges"] >= ep[-1]["steps"] - 3 * len(ep), ep
 
 
 def test_trainer_two_workers_bundled_data(tmp_path):
