@@ -12,7 +12,9 @@ fm_worker.cc:228-242, the ps-lite DefaultSlicer, ftrl.h:38-152):
                   per-step collective); the split sizes return through pinned
                   memory and are read when the batch's step starts -- with
                   next_batch, one step after they were produced (see prepare)
-  3. a2a keys     -> each owner receives the keys it serves
+  3. a2a keys     -> each owner receives the keys it serves (steady state:
+                  already received, in the previous step's gradient group
+                  call -- two group calls per step, see early_keys)
   4. s_pull       owner probes/inserts its shard, evaluates pull values
   5. a2a values   -> back to the requesting workers (send order)
   6. w_forward_backward  fused fwd/bwd on the rank's rows, per-(key,slice)
