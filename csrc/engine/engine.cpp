@@ -179,6 +179,7 @@ Engine::~Engine() {
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_,
                   lr_mask_};
   for (void* p : ptrs) be.free(p);
+  for (void* p : stage_io_) be.staging_free(p);
   for (SrvBuf& b : srv_) {
     void* bp[] = {b.slots, b.nz, b.w, b.own_pos, b.own_idx};
     for (void* p : bp) be.free(p);
@@ -1214,80 +1215,199 @@ void Engine::stage_release() {
 // ---------------------------------------------------------------------------
 // checkpoint
 // ---------------------------------------------------------------------------
-void Engine::export_table(std::vector<u64>& keys, std::vector<u32>& words) {
+// Checkpoint transfers stream through two pinned staging buffers: a table of
+// 1e9 LR keys is 16 GB of keys + state, and a pageable copy of it (plus the
+// zero-fill of the destination) ran at ~2.6 GB/s (profiles/r3s3_table_ops.txt).
+constexpr size_t kStageChunk = 64u << 20;
+
+// host memcpy of one staged chunk, split over a few threads (a single thread
+// copies well below the DMA rate)
+static void par_copy(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kPiece = 8u << 20;
+  const size_t parts = bytes / kPiece;
+  if (parts < 2) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t nt = parts < 8 ? parts : 8, per = (bytes + nt - 1) / nt;
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) {
+    const size_t o = t * per;
+    if (o >= bytes) break;
+    const size_t n = bytes - o < per ? bytes - o : per;
+    th.emplace_back([=] { std::memcpy((char*)dst + o, (const char*)src + o, n); });
+  }
+  std::memcpy(dst, src, per < bytes ? per : bytes);
+  for (std::thread& x : th) x.join();
+}
+
+template <typename Sink>
+void Engine::d2h_stream(const void* src, size_t bytes, Sink sink) {
+  if (bytes == 0) return;
+  for (void*& p : stage_io_)
+    if (!p) p = be_->staging_alloc(kStageChunk);
+  const char* s = static_cast<const char*>(src);
+  int cur = 0;
+  be_->copy_d2h_async(stage_io_[0], s, bytes < kStageChunk ? bytes : kStageChunk);
+  be_->synchronize();
+  for (size_t off = 0; off < bytes;) {
+    const size_t len = bytes - off < kStageChunk ? bytes - off : kStageChunk;
+    const size_t nxt = off + len;
+    if (nxt < bytes)  // the next chunk's DMA runs while the host consumes this one
+      be_->copy_d2h_async(stage_io_[cur ^ 1], s + nxt,
+                          bytes - nxt < kStageChunk ? bytes - nxt : kStageChunk);
+    sink(stage_io_[cur], off, len);
+    be_->synchronize();
+    off = nxt;
+    cur ^= 1;
+  }
+}
+
+template <typename Fill>
+void Engine::h2d_stream(void* dst, size_t bytes, Fill fill) {
+  if (bytes == 0) return;
+  for (void*& p : stage_io_)
+    if (!p) p = be_->staging_alloc(kStageChunk);
+  char* d = static_cast<char*>(dst);
+  int cur = 0;
+  for (size_t off = 0; off < bytes;) {
+    const size_t len = bytes - off < kStageChunk ? bytes - off : kStageChunk;
+    fill(stage_io_[cur], off, len);  // overlaps the previous chunk's DMA
+    be_->synchronize();              // (that DMA read the other buffer)
+    be_->copy_h2d_async(d + off, stage_io_[cur], len);
+    off += len;
+    cur ^= 1;
+  }
+  be_->synchronize();
+}
+
+void Engine::export_into(u64* keys, u32* words, int64_t n) {
   const int W = state_words();
-  int64_t n = table_size();
-  keys.assign((size_t)n, 0);
-  words.assign((size_t)n * W, 0);
+  if (n != table_size()) throw std::invalid_argument("export_into: n must equal table_size()");
   if (n == 0) return;
   u64* dk = balloc<u64>(*be_, n);
   u32* dw = balloc<u32>(*be_, n * W);
-  int64_t got = be_->table_export(table_, dk, dw, n);
-  if (got != n) {
-    be_->free(dk);
-    be_->free(dw);
-    throw std::runtime_error("export_table: live slot count mismatch");
+  const int64_t got = be_->table_export(table_, dk, dw, n);
+  if (got == n) {
+    d2h_stream(dk, sizeof(u64) * n, [&](const void* c, size_t o, size_t b) {
+      par_copy((char*)keys + o, c, b);
+    });
+    d2h_stream(dw, sizeof(u32) * n * W, [&](const void* c, size_t o, size_t b) {
+      par_copy((char*)words + o, c, b);
+    });
   }
-  be_->copy_d2h(keys.data(), dk, sizeof(u64) * n);
-  be_->copy_d2h(words.data(), dw, sizeof(u32) * n * W);
+  be_->free(dk);
+  be_->free(dw);
+  if (got != n) throw std::runtime_error("export_table: live slot count mismatch");
+}
+
+void Engine::export_table(std::vector<u64>& keys, std::vector<u32>& words) {
+  const int64_t n = table_size();
+  keys.resize((size_t)n);
+  words.resize((size_t)n * state_words());
+  export_into(keys.data(), words.data(), n);
+}
+
+// device arrays of n (key, state) pairs -> the table
+void Engine::table_from_device(const u64* dk, const u32* dw, int64_t n) {
+  be_->table_import(table_, dk, dw, n);
+  be_->synchronize();
+  (void)table_size();  // (re-bases the capacity monitor)
+}
+
+void Engine::import_from(const u64* keys, const u32* words, int64_t n) {
+  stale_stashes();  // the table changes: server stashes are stale
+  const int W = state_words();
+  if (n <= 0) return;
+  guard_inserts(n);
+  u64* dk = balloc<u64>(*be_, n);
+  u32* dw = balloc<u32>(*be_, n * W);
+  h2d_stream(dk, sizeof(u64) * n, [&](void* c, size_t o, size_t b) {
+    par_copy(c, (const char*)keys + o, b);
+  });
+  h2d_stream(dw, sizeof(u32) * n * W, [&](void* c, size_t o, size_t b) {
+    par_copy(c, (const char*)words + o, b);
+  });
+  table_from_device(dk, dw, n);
   be_->free(dk);
   be_->free(dw);
 }
 
 void Engine::import_table(const std::vector<u64>& keys, const std::vector<u32>& words) {
-  stale_stashes();  // the table changes: server stashes are stale
-  const int W = state_words();
   const int64_t n = (int64_t)keys.size();
-  if ((int64_t)words.size() != n * W) throw std::invalid_argument("import_table: size mismatch");
-  if (n == 0) return;
-  guard_inserts(n);
-  u64* dk = balloc<u64>(*be_, n);
-  u32* dw = balloc<u32>(*be_, n * W);
-  be_->copy_h2d(dk, keys.data(), sizeof(u64) * n);
-  be_->copy_h2d(dw, words.data(), sizeof(u32) * n * W);
-  be_->table_import(table_, dk, dw, n);
-  be_->synchronize();
-  be_->free(dk);
-  be_->free(dw);
-  (void)table_size();  // (re-bases the capacity monitor)
+  if ((int64_t)words.size() != n * state_words())
+    throw std::invalid_argument("import_table: size mismatch");
+  import_from(keys.data(), words.data(), n);
 }
 
+// Shard file: the device export streams chunk by chunk from the staging
+// buffers to the file (no whole-table host copy).
 void Engine::save(const std::string& path) {
-  std::vector<u64> keys;
-  std::vector<u32> words;
-  export_table(keys, words);
-  std::ofstream f(path, std::ios::binary);
+  const int W = state_words();
+  const int64_t n = table_size();
+  std::FILE* f = std::fopen(path.c_str(), "wb");
   if (!f) throw std::runtime_error("cannot open " + path);
+  bool ok = true;
   int32_t hdr[8] = {1, cfg_.model.kind, cfg_.model.v_dim, table_.L.P,
                     table_.L.p_w, table_.L.opt, table_.L.stride, 0};
-  uint64_t n = keys.size();
-  f.write(kMagic, 8);
-  f.write(reinterpret_cast<const char*>(hdr), sizeof(hdr));
-  f.write(reinterpret_cast<const char*>(&n), sizeof(n));
-  f.write(reinterpret_cast<const char*>(keys.data()), sizeof(u64) * n);
-  f.write(reinterpret_cast<const char*>(words.data()), sizeof(u32) * words.size());
-  if (!f) throw std::runtime_error("write failed: " + path);
+  const uint64_t un = (uint64_t)n;
+  ok = ok && std::fwrite(kMagic, 1, 8, f) == 8;
+  ok = ok && std::fwrite(hdr, sizeof(hdr), 1, f) == 1;
+  ok = ok && std::fwrite(&un, sizeof(un), 1, f) == 1;
+  if (n > 0 && ok) {
+    u64* dk = balloc<u64>(*be_, n);
+    u32* dw = balloc<u32>(*be_, n * W);
+    const int64_t got = be_->table_export(table_, dk, dw, n);
+    if (got == n) {
+      auto put = [&](const void* c, size_t, size_t b) {
+        ok = ok && std::fwrite(c, 1, b, f) == b;
+      };
+      d2h_stream(dk, sizeof(u64) * n, put);
+      d2h_stream(dw, sizeof(u32) * n * W, put);
+    }
+    be_->free(dk);
+    be_->free(dw);
+    if (got != n) {
+      std::fclose(f);
+      throw std::runtime_error("export_table: live slot count mismatch");
+    }
+  }
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok) throw std::runtime_error("write failed: " + path);
 }
 
 void Engine::load(const std::string& path) {
-  std::ifstream f(path, std::ios::binary);
+  std::FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) throw std::runtime_error("cannot open " + path);
   char magic[8];
   int32_t hdr[8];
   uint64_t n = 0;
-  f.read(magic, 8);
-  f.read(reinterpret_cast<char*>(hdr), sizeof(hdr));
-  f.read(reinterpret_cast<char*>(&n), sizeof(n));
-  if (!f || std::memcmp(magic, kMagic, 8) != 0) throw std::runtime_error("bad checkpoint " + path);
+  bool ok = std::fread(magic, 1, 8, f) == 8 && std::fread(hdr, sizeof(hdr), 1, f) == 1 &&
+            std::fread(&n, sizeof(n), 1, f) == 1;
+  if (!ok || std::memcmp(magic, kMagic, 8) != 0) {
+    std::fclose(f);
+    throw std::runtime_error("bad checkpoint " + path);
+  }
   if (hdr[1] != cfg_.model.kind || hdr[3] != table_.L.P || hdr[5] != table_.L.opt ||
-      hdr[6] != table_.L.stride)
+      hdr[6] != table_.L.stride) {
+    std::fclose(f);
     throw std::runtime_error("checkpoint layout does not match this model/optimizer");
-  std::vector<u64> keys(n);
-  std::vector<u32> words(n * (size_t)state_words());
-  f.read(reinterpret_cast<char*>(keys.data()), sizeof(u64) * n);
-  f.read(reinterpret_cast<char*>(words.data()), sizeof(u32) * words.size());
-  if (!f) throw std::runtime_error("truncated checkpoint " + path);
-  import_table(keys, words);
+  }
+  const int W = state_words();
+  stale_stashes();
+  if (n > 0) {
+    guard_inserts((int64_t)n);
+    u64* dk = balloc<u64>(*be_, n);
+    u32* dw = balloc<u32>(*be_, n * W);
+    auto get = [&](void* c, size_t, size_t b) { ok = ok && std::fread(c, 1, b, f) == b; };
+    h2d_stream(dk, sizeof(u64) * n, get);
+    h2d_stream(dw, sizeof(u32) * n * W, get);
+    if (ok) table_from_device(dk, dw, (int64_t)n);
+    be_->free(dk);
+    be_->free(dw);
+  }
+  std::fclose(f);
+  if (!ok) throw std::runtime_error("truncated checkpoint " + path);
 }
 
 }  // namespace xflow

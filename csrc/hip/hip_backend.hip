@@ -104,6 +104,20 @@ class HipBackend final : public Backend {
     if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream_));
     XF_HIP_CHECK(hipStreamSynchronize(stream_));
   }
+  void copy_d2h_async(void* dst, const void* src, size_t bytes) override {
+    if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream_));
+  }
+  void copy_h2d_async(void* dst, const void* src, size_t bytes) override {
+    if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream_));
+  }
+  void* staging_alloc(size_t bytes) override {
+    void* p = nullptr;
+    XF_HIP_CHECK(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault));
+    return p;
+  }
+  void staging_free(void* p) override {
+    if (p) (void)hipHostFree(p);
+  }
   void copy_d2d(void* dst, const void* src, size_t bytes) override {
     if (bytes) XF_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream_));
   }

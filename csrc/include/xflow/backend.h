@@ -376,6 +376,13 @@ class Backend {
   virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;
   virtual void copy_d2h(void* dst, const void* src, size_t bytes) = 0;  // synchronising
   virtual void copy_d2d(void* dst, const void* src, size_t bytes) = 0;
+  // queued on the stream, no host wait (checkpoint streaming through pinned
+  // staging buffers; the CPU backend copies at once)
+  virtual void copy_d2h_async(void* dst, const void* src, size_t bytes) { copy_d2h(dst, src, bytes); }
+  virtual void copy_h2d_async(void* dst, const void* src, size_t bytes) { copy_h2d(dst, src, bytes); }
+  // page-locked host memory for DMA staging (HIP: non-coherent pinned)
+  virtual void* staging_alloc(size_t bytes) { return host_alloc(bytes); }
+  virtual void staging_free(void* p) { host_free(p); }
   // <= 256 bytes from the host, queued without a host wait (HIP: the bytes
   // travel as a kernel argument)
   virtual void upload_small(void* dst, const void* src, size_t bytes) = 0;

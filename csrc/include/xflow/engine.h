@@ -162,6 +162,12 @@ class Engine {
   // Host copies of every live slot: keys + (stride-2) state words each.
   void export_table(std::vector<u64>& keys, std::vector<u32>& words);
   void import_table(const std::vector<u64>& keys, const std::vector<u32>& words);
+  // The same into / from caller memory of n keys and n * state_words()
+  // words (n = table_size() for export), streamed through two pinned
+  // staging buffers so the DMA of one chunk overlaps the host copy of the
+  // previous one.
+  void export_into(u64* keys, u32* words, int64_t n);
+  void import_from(const u64* keys, const u32* words, int64_t n);
   int state_words() const { return table_.L.stride - 2; }
   const TableLayout& layout() const { return table_.L; }
   // Binary shard file: header + keys + state words.
@@ -181,6 +187,16 @@ class Engine {
   void stage_release();
 
  private:
+  // chunked device<->host transfer through the staging pair (export / save,
+  // import / load): sink(host chunk, byte offset, bytes) consumes each chunk
+  // while the next one is in flight; fill(host chunk, offset, bytes)
+  // produces each chunk while the previous one uploads
+  template <typename Sink>
+  void d2h_stream(const void* src, size_t bytes, Sink sink);
+  template <typename Fill>
+  void h2d_stream(void* dst, size_t bytes, Fill fill);
+  void table_from_device(const u64* dk, const u32* dw, int64_t n);
+  void* stage_io_[2] = {nullptr, nullptr};
   void ensure_server_capacity(int64_t n, int buf = 0);
   // worker buffer sets (see w_prepare): the members pos_, uniq_pos_, inv_,
   // n_uniq_, send_pos_, send_map_, inv_valid_ describe set cur_wb_

@@ -370,19 +370,31 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def("nonzero_weights", &Engine::nonzero_weights)
       .def("export_table",
            [](Engine& e) {
-             std::vector<u64> k;
-             std::vector<u32> w;
-             e.export_table(k, w);
-             return py::make_tuple(to_np(k), to_np(w));
+             // straight into the returned arrays (no zero-fill, no extra copy)
+             const int64_t n = e.table_size();
+             py::array_t<uint64_t> k((py::ssize_t)n);
+             py::array_t<uint32_t> w((py::ssize_t)(n * e.state_words()));
+             u64* kp = reinterpret_cast<u64*>(k.mutable_data());
+             u32* wp = reinterpret_cast<u32*>(w.mutable_data());
+             {
+               py::gil_scoped_release nogil;
+               e.export_into(kp, wp, n);
+             }
+             return py::make_tuple(k, w);
            })
       .def("import_table",
-           [](Engine& e, py::array_t<uint64_t> keys, py::array_t<uint32_t> words) {
-             std::vector<u64> k(keys.data(), keys.data() + keys.size());
-             std::vector<u32> w(words.data(), words.data() + words.size());
-             e.import_table(k, w);
+           [](Engine& e, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> keys,
+              py::array_t<uint32_t, py::array::c_style | py::array::forcecast> words) {
+             const int64_t n = (int64_t)keys.size();
+             if ((int64_t)words.size() != n * e.state_words())
+               throw std::invalid_argument("import_table: size mismatch");
+             const u64* kp = reinterpret_cast<const u64*>(keys.data());
+             const u32* wp = reinterpret_cast<const u32*>(words.data());
+             py::gil_scoped_release nogil;
+             e.import_from(kp, wp, n);
            })
-      .def("save", &Engine::save)
-      .def("load", &Engine::load)
+      .def("save", &Engine::save, py::call_guard<py::gil_scoped_release>())
+      .def("load", &Engine::load, py::call_guard<py::gil_scoped_release>())
       .def("synth_batch",
            [](Engine& e, int64_t rows, std::vector<uint64_t> vocab, std::vector<float> zipf,
               uint64_t hash_space, uint64_t seed, uint64_t step, float scale, float bias,
