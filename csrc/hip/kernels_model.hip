@@ -1713,7 +1713,13 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
         for (int j = 0; j < len; ++j) {
           float c[D];
           contrib(j, c);
-          float* g = a.grad + ((size_t)pos[rs.at(j)] * S + s) * PS;
+          const u32 pj = pos[rs.at(j)];
+          float* g = a.grad + ((size_t)pj * S + s) * PS;
+          if (a.red_out) {  // (one slice: the unique-order rows k_mvm_red_sum adds to)
+            const u32 o = a.red_inv[pj];
+            if (o == 0xFFFFFFFFu) continue;
+            g = a.red_out + (size_t)o * PS;
+          }
 #pragma unroll
           for (int k = 0; k < D; ++k) atomicAdd(&g[k], c[k]);
         }
@@ -1802,6 +1808,8 @@ static bool mvm_atomics_forced() {
 
 struct MvmRedFinal {
   float* grad;
+  float* out;        // one slice: unique-order rows out[inv[dest]] (FwdArgs::red_out), or null
+  const u32* inv;
   const float* wpull;
   const float* rowv;
   int S, nb;
@@ -1877,6 +1885,15 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
   for (u32 l = threadIdx.x; l < kSub; l += kRedBlock) {
     const u64 dest = d0 + l;
     float* g = f.grad + dest * PS;
+    if (f.out) {  // (one slice: dest = slot; keys of this step only reach acc)
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < D; ++k) any = any || acc[l * D + k] != 0.0f;
+      if (!any) continue;
+      const u32 o = f.inv[dest];
+      if (o == 0xFFFFFFFFu) continue;
+      g = f.out + (u64)o * PS;
+    }
     const float* w = f.wpull + (dest / (u64)f.S) * PS;
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -1899,7 +1916,9 @@ static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
                      red_geom(a));
   const int nsubt = mvm_nsub(D) * a.red_nsub;
   const int grid = ((a.red_nb + 7) / 8) * 8 * nsubt;
-  MvmRedFinal f{a.grad, a.wpull, a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
+  if (a.red_out && (a.S != 1 || !a.red_inv))
+    throw std::runtime_error("MVM red_out: one slice and the slot -> unique map");
+  MvmRedFinal f{a.grad, a.red_out, a.red_inv, a.wpull, a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
   hipLaunchKernelGGL(k_mvm_red_sum<D>, dim3(grid), dim3(kRedBlock), 0, st,
                      reinterpret_cast<const u64*>(a.red_sorted), static_cast<const u32*>(start), f);
 }
@@ -1914,6 +1933,8 @@ static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
   case DD: {                                                                             \
     constexpr int B = mvm_block(DD);                                                     \
     const int g = (int)((a.batch.rows + B - 1) / B);                                     \
+    if (a.red_out && !red)                                                               \
+      throw std::runtime_error("MVM red_out needs the bucket reduction");                \
     if (red) {                                                                           \
       constexpr int R = kMvmGroupRows;                                                   \
       const int gr = (int)((a.batch.rows + R - 1) / R);                                  \
