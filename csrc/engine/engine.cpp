@@ -176,7 +176,7 @@ Engine::~Engine() {
                   stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_, mvm_grad_,
+                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_, row_grad_,
                   lr_mask_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
@@ -362,18 +362,23 @@ void Engine::train_step(const BatchView& b) {
     ensure_inv();
     if (!fm_grad_) fm_grad_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   }
-  // MVM, one slice, on the reduction path: the per-key gradient rows land in
-  // unique order too (a dense apply read instead of slot-indexed rows the
-  // apply had to zero after reading; XFLOW_MVM_SLOT_GRADS=1 restores those)
-  static const bool mvm_slot = std::getenv("XFLOW_MVM_SLOT_GRADS") != nullptr ||
-                               std::getenv("XFLOW_MVM_ATOMICS") != nullptr;
-  const bool mvmu = be_->is_gpu() && cfg_.model.kind == kMVM && S == 1 && red_pairs_ &&
-                    red_rowv_ && !mvm_slot && (double)scratch_.cap * ps < 4294967295.0;
-  if (mvmu) {
+  // MVM and standard-math FM, one slice, on their reduction paths: the
+  // per-key gradient rows land in unique order too (a dense apply read
+  // instead of slot-indexed rows the apply had to zero after reading;
+  // XFLOW_SLOT_GRAD_ROWS=1 restores those)
+  static const bool slot_rows = std::getenv("XFLOW_SLOT_GRAD_ROWS") != nullptr;
+  const bool rows_ok = be_->is_gpu() && S == 1 && red_pairs_ && !slot_rows &&
+                       (double)scratch_.cap * ps < 4294967295.0;
+  const bool mvmu = rows_ok && cfg_.model.kind == kMVM && red_rowv_ &&
+                    std::getenv("XFLOW_MVM_ATOMICS") == nullptr;
+  const bool fsu = rows_ok && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard &&
+                   std::getenv("XFLOW_FMSTD_ATOMICS") == nullptr;
+  const bool rowu = mvmu || fsu;
+  if (rowu) {
     ensure_inv();
-    if (!mvm_grad_) mvm_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps);
+    if (!row_grad_) row_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps);
   }
-  dedup_(b, 1, nullptr, lr16 || fmu || mvmu);
+  dedup_(b, 1, nullptr, lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)
   guard_inserts(b.nnz);  // (<= nnz new keys; may grow the table first)
 
@@ -399,8 +404,8 @@ void Engine::train_step(const BatchView& b) {
     pa.zero_out = fm_grad_;
     pa.zero_width = 2;
   }
-  if (mvmu) {
-    pa.zero_out = mvm_grad_;
+  if (rowu) {
+    pa.zero_out = row_grad_;
     pa.zero_width = ps;
   }
   be_->table_pull(pa);
@@ -434,8 +439,8 @@ void Engine::train_step(const BatchView& b) {
     fa.red_out = fm_grad_;
     fa.red_inv = inv_;
   }
-  if (mvmu) {
-    fa.red_out = mvm_grad_;
+  if (rowu) {
+    fa.red_out = row_grad_;
     fa.red_inv = inv_;
   }
   be_->forward_backward(fa);
@@ -475,8 +480,8 @@ void Engine::train_step(const BatchView& b) {
     aa.zero_after = false;
     aa.gstride = 2;
   }
-  if (mvmu) {  // unique-order rows, zeroed by the next pull
-    aa.grads = mvm_grad_;
+  if (rowu) {  // unique-order rows, zeroed by the next pull
+    aa.grads = row_grad_;
     aa.grad_map = nullptr;
     aa.zero_after = false;
     aa.gstride = ps;

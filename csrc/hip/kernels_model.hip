@@ -1219,7 +1219,9 @@ template <int D>
 __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restrict__ sorted,
                                                            const u32* __restrict__ start,
                                                            float* __restrict__ grad,
-                                                           RedGeom geom, int nb) {
+                                                           RedGeom geom, int nb,
+                                                           float* __restrict__ out,
+                                                           const u32* __restrict__ inv) {
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
@@ -1266,7 +1268,13 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
       float o[PS];
 #pragma unroll
       for (int c = 0; c < PS; ++c) o[c] = c < NV ? (float)fx_to_double<kFx>(acc[l * NV + c]) : 0.0f;
-      float4* g4 = reinterpret_cast<float4*>(grad + (lo + l) * PS);
+      float* row = grad + (lo + l) * PS;
+      if (out) {  // one slice: the unique-order row (FwdArgs::red_out)
+        const u32 u = inv[lo + l];
+        if (u == 0xFFFFFFFFu) continue;
+        row = out + (u64)u * PS;
+      }
+      float4* g4 = reinterpret_cast<float4*>(row);
 #pragma unroll
       for (int q = 0; q < PS / 4; ++q) g4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
     }
@@ -1289,8 +1297,11 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
                      geom);
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
+  if (a.red_out && (a.S != 1 || !a.red_inv))
+    throw std::runtime_error("standard FM red_out: one slice and the slot -> unique map");
   hipLaunchKernelGGL(k_red_sum_vec<D>, dim3(grid), dim3(kRedBlock), 0, st,
-                     static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb);
+                     static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
+                     a.red_out, a.red_inv);
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
@@ -1510,6 +1521,8 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   // standard math: per-component records through the LR reduction pipeline
   const bool red_std = agg && a.model.fm_math == kFmStandard && a.red_pairs && a.red_nb > 0 &&
                        a.red_nb <= kRedMaxBuckets && !a.red_masks && !fmstd_atomics_forced();
+  if (a.red_out && a.model.fm_math == kFmStandard && !red_std)
+    throw std::runtime_error("standard FM red_out needs the vector-record reduction");
   switch (a.model.v_dim) {
 #define XF_FM_CASE(DD)                                                                   \
   case DD: {                                                                             \

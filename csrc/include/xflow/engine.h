@@ -265,7 +265,7 @@ class Engine {
   int64_t nnz_seen_ = 0;          // most occurrences in one batch (ScratchView::grow)
   u32* lr_mask_ = nullptr;       // LR-FTRL fused step, S > 1: unique-order slice bits [max_nnz]
   float* fm_grad_ = nullptr;     // reference FM fused step: unique-order (B, C) [max_nnz][2]
-  float* mvm_grad_ = nullptr;    // MVM fused step (one slice): unique-order rows [max_nnz][pstride]
+  float* row_grad_ = nullptr;    // MVM / standard FM fused step (one slice): unique-order rows [max_nnz][pstride]
   int red_nb_ = 0;
   int red_nsub_ = 1;
   unsigned long long* bcap_ = nullptr;  // current worker set's batch scratch capacity
