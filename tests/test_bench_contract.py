@@ -22,7 +22,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(n, extra, cpu=True):
+def _run(n, extra, cpu=True, env_extra=None):
     args = ["--gpus", str(n), "--steps", "2", "--warmup", "1"] + (["--cpu"] if cpu else []) + extra
     if n == 1:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
@@ -30,7 +30,7 @@ def _run(n, extra, cpu=True):
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
                "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py")] + args
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2", **(env_extra or {}))
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -66,3 +66,22 @@ def test_bench_json_line_on_gpu(gpu_device, extra):
     assert d["config"]["backend"].startswith("hip:gfx950")
     assert d["table_load"] > 0.4 and d["prefilled_keys"] > 0
     assert 0.0 < d["logloss"] < 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,extra", [(2, []), (2, ["--async"]), (3, ["--model", "fm", "--v-dim", "8"])])
+def test_bench_multirank_rccl_on_one_gpu(gpu_device, n, extra):
+    """The driver's multi-GPU launch (torch.distributed.run, one process per
+    rank, RCCL) with every rank on this box's GPU 0 (XFLOW_SHARED_GPU=1:
+    RCCL's socket transport between the processes, parallel/dist.py): the
+    contract line of the N-rank bench, the native RCCL transport, the
+    steady-state two-exchange step (keys exchanged ahead), no overflow."""
+    d = _run(n, extra + ["--batch", "16384", "--log2-cap", "24", "--clock-warmup-s", "0"],
+             cpu=False, env_extra={"XFLOW_SHARED_GPU": "1"})
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == n and d["shared_gpu_rehearsal"] is True
+    assert d["config"]["a2a_transport"] == "rccl"
+    assert d["config"]["global_batch"] == 16384 * n
+    if "--async" not in extra:
+        assert d["early_key_exchanges"] >= d["steps"]
+    assert 0.0 < d["logloss"] < 1.0 and d["table_keys"] > 0
