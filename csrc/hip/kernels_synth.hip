@@ -20,6 +20,7 @@ struct SynthConsts {
 // them in field order (deterministic, the same order as the CPU backend).
 constexpr int kSynthRows = 64;
 
+template <bool kSmall>
 __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
   __shared__ float pw[kSynthRows * kSynthMaxFields];
   __shared__ u64 rseed[kSynthRows];
@@ -43,7 +44,7 @@ __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
       f = e - rl * F;
     }
     float w;
-    const u64 key = synth_sample(rseed[rl], f, fc[f], a.hash_space, a.planted_scale, w);
+    const u64 key = synth_sample<kSmall>(rseed[rl], f, fc[f], a.hash_space, a.planted_scale, w);
     const int64_t o = field_major ? (int64_t)f * a.col_stride + r0 + rl : r0 * F + e;
     a.keys[o] = key;
     if (a.fgid) a.fgid[o] = f;
@@ -62,8 +63,11 @@ void launch_synth(const SynthArgs& a, hipStream_t st) {
   if (a.fields > kSynthMaxFields) throw std::runtime_error("synth: at most 64 fields");
   SynthConsts c;
   for (int f = 0; f < a.fields; ++f) c.f[f] = synth_field(a.vocab[f], (double)a.zipf_s[f]);
-  hipLaunchKernelGGL(k_synth, dim3((int)((a.rows + kSynthRows - 1) / kSynthRows)), dim3(kBlock),
-                     0, st, a, c);
+  const dim3 grid((int)((a.rows + kSynthRows - 1) / kSynthRows));
+  if (synth_small_ok(a.vocab, a.fields, a.hash_space))
+    hipLaunchKernelGGL(k_synth<true>, grid, dim3(kBlock), 0, st, a, c);
+  else
+    hipLaunchKernelGGL(k_synth<false>, grid, dim3(kBlock), 0, st, a, c);
   XF_HIP_CHECK(hipGetLastError());
 }
 

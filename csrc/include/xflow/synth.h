@@ -120,21 +120,51 @@ inline SynthField synth_field(u64 vocab, double s) {
   return F;
 }
 
+// High 64 bits of a * b for b < 2^32: a*b = ah*b*2^32 + al*b, and
+// floor((ah*b + floor(al*b / 2^32)) / 2^32) is exact (the sum < 2^64).  Three
+// 32-bit multiplies on gfx950 instead of the general form's seven.
+XF_HD u64 mulhi64_u32(u64 a, u32 b) {
+  const u64 lo_hi = ((u64)(u32)a * b) >> 32;
+  return ((a >> 32) * (u64)b + lo_hi) >> 32;
+}
+
 // Key of field f for the row, and its planted weight.  Both come from one
 // hash of (field, rank): the key from its high bits (multiply-high into
 // [0, hash_space), no 64-bit division), the weight from its low bits, so
 // every occurrence of a key carries the same planted weight.
+// kSmall: hash_space < 2^32 and every vocab < 2^31 (synth_small_ok, checked
+// once per batch): the same bits through 32-bit rank conversion and the
+// 32-bit multiply-high -- the generator is VALU-bound on 64-bit multiplies.
+template <bool kSmall = false>
 XF_HD u64 synth_sample(u64 rowseed, int f, const SynthField& F, u64 hash_space, float scale,
                        float& weight) {
   const u64 h = fmix64(rowseed + (u64)(f + 1) * 0x94d049bb133111ebull);
   const float u = synth_unit_f(h);
   const float y = F.unit_s ? u * F.log2v1 : synth_log2(F.A * u + 1.0f) * F.inv_e;
-  u64 rank = (u64)synth_exp2(y);
-  if (rank < 1) rank = 1;
-  if (rank > F.vocab) rank = F.vocab;
+  u64 rank;
+  if constexpr (kSmall) {
+    // exp2(y) <= ~(V+1)(1 + 2^-20) < 2^32 for V < 2^31: the u32 conversion
+    // truncates exactly as the u64 one does
+    u32 r32 = (u32)synth_exp2(y);
+    if (r32 < 1u) r32 = 1u;
+    if (r32 > (u32)F.vocab) r32 = (u32)F.vocab;
+    rank = r32;
+  } else {
+    rank = (u64)synth_exp2(y);
+    if (rank < 1) rank = 1;
+    if (rank > F.vocab) rank = F.vocab;
+  }
   const u64 hk = fmix64(((u64)(f + 1) << 40) ^ (rank - 1) ^ 0x3c6ef372fe94f82bull);
   weight = scale * ((float)((u32)hk >> 8) * (2.0f / 16777216.0f) - 1.0f);
+  if constexpr (kSmall) return mulhi64_u32(hk, (u32)hash_space);
   return mulhi64(hk, hash_space);
+}
+
+inline bool synth_small_ok(const u64* vocab, int fields, u64 hash_space) {
+  if (hash_space >> 32) return false;
+  for (int f = 0; f < fields; ++f)
+    if ((vocab[f] ? vocab[f] : 1) >= (1ull << 31)) return false;
+  return true;
 }
 
 XF_HD float synth_label(u64 rowseed, float logit) {

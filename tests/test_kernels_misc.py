@@ -2,6 +2,7 @@
 data generator, FTRL / sigmoid scalar recipes, on the CPU backend and (gpu
 marker) on the gfx950 HIP backend."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -294,3 +295,54 @@ def test_engine_field_major_transpose(devname, rows, F):
     b = Batch(keys=keys, labels=torch.zeros(rows, device=dev), fgid=fg, nnz_per_row=F)
     a, t = b.to_field_major(eng), b.to_field_major()
     assert torch.equal(a.keys, t.keys) and torch.equal(a.fgid, t.fgid) and a.field_major
+
+
+def test_synth_small_fast_path_bit_identical(tmp_path):
+    """synth_sample<true> (32-bit rank conversion and multiply-high, used by
+    k_synth when hash_space < 2^32 and every vocab < 2^31) returns the same
+    key and weight bits as the general 64-bit recipe the CPU backend runs."""
+    import shutil
+    import subprocess
+
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("g++ not available")
+    src = tmp_path / "t.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include <cstring>
+#include <initializer_list>
+#include "xflow/synth.h"
+using namespace xflow;
+int main() {
+  const u64 vocabs[] = {1, 2, 3, 25, 1000, 65536, 10000000, 400000000, (1ull << 31) - 1};
+  const double ss[] = {0.6, 1.0, 1.05, 1.3};
+  const u64 spaces[] = {1, 7, 1000000000ull, (1ull << 32) - 1};
+  long bad = 0, n = 0;
+  for (u64 V : vocabs) for (double s : ss) for (u64 hs : spaces) {
+    const SynthField F = synth_field(V, s);
+    for (u64 r = 0; r < 20000; ++r) {
+      const u64 seed = fmix64(r * 0x9e3779b97f4a7c15ull + V + hs);
+      for (int f = 0; f < 39; f += 7) {
+        float w0, w1;
+        const u64 k0 = synth_sample<false>(seed, f, F, hs, 0.3f, w0);
+        const u64 k1 = synth_sample<true>(seed, f, F, hs, 0.3f, w1);
+        ++n;
+        if (k0 != k1 || memcmp(&w0, &w1, 4) != 0) ++bad;
+      }
+    }
+  }
+  for (u64 a : {0ull, 1ull, ~0ull, 0x8000000000000000ull, 0x123456789abcdefull})
+    for (u64 b : {0ull, 1ull, 0xffffffffull, 1000000000ull})
+      if (mulhi64_u32(a, (u32)b) != mulhi64(a, b)) ++bad;
+  std::printf("%ld %ld\n", n, bad);
+  return bad != 0;
+}
+''')
+    exe = tmp_path / "t"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc", "include")
+    r = subprocess.run([cxx, "-O2", "-std=c++17", "-ffp-contract=off", "-I" + inc, str(src), "-o",
+                        str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
