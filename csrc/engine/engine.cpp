@@ -144,6 +144,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       red_nb_ = nb;
       red_pairs_ = balloc<u64>(be, (size_t)nnz * recw);
       red_sorted_ = balloc<u64>(be, (size_t)nnz * recw);
+      red_sorted_words_ = (int64_t)nnz * recw;
       red_hist_ = balloc<u32>(be, (size_t)nb * groups);
       red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
       red_count_ = balloc<u32>(be, groups);
@@ -244,6 +245,7 @@ void Engine::set_reduction(FwdArgs& fa) const {
   fa.red_nsub = red_nsub_;
   fa.red_pairs = red_pairs_;
   fa.red_sorted = red_sorted_;
+  fa.red_sorted_words = red_sorted_words_;
   fa.red_hist = red_hist_;
   fa.red_tot = red_tot_;
   fa.red_count = red_count_;

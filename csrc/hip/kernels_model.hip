@@ -1034,7 +1034,15 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
 // keys over more rows (A/B: 128 rows per workgroup -21 %, 256 -> 512 below)
 constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128); }
 
-template <int D, int BLOCK>
+// kSeg (the scatter-free form, launch_fmstd_reduction): a pre-pass counts the
+// workgroup's occurrences per bucket -- an upper bound of its records there --
+// and the flush writes each record into its bucket's sub-range of the
+// workgroup region (LDS cursor), so the region leaves the kernel already
+// partitioned by bucket; the sub-range starts go to red_sorted (as u32
+// [bucket][workgroup]) and k_red_sum_vec<D, true> reads a bucket's records
+// straight from the producers' regions -- no k_red_scatter pass over the
+// (48-byte) records.
+template <int D, int BLOCK, bool kSeg = false>
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int NV = 1 + D;
@@ -1045,6 +1053,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   __shared__ long long s_acc[1][kSlots * NV];
   __shared__ unsigned short s_list[1][BLOCK];
   __shared__ u32 s_hist[kRedMaxBuckets];
+  __shared__ u32 s_off[kSeg ? kRedMaxBuckets : 1];
   __shared__ u32 s_nlist[3];
   __shared__ int s_wmax[BLOCK / kWave];
   const BatchView& b = a.batch;
@@ -1081,6 +1090,39 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 #pragma unroll
     for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
   }
+  const u32 S = (u32)a.S;
+  const u32 sl = active ? (u32)slice_of(b, r, a.S) : 0u;
+  if constexpr (kSeg) {
+    // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (s_off)
+    for (int j = 0; j < len; ++j) {
+      const u32 pj = pos[rs.at(j)];
+      if (pj != a.trash_pos) atomicAdd(&s_hist[(pj * S + sl) >> shift], 1u);
+    }
+    __syncthreads();
+    constexpr int kPer = kRedMaxBuckets / BLOCK;
+    const int nb = geom.active(shift, a.red_nb);
+    u32 c[kPer], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int i = (int)threadIdx.x * kPer + q;
+      c[q] = i < nb ? s_hist[i] : 0u;
+      sum += c[q];
+    }
+    u32 tot;
+    u32 ex = block_exclusive_scan<BLOCK>(sum, &tot);
+    u32* sub_out = reinterpret_cast<u32*>(a.red_sorted);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int i = (int)threadIdx.x * kPer + q;
+      if (i < nb) {
+        s_off[i] = ex;
+        sub_out[(size_t)i * gridDim.x + blockIdx.x] = ex;
+        s_hist[i] = 0u;  // now the record cursor
+      }
+      ex += c[q];
+    }
+    __syncthreads();
+  }
   StatAcc st;
   float loss = 0.0f;
   float vs[D];
@@ -1115,8 +1157,6 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     if (a.pctr) a.pctr[r] = p;
     st.add(p, lab);
   }
-  const u32 sl = active ? (u32)slice_of(b, r, a.S) : 0u;
-  const u32 S = (u32)a.S;
   const int lane = lane_id();
   u32 written = 0, bad = 0;
   for (int j = 0; j < maxlen; ++j) {
@@ -1147,22 +1187,13 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
         }
         h = (h + 1) & (kSlots - 1);
       }
-      float w[PS];
-      {
-        const float4* src = wp4 + (size_t)pj * (PS / 4);
-#pragma unroll
-        for (int q = 0; q < PS / 4; ++q) {
-          const float4 v4 = src[q];
-          w[4 * q] = v4.x;
-          w[4 * q + 1] = v4.y;
-          w[4 * q + 2] = v4.z;
-          w[4 * q + 3] = v4.w;
-        }
-      }
+      // factorised: Σ loss*(vs_k - v_k) = C_k - v_k*B with B = Σ loss and
+      // C_k = Σ loss*vs_k (v_k is the key's pulled value, one per step), so the
+      // column walk needs no second gather of the pulled row; k_red_sum_vec
+      // expands C - v*B once per dest
       vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
 #pragma unroll
-      for (int k = 0; k < D; ++k)
-        vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(loss * (vs[k] - w[1 + k]), bad));
+      for (int k = 0; k < D; ++k) vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(loss * vs[k], bad));
     }
     if (has) {
       long long* acc = &s_acc[t][h * NV];
@@ -1197,8 +1228,13 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 #pragma unroll
       for (int q = 0; q < W / 4; ++q)
         rec.q[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
-      region[written + i] = rec;
-      atomicAdd(&s_hist[d >> shift], 1u);
+      if constexpr (kSeg) {
+        const u32 bk = d >> shift;
+        region[s_off[bk] + atomicAdd(&s_hist[bk], 1u)] = rec;
+      } else {
+        region[written + i] = rec;
+        atomicAdd(&s_hist[d >> shift], 1u);
+      }
     }
     written += n;
     lds_barrier();  // (one table: flushed before the next column inserts)
@@ -1215,13 +1251,29 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 // (1+D) int64 accumulators per dest in LDS; every dest a record reached gets
 // its whole gradient row (pad components 0) -- the rows are the step's
 // (slot, slice) gradients the apply reads.
-template <int D>
+// kSeg: no scatter pass -- bucket bk's records are the producers' sub-ranges
+// (k_fm_std_red<.., true>): segment g holds hist[bk][g+1] - hist[bk][g]
+// records (hist: k_red_scan's exclusive prefix over the workgroups, tot[bk]
+// the total) at region(g) + subs[bk][g]; record i of the bucket is found by a
+// binary search of the LDS-staged prefix.
+constexpr int kSegMaxGroups = 2048;
+struct SegSrc {
+  const u32* hist;   // [nb][groups] exclusive prefix (k_red_scan)
+  const u32* tot;    // [nb]
+  const u32* subs;   // [nb][groups] sub-range start in the workgroup region
+  BatchView b;
+  int rows_per_group, groups;
+};
+
+template <int D, bool kSeg = false>
 __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restrict__ sorted,
                                                            const u32* __restrict__ start,
                                                            float* __restrict__ grad,
                                                            RedGeom geom, int nb,
                                                            float* __restrict__ out,
-                                                           const u32* __restrict__ inv) {
+                                                           const u32* __restrict__ inv,
+                                                           const float* __restrict__ wpull,
+                                                           int S, SegSrc sg) {
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
@@ -1231,20 +1283,50 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   using Rec = typename VecRedRec<NV>::T;
   __shared__ long long acc[kR * NV];
   __shared__ u32 seen[kR / 32];
+  __shared__ u32 s_pre[kSeg ? kSegMaxGroups : 1];
+  __shared__ u32 s_seg[kSeg ? kSegMaxGroups : 1];
   const Rec* src = static_cast<const Rec*>(sorted);
   const int shift = geom.shift(kShift);
   const u32 act = (u32)geom.active(shift, nb);
   const u32 units = act << (shift - kShift);
   for (u32 id = blockIdx.x; id < units; id += gridDim.x) {
     const u32 bk = id % act, sub = id / act;
-    const u32 beg = start[bk], end = start[bk + 1];
+    u32 beg, end;
+    if constexpr (kSeg) {
+      beg = 0;
+      end = sg.tot[bk];
+    } else {
+      beg = start[bk];
+      end = start[bk + 1];
+    }
     if (beg == end) continue;  // (block-uniform)
     const u64 lo = ((u64)bk << shift) + ((u64)sub << kShift);
     for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
     for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) seen[i] = 0u;
+    if constexpr (kSeg) {
+      // segment g: records [s_pre[g], s_pre[g+1]) of the bucket, at s_seg[g] + i
+      const size_t row0 = (size_t)bk * sg.groups;
+      for (int g = threadIdx.x; g < sg.groups; g += kRedBlock) {
+        const int64_t r0 = (int64_t)g * sg.rows_per_group;
+        const u32 base = (u32)(sg.b.row_ptr ? sg.b.row_ptr[r0] : r0 * sg.b.nnz_per_row);
+        const u32 p = sg.hist[row0 + g];
+        s_pre[g] = p;
+        s_seg[g] = base + sg.subs[row0 + g] - p;
+      }
+    }
     lds_barrier();
     for (u32 i = beg + threadIdx.x; i < end; i += kRedBlock) {
-      const Rec r = src[i];
+      u32 ri = i;
+      if constexpr (kSeg) {
+        int l0 = 0, l1 = sg.groups;  // first g with s_pre[g] > i
+        while (l0 < l1) {
+          const int m = (l0 + l1) >> 1;
+          if (s_pre[m] <= i) l0 = m + 1;
+          else l1 = m;
+        }
+        ri = s_seg[l0 - 1] + i;
+      }
+      const Rec r = src[ri];
       const u64 l = (u64)r.q[0].x - lo;
       if (l >= kR) continue;  // (another sub-unit's dest)
       u32 wv[W];
@@ -1265,9 +1347,22 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
     lds_barrier();
     for (u32 l = threadIdx.x; l < kR; l += kRedBlock) {
       if (!((seen[l >> 5] >> (l & 31)) & 1u)) continue;
+      // (B, C_0..C_{D-1}) -> g_w = B, g_v[k] = C_k - v_k*B (k_fm_std_red)
+      const double B = fx_to_double<kFx>(acc[l * NV]);
+      const float4* v4 = reinterpret_cast<const float4*>(wpull + ((lo + l) / (u64)S) * PS);
       float o[PS];
 #pragma unroll
-      for (int c = 0; c < PS; ++c) o[c] = c < NV ? (float)fx_to_double<kFx>(acc[l * NV + c]) : 0.0f;
+      for (int q = 0; q < PS / 4; ++q) {
+        const float4 v = v4[q];
+        o[4 * q] = v.x;
+        o[4 * q + 1] = v.y;
+        o[4 * q + 2] = v.z;
+        o[4 * q + 3] = v.w;
+      }
+      o[0] = (float)B;
+#pragma unroll
+      for (int c = 1; c < PS; ++c)
+        o[c] = c < NV ? (float)(fx_to_double<kFx>(acc[l * NV + c]) - (double)o[c] * B) : 0.0f;
       float* row = grad + (lo + l) * PS;
       if (out) {  // one slice: the unique-order row (FwdArgs::red_out)
         const u32 u = inv[lo + l];
@@ -1282,13 +1377,37 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   }
 }
 
+// XFLOW_FMSTD_SCATTER=1 keeps standard-math FM on the k_red_scatter form (A/B)
+static bool fmstd_scatter_forced() {
+  static const bool forced = std::getenv("XFLOW_FMSTD_SCATTER") != nullptr;
+  return forced;
+}
+
 template <int D>
 static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
   constexpr int BLOCK = fmstd_block(D);
   constexpr int NV = 1 + D;
   const int groups = (int)((a.batch.rows + BLOCK - 1) / BLOCK);
-  hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
   const RedGeom geom = red_geom(a);
+  const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
+  if (a.red_out && (a.S != 1 || !a.red_inv))
+    throw std::runtime_error("standard FM red_out: one slice and the slot -> unique map");
+  // scatter-free form: the sub-range starts ([nb][groups] u32) live in red_sorted
+  const bool seg = !fmstd_scatter_forced() && groups <= kSegMaxGroups &&
+                   (int64_t)a.red_nb * groups <= 2 * a.red_sorted_words &&
+                   a.red_sorted_words * 8 / (vec_rec_words(NV) * 4) < (1ll << 32);
+  if (seg) {
+    hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true>), dim3(groups), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
+                       a.red_tot, geom, red_shift(NV));
+    const SegSrc sg{a.red_hist, a.red_tot, reinterpret_cast<const u32*>(a.red_sorted), a.batch,
+                    BLOCK, groups};
+    hipLaunchKernelGGL((k_red_sum_vec<D, true>), dim3(grid), dim3(kRedBlock), 0, st,
+                       static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
+                       a.red_out, a.red_inv, a.wpull, a.S, sg);
+    return;
+  }
+  hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
   hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
                      a.red_tot, geom, red_shift(NV));
   u32* start = a.red_tot + a.red_nb + 1;
@@ -1296,12 +1415,9 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                      a.batch, BLOCK, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
                      geom);
-  const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
-  if (a.red_out && (a.S != 1 || !a.red_inv))
-    throw std::runtime_error("standard FM red_out: one slice and the slot -> unique map");
   hipLaunchKernelGGL(k_red_sum_vec<D>, dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
-                     a.red_out, a.red_inv);
+                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{});
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's

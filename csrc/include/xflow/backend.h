@@ -137,6 +137,7 @@ struct FwdArgs {
   u32* red_tot = nullptr;          // [red_nb + 1] pairs per bucket, then bucket starts
   u32* red_count = nullptr;        // [workgroups] pairs per workgroup
   int red_nb = 0;                  // buckets allocated (<= kRedMaxBuckets)
+  int64_t red_sorted_words = 0;    // u64 words of red_sorted
   // This step's bucket width is decided on the device: dests = slot*S + s lie
   // below red_bcap[0]*S (the scratch capacity the batch was deduplicated
   // with, adaptive), and the shift is the smallest >= red_shift(NV) giving at

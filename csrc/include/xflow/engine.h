@@ -256,6 +256,7 @@ class Engine {
   // HIP LR gradient reduction workspace (FwdArgs::red_*), null when unused
   u64* red_pairs_ = nullptr;
   u64* red_sorted_ = nullptr;
+  int64_t red_sorted_words_ = 0;  // u64 words of red_sorted_
   u32* red_hist_ = nullptr;
   u32* red_tot_ = nullptr;
   u32* red_count_ = nullptr;
