@@ -1265,7 +1265,9 @@ struct SegSrc {
   int rows_per_group, groups;
 };
 
-template <int D, bool kSeg = false>
+// G: segment-table capacity (groups); 512 keeps the rank-8 form at 76 KB of
+// LDS, two workgroups per CU (the per-unit phases are latency chains)
+template <int D, bool kSeg = false, int G = kSegMaxGroups>
 __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restrict__ sorted,
                                                            const u32* __restrict__ start,
                                                            float* __restrict__ grad,
@@ -1283,8 +1285,8 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   using Rec = typename VecRedRec<NV>::T;
   __shared__ long long acc[kR * NV];
   __shared__ u32 seen[kR / 32];
-  __shared__ u32 s_pre[kSeg ? kSegMaxGroups : 1];
-  __shared__ u32 s_seg[kSeg ? kSegMaxGroups : 1];
+  __shared__ u32 s_pre[kSeg ? G : 1];
+  __shared__ u32 s_seg[kSeg ? G : 1];
   const Rec* src = static_cast<const Rec*>(sorted);
   const int shift = geom.shift(kShift);
   const u32 act = (u32)geom.active(shift, nb);
@@ -1383,6 +1385,12 @@ static bool fmstd_scatter_forced() {
   return forced;
 }
 
+// XFLOW_FMSTD_ONE_WG=1: the scatter-free sum at one workgroup per CU (A/B)
+static bool fmstd_one_wg_forced() {
+  static const bool forced = std::getenv("XFLOW_FMSTD_ONE_WG") != nullptr;
+  return forced;
+}
+
 template <int D>
 static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
   constexpr int BLOCK = fmstd_block(D);
@@ -1402,9 +1410,16 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                        a.red_tot, geom, red_shift(NV));
     const SegSrc sg{a.red_hist, a.red_tot, reinterpret_cast<const u32*>(a.red_sorted), a.batch,
                     BLOCK, groups};
-    hipLaunchKernelGGL((k_red_sum_vec<D, true>), dim3(grid), dim3(kRedBlock), 0, st,
-                       static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                       a.red_out, a.red_inv, a.wpull, a.S, sg);
+    if (groups <= 512 && !fmstd_one_wg_forced()) {
+      const u32 grid2 = std::min<u32>((u32)(a.red_nb * a.red_nsub), 2u * (u32)device_cus());
+      hipLaunchKernelGGL((k_red_sum_vec<D, true, 512>), dim3(grid2), dim3(kRedBlock), 0, st,
+                         static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
+                         a.red_out, a.red_inv, a.wpull, a.S, sg);
+    } else {
+      hipLaunchKernelGGL((k_red_sum_vec<D, true>), dim3(grid), dim3(kRedBlock), 0, st,
+                         static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
+                         a.red_out, a.red_inv, a.wpull, a.S, sg);
+    }
     return;
   }
   hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
