@@ -148,7 +148,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       red_hist_ = balloc<u32>(be, (size_t)nb * groups);
       red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
       red_count_ = balloc<u32>(be, groups);
-      if (mvm) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
+      // MVM: T = loss*M per row; standard FM: (loss, loss*vs) per row (k_fm_std_fwd)
+      if (mvm || fm_std) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
     }
   }
   // reference-math FM with the GPU reduction: compact (w, Σv, Σv^2, 0) value rows

@@ -1042,7 +1042,11 @@ constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128);
 // [bucket][workgroup]) and k_red_sum_vec<D, true> reads a bucket's records
 // straight from the producers' regions -- no k_red_scatter pass over the
 // (48-byte) records.
-template <int D, int BLOCK, bool kSeg = false>
+// kSplit: the forward ran in k_fm_std_fwd (its own high-occupancy launch: this
+// kernel's LDS tables leave a CU two waves per SIMD for the row gathers), which
+// left (loss, loss*vs_k) per row in red_rowv -- the same floats the fused form
+// computes here, so both forms sum identical fixed-point values.
+template <int D, int BLOCK, bool kSeg = false, bool kSplit = false>
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int NV = 1 + D;
@@ -1125,10 +1129,24 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   }
   StatAcc st;
   float loss = 0.0f;
-  float vs[D];
+  float vs[D];  // (kSplit: loss*vs_k)
 #pragma unroll
   for (int k = 0; k < D; ++k) vs[k] = 0.0f;
-  if (active) {
+  if (kSplit && active) {
+    const float4* rv = reinterpret_cast<const float4*>(a.red_rowv + (size_t)r * PS);
+    float t[PS];
+#pragma unroll
+    for (int q = 0; q < PS / 4; ++q) {
+      const float4 v4 = rv[q];
+      t[4 * q] = v4.x;
+      t[4 * q + 1] = v4.y;
+      t[4 * q + 2] = v4.z;
+      t[4 * q + 3] = v4.w;
+    }
+    loss = t[0];
+#pragma unroll
+    for (int k = 0; k < D; ++k) vs[k] = t[1 + k];
+  } else if (active) {
     float wx = 0.0f, vp = 0.0f;
     for (int j = 0; j < len; ++j) {
       const float4* src = wp4 + (size_t)pos[rs.at(j)] * (PS / 4);
@@ -1193,7 +1211,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       // expands C - v*B once per dest
       vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
 #pragma unroll
-      for (int k = 0; k < D; ++k) vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(loss * vs[k], bad));
+      for (int k = 0; k < D; ++k)
+        vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(kSplit ? vs[k] : loss * vs[k], bad));
     }
     if (has) {
       long long* acc = &s_acc[t][h * NV];
@@ -1385,6 +1404,66 @@ static bool fmstd_scatter_forced() {
   return forced;
 }
 
+// Standard-math FM forward of the split form (k_fm_std_red<.., kSplit>): one
+// lane per row, the same sums in the same order as the fused kernel; writes
+// (loss, loss*vs_0 .. loss*vs_{D-1}, pad) per row to red_rowv.
+template <int D>
+__global__ void __launch_bounds__(kBlock) k_fm_std_fwd(FwdArgs a) {
+  constexpr int PS = fm_ps(D);
+  const BatchView& b = a.batch;
+  const u32* __restrict__ pos = a.pos;
+  const float4* __restrict__ wp4 = reinterpret_cast<const float4*>(a.wpull);
+  const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  StatAcc st;
+  if (r < b.rows) {
+    const RowSpan rs = row_span(b, r);
+    float vs[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) vs[k] = 0.0f;
+    float wx = 0.0f, vp = 0.0f;
+    for (int j = 0; j < rs.len; ++j) {
+      const float4* src = wp4 + (size_t)pos[rs.at(j)] * (PS / 4);
+      float w[PS];
+#pragma unroll
+      for (int q = 0; q < PS / 4; ++q) {
+        const float4 v4 = src[q];
+        w[4 * q] = v4.x;
+        w[4 * q + 1] = v4.y;
+        w[4 * q + 2] = v4.z;
+        w[4 * q + 3] = v4.w;
+      }
+      wx += w[0];
+#pragma unroll
+      for (int k = 0; k < D; ++k) {
+        vs[k] += w[1 + k];
+        vp += w[1 + k] * w[1 + k];
+      }
+    }
+    float sq = 0.0f;
+#pragma unroll
+    for (int k = 0; k < D; ++k) sq += vs[k] * vs[k];
+    const float p = sigmoid_ref(wx + 0.5f * (sq - vp));
+    const float lab = b.labels[r];
+    const float loss = p - lab;
+    if (a.pctr) a.pctr[r] = p;
+    st.add(p, lab);
+    float o[PS];
+    o[0] = loss;
+#pragma unroll
+    for (int c = 1; c < PS; ++c) o[c] = c <= D ? loss * vs[c - 1] : 0.0f;
+    float4* t4 = reinterpret_cast<float4*>(a.red_rowv + (size_t)r * PS);
+#pragma unroll
+    for (int q = 0; q < PS / 4; ++q) t4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  }
+  flush_stats<kBlock>(st, a.stats, a.fx_bad);
+}
+
+// XFLOW_FMSTD_FUSED=1 keeps the forward inside k_fm_std_red (A/B)
+static bool fmstd_fused_forced() {
+  static const bool forced = std::getenv("XFLOW_FMSTD_FUSED") != nullptr;
+  return forced;
+}
+
 // XFLOW_FMSTD_ONE_WG=1: the scatter-free sum at one workgroup per CU (A/B)
 static bool fmstd_one_wg_forced() {
   static const bool forced = std::getenv("XFLOW_FMSTD_ONE_WG") != nullptr;
@@ -1404,8 +1483,13 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
   const bool seg = !fmstd_scatter_forced() && groups <= kSegMaxGroups &&
                    (int64_t)a.red_nb * groups <= 2 * a.red_sorted_words &&
                    a.red_sorted_words * 8 / (vec_rec_words(NV) * 4) < (1ll << 32);
+  const bool split = a.red_rowv && !fmstd_fused_forced();
+  if (split)
+    hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, a);
   if (seg) {
-    hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true>), dim3(groups), dim3(BLOCK), 0, st, a);
+    if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true>), dim3(groups), dim3(BLOCK), 0, st, a);
+    else hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true>), dim3(groups), dim3(BLOCK), 0, st, a);
     hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
                        a.red_tot, geom, red_shift(NV));
     const SegSrc sg{a.red_hist, a.red_tot, reinterpret_cast<const u32*>(a.red_sorted), a.batch,
@@ -1422,7 +1506,8 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
     }
     return;
   }
-  hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
+  if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, false, true>), dim3(groups), dim3(BLOCK), 0, st, a);
+  else hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
   hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
                      a.red_tot, geom, red_shift(NV));
   u32* start = a.red_tot + a.red_nb + 1;
