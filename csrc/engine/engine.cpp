@@ -44,8 +44,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     throw std::invalid_argument("grow_load must be in (0, 1)");
   if (cfg_.monitor_lag < 0 || cfg_.monitor_lag >= kSnaps)
     throw std::invalid_argument("monitor_lag must be in [0, 63]");
-  if (cfg_.max_slices < 1 || cfg_.max_slices > 32)
-    throw std::invalid_argument("max_slices must be in [1, 32]");
+  if (cfg_.max_slices < 1) throw std::invalid_argument("max_slices must be >= 1");
+  // buffers hold one slice group (more slices per step run group by group)
+  slice_cap_ = cfg_.max_slices < kSliceGroup ? cfg_.max_slices : kSliceGroup;
   if (cfg_.model.kind != kLR && (cfg_.model.v_dim < 1 || cfg_.model.v_dim > 32))
     throw std::invalid_argument("v_dim must be in [1, 32]");
   be_ = cfg_.device >= 0 ? make_hip_backend(cfg_.device) : make_cpu_backend();
@@ -110,8 +111,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // slot-indexed buffers carry one extra row: the trash slot (index cap) that
   // a dedup probe overflow sends its occurrences to (flagged, never applied)
   const uint64_t rows1 = scratch_.cap + 1;
-  grad_ = balloc<float>(be, rows1 * cfg_.max_slices * ps);
-  be.memset(grad_, 0, sizeof(float) * rows1 * cfg_.max_slices * ps);
+  grad_ = balloc<float>(be, rows1 * slice_cap_ * ps);
+  be.memset(grad_, 0, sizeof(float) * rows1 * slice_cap_ * ps);
   tmask_ = balloc<u32>(be, rows1);
   be.memset(tmask_, 0, sizeof(u32) * rows1);
   // atomic-free gradient reduction (FwdArgs::red_*): LR (1 value per key) and
@@ -133,7 +134,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     // sums a wide bucket with red_nsub workgroups -- only when the adaptive
     // scratch has grown that far (bench shape: S = 8 at 2^23 active slots
     // stays at 4096 buckets of 2^14).
-    const uint64_t dests = scratch_.cap * (uint64_t)cfg_.max_slices;
+    const uint64_t dests = scratch_.cap * (uint64_t)slice_cap_;
     int nb = (int)((dests + (1ull << shift) - 1) >> shift);
     int nsub = 1;
     while ((uint64_t)nb > (uint64_t)kRedMaxBuckets * nsub) nsub <<= 1;
@@ -160,7 +161,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   stats_ = balloc<LossStats>(be, 2);
   be.memset(stats_, 0, 2 * sizeof(LossStats));
   bucket_ws_ = balloc<int64_t>(be, 512);
-  slice_rows_ = balloc<int32_t>(be, 32);
+  slice_rows_cap_ = kSliceGroup;
+  slice_rows_ = balloc<int32_t>(be, slice_rows_cap_);
 
   st_keys_ = balloc<u64>(be, nnz);
   st_fgid_ = balloc<int32_t>(be, nnz);
@@ -179,7 +181,7 @@ Engine::~Engine() {
                   host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_, row_grad_,
-                  lr_mask_};
+                  lr_mask_, fm_w_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
   for (SrvBuf& b : srv_) {
@@ -231,11 +233,12 @@ void Engine::use_worker_set(int wb) {
 }
 
 // The GPU reduction path sees every (key, slice) that occurs (a record per
-// column-table entry), so it can write the slice bits: LR and reference FM.
+// column-table entry, or per occurrence), so it can write the slice bits:
+// every model on its bucket-reduction path.
 bool Engine::reduction_masks() const {
-  return red_pairs_ && (double)scratch_.cap * cfg_.max_slices * pstride() < 4294967295.0 &&
-         (cfg_.model.kind == kLR ||
-          (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference));
+  if (!red_pairs_ || (double)scratch_.cap * slice_cap_ * pstride() >= 4294967295.0) return false;
+  return cfg_.model.kind == kLR || cfg_.model.kind == kFM ||
+         (cfg_.model.kind == kMVM && red_rowv_ != nullptr);
 }
 
 void Engine::set_reduction(FwdArgs& fa) const {
@@ -262,19 +265,55 @@ int Engine::slices_of(const BatchView& b) const {
 const int32_t* Engine::slice_rows_dev(const BatchView& b, int S) {
   if (b.rows == cached_rows_ && b.slice_rows == cached_slice_rows_ && S == cached_S_)
     return slice_rows_;
-  int32_t h[32];
-  for (int s = 0; s < S; ++s) {
-    int64_t sr = b.slice_rows > 0 ? b.slice_rows : b.rows;
-    int64_t rem = b.rows - (int64_t)s * sr;
-    rem = rem < 0 ? 0 : rem;
-    // an empty slice has no gradient rows; 1 keeps 0/rows finite
-    h[s] = (int32_t)(rem < sr ? (rem > 0 ? rem : 1) : sr);
+  const int ng = slice_groups(S);
+  if ((int64_t)ng * kSliceGroup > slice_rows_cap_) {
+    be_->synchronize();  // (the old normalisers may still be read)
+    be_->free(slice_rows_);
+    slice_rows_cap_ = (int64_t)ng * kSliceGroup;
+    slice_rows_ = balloc<int32_t>(*be_, slice_rows_cap_);
   }
-  be_->upload_small(slice_rows_, h, sizeof(int32_t) * S);  // (no host wait)
+  const int64_t sr = b.slice_rows > 0 ? b.slice_rows : b.rows;
+  for (int g = 0; g < ng; ++g) {
+    int32_t h[kSliceGroup];
+    const int n = ng == 1 ? S : kSliceGroup;
+    for (int l = 0; l < n; ++l) {
+      const int64_t s = (int64_t)g * kSliceGroup + l;
+      int64_t rem = s < S ? b.rows - s * sr : 0;
+      rem = rem < 0 ? 0 : rem;
+      // an empty slice has no gradient rows; 1 keeps 0/rows finite
+      h[l] = (int32_t)(rem < sr ? (rem > 0 ? rem : 1) : sr);
+    }
+    // (no host wait)
+    be_->upload_small(slice_rows_ + (int64_t)g * kSliceGroup, h, sizeof(int32_t) * n);
+  }
   cached_S_ = S;
   cached_rows_ = b.rows;
   cached_slice_rows_ = b.slice_rows;
   return slice_rows_;
+}
+
+BatchView Engine::group_view(const BatchView& b, int S, int k, const u32*& pos) const {
+  if (slice_groups(S) == 1) return b;
+  const int64_t sr = b.slice_rows > 0 ? b.slice_rows : b.rows;
+  int64_t r0 = (int64_t)k * kSliceGroup * sr;
+  r0 = r0 < b.rows ? r0 : b.rows;
+  int64_t n = (int64_t)kSliceGroup * sr;
+  n = n < b.rows - r0 ? n : b.rows - r0;
+  BatchView g = b;
+  g.rows = n;
+  if (b.row_ptr) {  // CSR: occurrence indices stay absolute
+    g.row_ptr = b.row_ptr + r0;
+    g.labels = b.labels + r0;
+    return g;  // (g.nnz: the whole batch's, an upper bound; no kernel reads it)
+  }
+  // fixed width: row-major (r, j) at r*npr + j, field-major at j*col_stride + r
+  const int64_t off = b.col_stride > 0 ? r0 : r0 * b.nnz_per_row;
+  g.keys = b.keys + off;
+  if (b.fgid) g.fgid = b.fgid + off;
+  g.labels = b.labels + r0;
+  g.nnz = n * b.nnz_per_row;
+  pos += off;
+  return g;
 }
 
 void Engine::ensure_inv() {
@@ -325,20 +364,19 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
   be_->dedup(b.keys, b.nnz, scratch_, o);
 }
 
-// XFLOW_LR_SLOT_GRADS=1: LR-FTRL fused step with slot-indexed gradients and
-// a table re-read in the apply (the pre-stash path; A/B and fallback tests)
-static bool lr16_disabled() {
-  static const bool off = std::getenv("XFLOW_LR_SLOT_GRADS") != nullptr;
-  return off;
-}
 
 void Engine::train_step(const BatchView& b) {
   stale_stashes();  // the table changes: server stashes are stale
   use_worker_set(0);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  const int ng = slice_groups(S);
+  if (ng > 1 && cfg_.sum_slices)
+    throw std::invalid_argument("sum_slices: at most 32 slices per step (ordered pushes: any count)");
+  // (slice groups always run the masked multi-slice paths: every group has >= 2 slices)
+  const int Sf = ng > 1 ? kSliceGroup : S;
   const int ps = pstride();
-  const bool masks = S > 1 && !cfg_.sum_slices;
+  const bool masks = Sf > 1 && !cfg_.sum_slices;
   const int32_t* srows = slice_rows_dev(b, S);
   // LR-FTRL on 16-byte slots, bucket reduction: the reduction writes
   // normalised gradients in unique order (through the compaction's slot ->
@@ -348,39 +386,48 @@ void Engine::train_step(const BatchView& b) {
   const TableLayout& L = table_.L;
   const bool lr16_layout_ok = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 &&
                               L.P == 1 && L.opt == kFTRL && !L.has_flag && red_pairs_ &&
-                              (double)scratch_.cap < 4294967295.0 && !lr16_disabled();
-  const bool lr16 = lr16_layout_ok && (S == 1 || (masks && reduction_masks()));
+                              (double)scratch_.cap < 4294967295.0;
+  const bool lr16 = lr16_layout_ok && (Sf == 1 || (masks && reduction_masks()));
   // summed slices: slot-indexed sums (packed apply), still the (n, z) stash
-  const bool lr16s = lr16_layout_ok && S > 1 && !lr16;
+  const bool lr16s = lr16_layout_ok && Sf > 1 && !lr16;
   if (lr16s && !lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
+  // several slices on the reduction path: unique-order [unique][slice]
+  // gradients plus the slice bits the reduction writes (uq_mask_); the pull
+  // clears the bits, the apply reads only the present slices
+  const bool uqm = masks && reduction_masks();
   if (lr16) {
     ensure_inv();
-    if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * cfg_.max_slices);
+    if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * slice_cap_);
     if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
-    if (S > 1 && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
   }
-  // reference FM, one slice: the (B, C) sums land in unique order (dense apply read)
-  const bool fmu = fm_vals_ && S == 1;
+  // reference FM: the (B, C) sums land in unique order (dense apply read)
+  const bool fmu = fm_vals_ && (Sf == 1 || uqm);
   if (fmu) {
     ensure_inv();
-    if (!fm_grad_) fm_grad_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
+    if (!fm_grad_) fm_grad_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * slice_cap_);
   }
-  // MVM and standard-math FM, one slice, on their reduction paths: the
-  // per-key gradient rows land in unique order too (a dense apply read
-  // instead of slot-indexed rows the apply had to zero after reading;
-  // XFLOW_SLOT_GRAD_ROWS=1 restores those)
-  static const bool slot_rows = std::getenv("XFLOW_SLOT_GRAD_ROWS") != nullptr;
-  const bool rows_ok = be_->is_gpu() && S == 1 && red_pairs_ && !slot_rows &&
-                       (double)scratch_.cap * ps < 4294967295.0;
-  const bool mvmu = rows_ok && cfg_.model.kind == kMVM && red_rowv_ &&
-                    std::getenv("XFLOW_MVM_ATOMICS") == nullptr;
-  const bool fsu = rows_ok && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard &&
-                   std::getenv("XFLOW_FMSTD_ATOMICS") == nullptr;
+  // compact reference-FM rows of a grouped step: the (B, C) of later groups
+  // expand with the PULLED weights, not the table's (updated by the earlier
+  // groups), so the pull keeps the per-parameter weights
+  const bool fm_keep_w = fm_vals_ && ng > 1;
+  if (fm_keep_w && !fm_w_) fm_w_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps);
+  // MVM (one slice) and standard-math FM (any slices) on their reduction
+  // paths: the per-key gradient rows land in unique order too (a dense apply
+  // read instead of slot-indexed rows the apply had to zero after reading)
+  const bool rows_ok = be_->is_gpu() && red_pairs_ &&
+                       (double)scratch_.cap * ps * slice_cap_ < 4294967295.0;
+  const bool mvmu = rows_ok && Sf == 1 && cfg_.model.kind == kMVM && red_rowv_;
+  const bool fsu = rows_ok && (Sf == 1 || uqm) && cfg_.model.kind == kFM &&
+                   cfg_.model.fm_math == kFmStandard;
   const bool rowu = mvmu || fsu;
   if (rowu) {
     ensure_inv();
-    if (!row_grad_) row_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps);
+    const int rs = fsu ? slice_cap_ : 1;
+    if (!row_grad_) row_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps * rs);
   }
+  // the unique-order outputs of a multi-slice step and their slice bits
+  const bool uq = Sf > 1 && (lr16 || fmu || fsu);
+  if (uq && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
   dedup_(b, 1, nullptr, lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)
   guard_inserts(b.nnz);  // (<= nnz new keys; may grow the table first)
@@ -397,10 +444,10 @@ void Engine::train_step(const BatchView& b) {
   pa.out_map = uniq_pos_;
   pa.pstride = ps;
   pa.fm_vals = fm_vals_;
+  if (fm_keep_w) pa.out_w = fm_w_;
   if (lr16) {
     pa.out_nz = lr_nz_;
-    // S > 1: only a key's present slices are read, so only its bits need clearing
-    pa.zero_out = S == 1 ? lr_grad_ : reinterpret_cast<float*>(lr_mask_);
+    pa.zero_out = lr_grad_;
   }
   if (lr16s) pa.out_nz = lr_nz_;
   if (fmu) {
@@ -411,86 +458,106 @@ void Engine::train_step(const BatchView& b) {
     pa.zero_out = row_grad_;
     pa.zero_width = ps;
   }
+  if (uq) {  // S > 1: only a key's present slices are read, so only its bits need clearing
+    pa.zero_out = reinterpret_cast<float*>(lr_mask_);
+    pa.zero_width = 1;
+  }
   be_->table_pull(pa);
 
-  FwdArgs fa;
-  fa.batch = b;
-  fa.pos = pos_;
-  fa.wpull = wpull_;
-  fa.grad = grad_;
-  fa.stats = stats_;
-  fa.model = cfg_.model;
-  fa.S = S;
-  fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
-  fa.fx_bad = overflow_;
-  set_reduction(fa);
-  // slice bits from the reduction (LR / reference FM), else per occurrence
-  if (masks && lr16) fa.red_masks = lr_mask_;
-  else if (masks && reduction_masks()) fa.red_masks = tmask_;
-  else if (masks) be_->slice_masks(b, pos_, tmask_);
-  // reference-math FM on the GPU reduction path: (B, C) rows, expanded by the apply
-  fa.fm_compact = fa.red_pairs && fa.agg_ok && cfg_.model.kind == kFM &&
-                  cfg_.model.fm_math == kFmReference;
-  fa.fm_vals = fm_vals_;
-  if (fm_vals_ && !fa.fm_compact) throw std::logic_error("train_step: compact FM rows need the reduction");
-  if (lr16) {
-    fa.red_out = lr_grad_;
-    fa.red_inv = inv_;
-    fa.red_rows = srows;
-  }
-  if (fmu) {
-    fa.red_out = fm_grad_;
-    fa.red_inv = inv_;
-  }
-  if (rowu) {
-    fa.red_out = row_grad_;
-    fa.red_inv = inv_;
-  }
-  be_->forward_backward(fa);
+  for (int k = 0; k < ng; ++k) {
+    const u32* posk = pos_;
+    const BatchView bk = group_view(b, S, k, posk);
+    const int Sg = group_slices(S, k);
+    const int32_t* srk = srows + (int64_t)k * kSliceGroup;
+    // a later group's unique-order slice bits start from zero again (the
+    // pull cleared them for the first); its apply reads the table, which
+    // the earlier groups updated, instead of the pull's (n, z) stash
+    if (k > 0 && uq) be_->memset(lr_mask_, 0, sizeof(u32) * (size_t)b.nnz);
+    const bool stash = k == 0;
 
-  ApplyArgs aa;
-  aa.table = table_;
-  aa.opt = cfg_.opt;
-  aa.keys = uniq_keys_;
-  aa.slots = uniq_slot_;
-  aa.n_dev = n_uniq_;
-  aa.n_max = b.nnz;
-  aa.grads = grad_;
-  aa.grad_map = uniq_pos_;
-  aa.masks = masks ? tmask_ : nullptr;
-  aa.masks_rw = masks ? tmask_ : nullptr;
-  aa.zero_after = true;
-  aa.S = S;
-  aa.pstride = ps;
-  aa.P = cfg_.model.P();
-  aa.sum_slices = cfg_.sum_slices;
-  aa.slice_rows = srows;
-  aa.fm_compact = fa.fm_compact;
-  aa.fm_D = cfg_.model.v_dim;
-  if (lr16) {  // unique-order, already normalised, zeroed by the next pull
-    aa.grads = lr_grad_;
-    aa.grad_map = nullptr;
-    aa.zero_after = false;
-    aa.slice_rows = nullptr;
-    aa.nz_stash = lr_nz_;
-    aa.masks = S > 1 ? lr_mask_ : nullptr;
-    aa.masks_rw = nullptr;
+    FwdArgs fa;
+    fa.batch = bk;
+    fa.pos = posk;
+    fa.wpull = wpull_;
+    fa.grad = grad_;
+    fa.stats = stats_;
+    fa.model = cfg_.model;
+    fa.S = Sg;
+    fa.agg_ok = (double)scratch_.cap * Sg * ps < 4294967295.0;
+    fa.fx_bad = overflow_;
+    set_reduction(fa);
+    // slice bits from the reduction (unique order with the outputs, else
+    // slot-indexed), else per occurrence
+    if (uq) fa.red_masks = lr_mask_;
+    else if (uqm) fa.red_masks = tmask_;
+    else if (masks) be_->slice_masks(bk, posk, tmask_);
+    // reference-math FM on the GPU reduction path: (B, C) rows, expanded by the apply
+    fa.fm_compact = fa.red_pairs && fa.agg_ok && cfg_.model.kind == kFM &&
+                    cfg_.model.fm_math == kFmReference;
+    fa.fm_vals = fm_vals_;
+    if (fm_vals_ && !fa.fm_compact) throw std::logic_error("train_step: compact FM rows need the reduction");
+    if (lr16) {
+      fa.red_out = lr_grad_;
+      fa.red_inv = inv_;
+      fa.red_rows = srk;
+    }
+    if (fmu) {
+      fa.red_out = fm_grad_;
+      fa.red_inv = inv_;
+    }
+    if (rowu) {
+      fa.red_out = row_grad_;
+      fa.red_inv = inv_;
+    }
+    be_->forward_backward(fa);
+
+    ApplyArgs aa;
+    aa.table = table_;
+    aa.opt = cfg_.opt;
+    aa.keys = uniq_keys_;
+    aa.slots = uniq_slot_;
+    aa.n_dev = n_uniq_;
+    aa.n_max = b.nnz;
+    aa.grads = grad_;
+    aa.grad_map = uniq_pos_;
+    aa.masks = masks ? tmask_ : nullptr;
+    aa.masks_rw = masks ? tmask_ : nullptr;
+    aa.zero_after = true;
+    aa.S = Sg;
+    aa.pstride = ps;
+    aa.P = cfg_.model.P();
+    aa.sum_slices = cfg_.sum_slices;
+    aa.slice_rows = srk;
+    aa.fm_compact = fa.fm_compact;
+    aa.fm_D = cfg_.model.v_dim;
+    if (fm_keep_w) aa.pulled = fm_w_;
+    if (lr16) {  // unique-order, already normalised, zeroed by the next pull
+      aa.grads = lr_grad_;
+      aa.grad_map = nullptr;
+      aa.zero_after = false;
+      aa.slice_rows = nullptr;
+      aa.nz_stash = stash ? lr_nz_ : nullptr;
+    }
+    if (lr16s) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
+    if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
+      aa.grads = fm_grad_;
+      aa.grad_map = nullptr;
+      aa.zero_after = false;
+      aa.gstride = 2;
+    }
+    if (rowu) {  // unique-order rows, zeroed by the next pull
+      aa.grads = row_grad_;
+      aa.grad_map = nullptr;
+      aa.zero_after = false;
+      aa.gstride = ps;
+    }
+    if (uq) {  // present slices by the unique-order bits (cleared by the next pull)
+      aa.masks = lr_mask_;
+      aa.masks_rw = nullptr;
+    }
+    attach_snapshot(aa);
+    be_->table_apply(aa);
   }
-  if (lr16s) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
-  if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
-    aa.grads = fm_grad_;
-    aa.grad_map = nullptr;
-    aa.zero_after = false;
-    aa.gstride = 2;
-  }
-  if (rowu) {  // unique-order rows, zeroed by the next pull
-    aa.grads = row_grad_;
-    aa.grad_map = nullptr;
-    aa.zero_after = false;
-    aa.gstride = ps;
-  }
-  attach_snapshot(aa);
-  be_->table_apply(aa);
   end_step();
 }
 
@@ -618,8 +685,8 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
                        int wb, int64_t seq) {
   if (world <= 1) seq = -1;  // (no exchange to check)
   use_worker_set(wb);
-  const int S = slices_of(b);
-  if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  if (slices_of(b) > cfg_.max_slices)
+    throw std::invalid_argument("batch has more slices than max_slices");
   if (b.nnz == 0) {
     // nothing to send; a batch without rows (a rank out of data) sends -1
     // counts, which tell the receivers "no data from this source" (the loop
@@ -658,7 +725,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
   ba.seq = seq;
   be_->bucket(ba);
   send_map_ = send_pos_;
-  (void)S;  // slice masks are built in w_forward_backward with the step's global S
+  // (slice masks are built in w_forward_backward with the step's global S)
 }
 
 void Engine::ensure_server_capacity(int64_t n, int buf) {
@@ -676,8 +743,7 @@ void Engine::ensure_server_capacity(int64_t n, int buf) {
 
 bool Engine::lr16_layout() const {
   const TableLayout& L = table_.L;
-  return be_->is_gpu() && L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag &&
-         !lr16_disabled();
+  return be_->is_gpu() && L.stride == 4 && L.P == 1 && L.opt == kFTRL && !L.has_flag;
 }
 
 void Engine::w_forward(const BatchView& b, const float* pulled, int64_t n_send, float* pctr,
@@ -754,10 +820,9 @@ void Engine::s_pull(const u64* recv_keys, int64_t n, float* out_vals, bool inser
 // 4x the step's entries, so the load stays below 0.75.
 bool Engine::group_entries(const u64* recv_keys, int64_t n, int buf,
                            const std::vector<int64_t>& offs) {
-  // (EngineConfig::owner_group: grouping is opt-in; XFLOW_OWNER_GROUP=1 too, for A/Bs)
-  static const bool env_group = std::getenv("XFLOW_OWNER_GROUP") != nullptr;
+  // (EngineConfig::owner_group: grouping is opt-in)
   const int nsrc = (int)offs.size() - 1;
-  if (cfg_.owner_group != 1 && !env_group) return false;
+  if (cfg_.owner_group != 1) return false;
   if (!be_->owner_grouping() || nsrc < 2 || nsrc > kMaxGroupSources) return false;
   if (offs.front() != 0 || offs.back() != n) throw std::invalid_argument("s_pull: source offsets");
   int active = 0;
@@ -821,26 +886,37 @@ bool Engine::group_entries(const u64* recv_keys, int64_t n, int buf,
 }
 
 void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
-                                float* grads_out, u32* masks_out, int S_global, int wb) {
+                                float* grads_out, u32* masks_out, int S_global, int wb,
+                                int group) {
   use_worker_set(wb);
   // All ranks of a step must agree on the gradient row width (S*pstride):
   // S_global (>= this batch's slices) lets a rank with a short or empty batch
   // emit the same layout; its extra slices carry no rows and no mask bits.
-  const int S = S_global > 0 ? S_global : slices_of(b);
-  if (S < slices_of(b) || S > cfg_.max_slices)
+  const int St = S_global > 0 ? S_global : slices_of(b);
+  if (St < slices_of(b) || St > cfg_.max_slices)
     throw std::invalid_argument("w_forward_backward: S_global out of range");
+  const int ng = slice_groups(St);
+  if (group < 0 || group >= ng) throw std::invalid_argument("w_forward_backward: slice group");
+  if (ng > 1 && cfg_.sum_slices)
+    throw std::invalid_argument("sum_slices: at most 32 slices per step (ordered pushes: any count)");
+  // slice group `group` of the step: its rows, its slices (>= 2 when grouped)
+  const u32* posk = pos_;
+  const BatchView bk = group_view(b, St, group, posk);
+  const int S = group_slices(St, group);
   const int ps = pstride();
   const bool masks = S > 1 && !cfg_.sum_slices;
-  const int32_t* srows = slice_rows_dev(b, S);
+  const int32_t* srows = slice_rows_dev(b, St) + (int64_t)group * kSliceGroup;
   const bool direct = inv_valid_ && red_pairs_ && S == 1 &&
                       (cfg_.model.kind == kLR || fm_vals_) &&
                       (double)scratch_.cap * S * ps < 4294967295.0;
-  // the direct path's send buffer is zeroed by the scatter
-  be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, vstride_,
-                    direct ? grads_out : nullptr, grad_width());
+  // the direct path's send buffer is zeroed by the scatter; the pulled rows
+  // are placed once per step (every group reads the same ones)
+  if (group == 0)
+    be_->scatter_rows(pulled, wpull_, send_map_, nullptr, n_send, vstride_,
+                      direct ? grads_out : nullptr, grad_width());
   FwdArgs fa;
-  fa.batch = b;
-  fa.pos = pos_;
+  fa.batch = bk;
+  fa.pos = posk;
   fa.wpull = wpull_;
   fa.grad = grad_;
   fa.stats = stats_;
@@ -850,7 +926,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.fx_bad = overflow_;
   set_reduction(fa);
   if (masks && reduction_masks()) fa.red_masks = tmask_;
-  else if (masks) be_->slice_masks(b, pos_, tmask_);
+  else if (masks) be_->slice_masks(bk, posk, tmask_);
   fa.fm_compact = sharded_fm_compact() && fa.agg_ok;
   fa.fm_vals = fm_vals_;
   if (sharded_fm_compact() && !fa.fm_compact)
@@ -910,10 +986,10 @@ void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* r
   base.sum_slices = cfg_.sum_slices;
   base.slice_rows = nullptr;
   const SrcGroups& g = sb.grp;
-  if (g.oidx && (int)src_offsets.size() == g.nsrc + 1) {
-    bool same = true;
-    for (int s = 0; s <= g.nsrc; ++s) same = same && src_offsets[s] == g.offs[s];
-    if (!same) throw std::invalid_argument("s_apply: source offsets differ from the pull's");
+  bool same = g.oidx && (int)src_offsets.size() == g.nsrc + 1;
+  for (int s = 0; same && s <= g.nsrc; ++s) same = src_offsets[s] == g.offs[s];
+  // (other offsets, e.g. one source at a time for a grouped-slice step: per source below)
+  if (same) {
     const int64_t n = g.offs[g.nsrc];
     if (n > sb.n) throw std::invalid_argument("s_apply: offsets beyond pull");
     ApplyArgs aa = base;

@@ -78,10 +78,14 @@ EvalResult eval_result(const EvalMetrics& m) {
 }
 
 Trainer::Trainer(const TrainerConfig& cfg) : cfg_(cfg) {
-  threads_ = cfg_.threads > 0 ? cfg_.threads : (int)std::thread::hardware_concurrency();
+  // the reference's slice count is std::thread::hardware_concurrency()
+  // (lr_worker.h:40-41); XFLOW_HARDWARE_CONCURRENCY stands in for it (tests
+  // of many-core hosts on a small one)
+  const char* hc = std::getenv("XFLOW_HARDWARE_CONCURRENCY");
+  const int hw = hc && std::atoi(hc) > 0 ? std::atoi(hc) : (int)std::thread::hardware_concurrency();
+  threads_ = cfg_.threads > 0 ? cfg_.threads : hw;
   if (threads_ < 1) threads_ = 1;
-  if (!cfg_.serial_slices && threads_ > 32)
-    throw std::invalid_argument("concurrent slices: at most 32 slices per block (use serial)");
+  // (any count: more than Engine::kSliceGroup slices run group by group)
   if (cfg_.test_block_bytes <= 0) cfg_.test_block_bytes = cfg_.model == kLR ? (4 << 20) : (2 << 20);
   EngineConfig ec;
   ec.model = cfg_.model_spec;

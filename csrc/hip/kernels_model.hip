@@ -694,6 +694,28 @@ __device__ __forceinline__ u32 slot_bits(const u32* pbits, u64 slot, u64 S, u64 
   return bits;
 }
 
+// Slice bits of every slot whose dests slot*S + s meet the unit [lo, lo + kR),
+// from the unit's presence bitmap (bit l: dest lo + l has records): one plain
+// store per slot inside the unit, an atomic OR for a slot straddling its edge
+// (S not dividing kR; the masks start zeroed).  masks are indexed by slot, or
+// by the slot's unique index (inv != null: unique-order outputs).
+template <u32 kR>
+__device__ __forceinline__ void unit_masks(const u32* pbits, u64 lo, u64 S, u32* __restrict__ masks,
+                                           const u32* __restrict__ inv) {
+  const u64 s0 = lo / S, s1 = (lo + kR + S - 1) / S;
+  for (u64 slot = s0 + threadIdx.x; slot < s1; slot += blockDim.x) {
+    const u32 bits = slot_bits<kR>(pbits, slot, S, lo);
+    if (!bits) continue;
+    u64 m = slot;
+    if (inv) {
+      m = inv[slot];
+      if (m == 0xFFFFFFFFu) continue;  // (the trash slot)
+    }
+    if (slot * S >= lo && slot * S + S <= lo + kR) masks[m] = bits;
+    else atomicOr(&masks[m], bits);
+  }
+}
+
 // A bucket's sums are either initialised and written densely (all kR dests)
 // or per record: with the 4x-headroom dedup scratch and S slices, a bucket's
 // dests are mostly untouched (S = 8 at bench shape: ~1500 records over 16384
@@ -812,13 +834,17 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
         f.grad[dest] = (float)fx_to_double<kFx>(a);
       }
     } else {
-      if (acc[2 * l] == 0 && acc[2 * l + 1] == 0) return;
+      // (a present slice of the S > 1 unique-order output is written even
+      // when zero: the apply reads it by its slice bit)
+      if (acc[2 * l] == 0 && acc[2 * l + 1] == 0 && !(present && f.out && S > 1)) return;
       const float B = (float)fx_to_double<kFx>(acc[2 * l]);
       const float C = (float)fx_to_double<kFx>(acc[2 * l + 1]);
       if (f.compact) {  // expanded by the apply (k_apply_group)
-        if (f.out) {    // one slice: unique (send) order
-          const u32 o = f.inv[dest];
-          if (o == 0xFFFFFFFFu) return;
+        if (f.out) {    // unique (send) order; S > 1: [unique][slice]
+          const u64 slot = dest / S, sl = dest - slot * S;
+          const u32 o0 = f.inv[slot];
+          if (o0 == 0xFFFFFFFFu) return;
+          const u64 o = (u64)o0 * S + sl;
           if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
             const double rows = (double)f.rows[0];
             reinterpret_cast<float2*>(f.out)[o] =
@@ -920,8 +946,12 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
                      rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
                      red_geom(a));
-  if (a.red_out && (NV == 2 ? (a.S != 1 || !a.fm_compact) : (a.S != 1 && !a.red_masks)))
-    throw std::runtime_error("red_out: one slice or slice bits (LR), compact rows (FM)");
+  if (a.red_out && (NV == 2 ? !a.fm_compact : false))
+    throw std::runtime_error("red_out: compact rows (reference FM)");
+  if (a.red_out && a.S != 1 && !a.red_masks)
+    throw std::runtime_error("red_out with several slices needs the slice bits (red_masks)");
+  if (a.red_out && a.red_rows && NV == 2 && a.S != 1)
+    throw std::runtime_error("red_out: normalised compact FM rows are one-slice (send buffer)");
   RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim, a.red_out, a.red_inv,
              a.red_rows, NV == 2 && a.fm_compact, a.S > 1 ? a.red_masks : nullptr};
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
@@ -1294,7 +1324,8 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
                                                            float* __restrict__ out,
                                                            const u32* __restrict__ inv,
                                                            const float* __restrict__ wpull,
-                                                           int S, SegSrc sg) {
+                                                           int S, SegSrc sg,
+                                                           u32* __restrict__ masks) {
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
@@ -1385,24 +1416,24 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
       for (int c = 1; c < PS; ++c)
         o[c] = c < NV ? (float)(fx_to_double<kFx>(acc[l * NV + c]) - (double)o[c] * B) : 0.0f;
       float* row = grad + (lo + l) * PS;
-      if (out) {  // one slice: the unique-order row (FwdArgs::red_out)
-        const u32 u = inv[lo + l];
+      if (out) {  // the unique-order row (FwdArgs::red_out); S > 1: [unique][slice]
+        const u64 slot = (lo + l) / (u64)S;
+        const u32 u = inv[slot];
         if (u == 0xFFFFFFFFu) continue;
-        row = out + (u64)u * PS;
+        row = out + ((u64)u * (u64)S + (lo + l - slot * (u64)S)) * PS;
       }
       float4* g4 = reinterpret_cast<float4*>(row);
 #pragma unroll
       for (int q = 0; q < PS / 4; ++q) g4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
     }
+    // S > 1: each slot's slice bits from the records' presence (every
+    // occurrence leaves a record, so a slice that touched the key is present
+    // even with a zero gradient -- it still pushes, like the reference's slice)
+    if (masks) unit_masks<kR>(seen, lo, (u64)S, masks, out ? inv : nullptr);
     lds_barrier();  // (the next unit reinitialises what this one read)
   }
 }
 
-// XFLOW_FMSTD_SCATTER=1 keeps standard-math FM on the k_red_scatter form (A/B)
-static bool fmstd_scatter_forced() {
-  static const bool forced = std::getenv("XFLOW_FMSTD_SCATTER") != nullptr;
-  return forced;
-}
 
 // Standard-math FM forward of the split form (k_fm_std_red<.., kSplit>): one
 // lane per row, the same sums in the same order as the fused kernel; writes
@@ -1458,17 +1489,7 @@ __global__ void __launch_bounds__(kBlock) k_fm_std_fwd(FwdArgs a) {
   flush_stats<kBlock>(st, a.stats, a.fx_bad);
 }
 
-// XFLOW_FMSTD_FUSED=1 keeps the forward inside k_fm_std_red (A/B)
-static bool fmstd_fused_forced() {
-  static const bool forced = std::getenv("XFLOW_FMSTD_FUSED") != nullptr;
-  return forced;
-}
 
-// XFLOW_FMSTD_ONE_WG=1: the scatter-free sum at one workgroup per CU (A/B)
-static bool fmstd_one_wg_forced() {
-  static const bool forced = std::getenv("XFLOW_FMSTD_ONE_WG") != nullptr;
-  return forced;
-}
 
 template <int D>
 static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
@@ -1477,13 +1498,14 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
   const int groups = (int)((a.batch.rows + BLOCK - 1) / BLOCK);
   const RedGeom geom = red_geom(a);
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
-  if (a.red_out && (a.S != 1 || !a.red_inv))
-    throw std::runtime_error("standard FM red_out: one slice and the slot -> unique map");
+  if (a.red_out && (!a.red_inv || (a.S != 1 && !a.red_masks)))
+    throw std::runtime_error("standard FM red_out: the slot -> unique map (S > 1: and slice bits)");
+  u32* masks = a.S > 1 ? a.red_masks : nullptr;
   // scatter-free form: the sub-range starts ([nb][groups] u32) live in red_sorted
-  const bool seg = !fmstd_scatter_forced() && groups <= kSegMaxGroups &&
+  const bool seg = groups <= kSegMaxGroups &&
                    (int64_t)a.red_nb * groups <= 2 * a.red_sorted_words &&
                    a.red_sorted_words * 8 / (vec_rec_words(NV) * 4) < (1ll << 32);
-  const bool split = a.red_rowv && !fmstd_fused_forced();
+  const bool split = a.red_rowv != nullptr;
   if (split)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a);
@@ -1494,15 +1516,15 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                        a.red_tot, geom, red_shift(NV));
     const SegSrc sg{a.red_hist, a.red_tot, reinterpret_cast<const u32*>(a.red_sorted), a.batch,
                     BLOCK, groups};
-    if (groups <= 512 && !fmstd_one_wg_forced()) {
+    if (groups <= 512) {
       const u32 grid2 = std::min<u32>((u32)(a.red_nb * a.red_nsub), 2u * (u32)device_cus());
       hipLaunchKernelGGL((k_red_sum_vec<D, true, 512>), dim3(grid2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                         a.red_out, a.red_inv, a.wpull, a.S, sg);
+                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks);
     } else {
       hipLaunchKernelGGL((k_red_sum_vec<D, true>), dim3(grid), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                         a.red_out, a.red_inv, a.wpull, a.S, sg);
+                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks);
     }
     return;
   }
@@ -1517,7 +1539,7 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                      geom);
   hipLaunchKernelGGL(k_red_sum_vec<D>, dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
-                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{});
+                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks);
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
@@ -1697,19 +1719,14 @@ __global__ void __launch_bounds__(256) k_fm_fwd_mfma(FwdArgs a) {
 }
 
 // XFLOW_FMSTD_ATOMICS=1 keeps standard-math FM on the column-table + global
-// float atomic backward (A/B)
-static bool fmstd_atomics_forced() {
-  static const bool forced = std::getenv("XFLOW_FMSTD_ATOMICS") != nullptr;
-  return forced;
-}
-
 template <bool kGrad>
 static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.model.fm_math == kFmReference && a.red_pairs && a.red_nb > 0 &&
                    a.red_nb <= kRedMaxBuckets;
   if (a.fm_compact && !red) throw std::runtime_error("fm_compact needs the FM reduction path");
-  if (a.red_masks && a.S > 1 && !red) throw std::runtime_error("red_masks need the FM reduction path");
+  if (a.red_masks && a.S > 1 && a.model.fm_math == kFmReference && !red)
+    throw std::runtime_error("red_masks need the FM reduction path");
   if (!kGrad && a.model.fm_math == kFmStandard && a.model.fm_mfma) {
     const int g = (int)((a.batch.rows + 63) / 64);  // 4 waves x 16 rows
     switch (a.model.v_dim) {
@@ -1736,7 +1753,9 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   }
   // standard math: per-component records through the LR reduction pipeline
   const bool red_std = agg && a.model.fm_math == kFmStandard && a.red_pairs && a.red_nb > 0 &&
-                       a.red_nb <= kRedMaxBuckets && !a.red_masks && !fmstd_atomics_forced();
+                       a.red_nb <= kRedMaxBuckets;
+  if (a.red_masks && a.S > 1 && a.model.fm_math == kFmStandard && !red_std)
+    throw std::runtime_error("red_masks need the standard-FM reduction path");
   if (a.red_out && a.model.fm_math == kFmStandard && !red_std)
     throw std::runtime_error("standard FM red_out needs the vector-record reduction");
   switch (a.model.v_dim) {
@@ -1929,14 +1948,20 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
       // factorises as T_k/(1+v_k) with T = loss*M per row -- one 8-byte
       // record (dest, row) per occurrence, summed per key by k_mvm_red_sum.
       // Rows with a repeated field (S = field sum): global atomics.
+      // S > 1 with slice bits from the reduction: a record for EVERY
+      // occurrence (T = 0 where the product vanished, and for repeated-field
+      // rows, whose gradients go by atomics), so that the bits show every
+      // slice that touched a key -- such a slice pushes, even a zero gradient
+      const bool all = a.red_masks != nullptr && S > 1u;
       bool emit = false;
-      if (active && !dup && loss != 0.0f) {
+      if (active && (all || (!dup && loss != 0.0f))) {
         float* t = a.red_rowv + (size_t)r * PS;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-          t[k] = loss * M[k];
+          t[k] = dup ? 0.0f : loss * M[k];
           emit |= M[k] != 0.0f;
         }
+        emit |= all;
       }
       if (active && dup) {
         for (int j = 0; j < len; ++j) {
@@ -2029,14 +2054,9 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
 // grad (the duplicate-field rows' atomics may already be there).
 constexpr int mvm_nsub(int D) { return D <= 16 ? 16 : 32; }
 
-// XFLOW_MVM_ATOMICS=1 keeps the LDS-column + global-atomic backward (A/B)
-static bool mvm_atomics_forced() {
-  static const bool forced = std::getenv("XFLOW_MVM_ATOMICS") != nullptr;
-  return forced;
-}
-
 struct MvmRedFinal {
   float* grad;
+  u32* masks;        // S > 1: slice bits of each slot (FwdArgs::red_masks), or null
   float* out;        // one slice: unique-order rows out[inv[dest]] (FwdArgs::red_out), or null
   const u32* inv;
   const float* wpull;
@@ -2055,6 +2075,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
   constexpr int kSubShift = kRedShift - ilog2c(NSUB);
   constexpr u32 kSub = 1u << kSubShift;
   __shared__ float acc[kSub * D];
+  __shared__ u32 pbits[kSub / 32];  // (f.masks) dests some record reached
   const u32 q = blockIdx.x >> 3;
   const u32 sub = q % (u32)f.nsubt;
   const int bucket = (int)((q / (u32)f.nsubt) * 8 + (blockIdx.x & 7));
@@ -2066,6 +2087,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
   const u32 beg = start[bucket], end = start[bucket + 1];
   if (beg == end) return;
   for (u32 i = threadIdx.x; i < kSub * D; i += kRedBlock) acc[i] = 0.0f;
+  for (u32 i = threadIdx.x; i < kSub / 32; i += kRedBlock) pbits[i] = 0u;
   __syncthreads();
   const int lane = lane_id();
   // block-uniform trip count: every lane takes part in the wave-level combine
@@ -2080,6 +2102,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
     for (int u = 0; u < kRedUnroll; ++u) {
       const u32 d = (u32)pr[u];
       bool pending = pr[u] != ~0ull && (u64)d - lo < (u64)kSub;
+      if (f.masks && pending) atomicOr(&pbits[(d - (u32)lo) >> 5], 1u << ((d - (u32)lo) & 31));
       float t[PS];
       if (pending) load_row<PS>(f.rowv, (u32)(pr[u] >> 32), t);
       // Power-law keys: a hot key's records arrive many to a wave and would
@@ -2132,6 +2155,10 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
       if (wk != 0.0f) g[k] += (float)((double)v / (1.0 + (double)wk));
     }
   }
+  if (f.masks) {
+    __syncthreads();
+    unit_masks<kSub>(pbits, lo, (u64)f.S, f.masks, f.out ? f.inv : nullptr);
+  }
 }
 
 template <int D>
@@ -2147,7 +2174,8 @@ static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
   const int grid = ((a.red_nb + 7) / 8) * 8 * nsubt;
   if (a.red_out && (a.S != 1 || !a.red_inv))
     throw std::runtime_error("MVM red_out: one slice and the slot -> unique map");
-  MvmRedFinal f{a.grad, a.red_out, a.red_inv, a.wpull, a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
+  MvmRedFinal f{a.grad, a.S > 1 ? a.red_masks : nullptr, a.red_out, a.red_inv, a.wpull,
+                a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
   hipLaunchKernelGGL(k_mvm_red_sum<D>, dim3(grid), dim3(kRedBlock), 0, st,
                      reinterpret_cast<const u64*>(a.red_sorted), static_cast<const u32*>(start), f);
 }
@@ -2156,7 +2184,8 @@ template <bool kGrad>
 static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.red_pairs && a.red_rowv && a.red_nb > 0 &&
-                   a.red_nb <= kRedMaxBuckets && !mvm_atomics_forced();
+                   a.red_nb <= kRedMaxBuckets;
+  if (a.red_masks && a.S > 1 && !red) throw std::runtime_error("red_masks need the MVM reduction path");
   switch (a.model.v_dim) {
 #define XF_MVM_CASE(DD)                                                                  \
   case DD: {                                                                             \

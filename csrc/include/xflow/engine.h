@@ -25,7 +25,9 @@ struct EngineConfig {
   int table_log2_cap = 20;     // slots = 2^table_log2_cap (<= 2^31)
   int64_t max_rows = 1 << 16;  // per step
   int64_t max_nnz = 1 << 22;   // per step
-  int max_slices = 1;          // slices per step (<= 32)
+  // slices per step (any count: a step of more than kSliceGroup slices runs
+  // its slices in groups of kSliceGroup over one dedup + pull, see train_step)
+  int max_slices = 1;
   bool sum_slices = false;     // apply Σ_s g_s once instead of ordered per-slice pushes
   double scratch_factor = 2.5;  // dedup scratch capacity = pow2 >= factor * max_nnz
   int device = -1;             // -1 => CPU backend, else HIP device ordinal
@@ -113,8 +115,12 @@ class Engine {
   // worker: place pulled rows (in send order) into the pos-indexed buffer,
   // run forward/backward, then emit normalised gradients in send order.
   // grads_out: [n_send][S*pstride]; masks_out: [n_send] (used when S>1).
+  // S_global > kSliceGroup: slice group `group` only (its rows, group_slices
+  // slices: grads_out [n_send][group_slices*width]); every group reads the
+  // same pulled rows, and the groups' pushes are applied in group order.
   void w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
-                          float* grads_out, u32* masks_out, int S_global = 0, int wb = 0);
+                          float* grads_out, u32* masks_out, int S_global = 0, int wb = 0,
+                          int group = 0);
   // server: apply received gradients source by source (deterministic order).
   // src_offsets has world+1 entries delimiting each source's rows.
   void s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
@@ -157,6 +163,21 @@ class Engine {
   // by the owner with the values it served)
   int grad_width() const { return sharded_fm_compact() ? 2 : pstride(); }
   int slices_of(const BatchView& b) const;
+  // Hogwild slices beyond kSliceGroup per step (the reference's default is
+  // hardware_concurrency threads per block, lr_worker.h:40-41): the step's
+  // slices run in groups of kSliceGroup -- one dedup + pull for the whole
+  // step (every slice reads the same weights), then per group a
+  // forward/backward over the group's rows and an apply of its pushes in
+  // slice order, so the pushes of all S slices are applied in global slice
+  // order: the same semantics as one S-slice step.  A group of one slice
+  // runs as two (masked path; the second slice has no rows).
+  static constexpr int kSliceGroup = 32;
+  static int slice_groups(int S) { return S <= kSliceGroup ? 1 : (S + kSliceGroup - 1) / kSliceGroup; }
+  static int group_slices(int S, int group) {
+    if (S <= kSliceGroup) return S;
+    const int n = S - group * kSliceGroup;
+    return n >= kSliceGroup ? kSliceGroup : (n < 2 ? 2 : n);
+  }
 
   // ---- checkpoint ------------------------------------------------------
   // Host copies of every live slot: keys + (stride-2) state words each.
@@ -221,7 +242,13 @@ class Engine {
   u32 own_epoch_ = 0;
   bool group_entries(const u64* recv_keys, int64_t n, int buf,
                      const std::vector<int64_t>& src_offsets);
+  // per-slice normalisers, kSliceGroup entries per slice group (group k's
+  // local slice s at [k * kSliceGroup + s])
   const int32_t* slice_rows_dev(const BatchView& b, int S);
+  // rows of slice group k of a batch of S slices, and the matching dedup
+  // positions (a row-range view: same layout, offset pointers)
+  BatchView group_view(const BatchView& b, int S, int k, const u32*& pos) const;
+  int slice_cap_ = 1;            // slices per group the buffers are sized for
   // parts > 1: owner-partitioned scratch (ScratchView::parts); uniq_keys_out
   // redirects the unique-key list (the sharded step's send buffer)
   void dedup_(const BatchView& b, int parts = 1, u64* uniq_keys_out = nullptr,
@@ -229,7 +256,7 @@ class Engine {
   const u32* send_map_ = nullptr;  // send order -> scratch slot (send_pos_ or uniq_pos_)
   bool sharded_fm_compact() const {
     return red_pairs_ && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmReference &&
-           (double)scratch_.cap * cfg_.max_slices * pstride() < 4294967295.0;
+           (double)scratch_.cap * slice_cap_ * pstride() < 4294967295.0;
   }
   bool fm_vals_ = false;
   int vstride_ = 1;
@@ -251,7 +278,7 @@ class Engine {
   u32* mon_ = nullptr;          // [4]: table size (u64), overflow_ (below)
   u32* overflow_ = nullptr;     // [2]: scratch, table (= mon_ + 2)
   float* wpull_ = nullptr;      // [scratch_cap * pstride]
-  float* grad_ = nullptr;       // [scratch_cap * max_slices * pstride]
+  float* grad_ = nullptr;       // [scratch_cap * slice_cap * pstride]
   u32* tmask_ = nullptr;        // [scratch_cap]
   // HIP LR gradient reduction workspace (FwdArgs::red_*), null when unused
   u64* red_pairs_ = nullptr;
@@ -261,12 +288,13 @@ class Engine {
   u32* red_tot_ = nullptr;
   u32* red_count_ = nullptr;
   float* red_rowv_ = nullptr;    // MVM: per-row loss*M (FwdArgs::red_rowv)
-  float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz][max_slices]
+  float* lr_grad_ = nullptr;     // LR-FTRL fused step: unique-order gradients [max_nnz][slice_cap]
   float* lr_nz_ = nullptr;       // LR-FTRL fused step: pulled (n, z) [max_nnz][2]
   int64_t nnz_seen_ = 0;          // most occurrences in one batch (ScratchView::grow)
   u32* lr_mask_ = nullptr;       // LR-FTRL fused step, S > 1: unique-order slice bits [max_nnz]
   float* fm_grad_ = nullptr;     // reference FM fused step: unique-order (B, C) [max_nnz][2]
   float* row_grad_ = nullptr;    // MVM / standard FM fused step (one slice): unique-order rows [max_nnz][pstride]
+  float* fm_w_ = nullptr;        // reference FM, grouped step: pulled per-parameter weights [max_nnz][pstride]
   int red_nb_ = 0;
   int red_nsub_ = 1;
   unsigned long long* bcap_ = nullptr;  // current worker set's batch scratch capacity
@@ -278,7 +306,8 @@ class Engine {
   LossStats* stats_ = nullptr;  // [1]
   u32* send_pos_ = nullptr;     // [max_nnz]
   int64_t* bucket_ws_ = nullptr;  // [2*256]
-  int32_t* slice_rows_ = nullptr;  // [32]
+  int32_t* slice_rows_ = nullptr;  // [slice_rows_cap_]
+  int64_t slice_rows_cap_ = 0;
   int64_t cached_rows_ = -1, cached_slice_rows_ = -1;
   int cached_S_ = -1;
   int64_t last_nsend_ = 0;

@@ -278,6 +278,9 @@ PYBIND11_MODULE(_xflow_native, m) {
            [](Engine& e, const BatchView& b, uintptr_t pctr) { e.eval_step(b, P<float>(pctr)); },
            py::call_guard<py::gil_scoped_release>())
       .def("slices_of", &Engine::slices_of)
+      .def_static("slice_groups", &Engine::slice_groups)
+      .def_static("group_slices", &Engine::group_slices)
+      .def_readonly_static("slice_group", &Engine::kSliceGroup)
       .def("push_host",
            [](Engine& e, py::array_t<uint64_t> keys, py::array_t<float> grads) {
              std::vector<u64> k(keys.data(), keys.data() + keys.size());
@@ -337,12 +340,12 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("wb") = 0, py::call_guard<py::gil_scoped_release>())
       .def("w_forward_backward",
            [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, uintptr_t grads,
-              uintptr_t masks, int S, int wb) {
+              uintptr_t masks, int S, int wb, int group) {
              e.w_forward_backward(b, P<const float>(pulled), n_send, P<float>(grads),
-                                  P<u32>(masks), S, wb);
+                                  P<u32>(masks), S, wb, group);
            },
            py::arg("batch"), py::arg("pulled"), py::arg("n_send"), py::arg("grads"),
-           py::arg("masks"), py::arg("S") = 0, py::arg("wb") = 0,
+           py::arg("masks"), py::arg("S") = 0, py::arg("wb") = 0, py::arg("group") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("s_apply",
            [](Engine& e, uintptr_t keys, uintptr_t grads, uintptr_t masks,

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${TAG:-w8ab}
 MODEL=${MODEL:-lr}
-VARIANTS=${VARIANTS:-"base:|grouped:XFLOW_OWNER_GROUP=1"}
+VARIANTS=${VARIANTS:-"base:"}
 IFS='|' read -ra VL <<< "$VARIANTS"
 for rep in ${REPS:-1}; do
 for v in "${VL[@]}"; do

@@ -231,8 +231,8 @@ def test_field_major_synthetic_lr_matches_cpu(gpu_device):
 def test_field_major_synthetic_mvm_matches_cpu(gpu_device, rows):
     """MVM on the bench shape (field-major, 39 fields, one field per column)
     with O(1) latent init, so the field products and gradients are live: the
-    GPU backward (reduction path, or the column-atomic one under
-    XFLOW_MVM_ATOMICS=1) trains the same table as the CPU backend."""
+    GPU backward (the bucket-reduction path) trains the same table as the
+    CPU backend."""
     from xflow_amd.engine import Batch
 
     m = ModelConfig(kind="mvm", v_dim=10)

@@ -51,7 +51,9 @@ def _sharded_worker(rank, world, kind, slices, out_dir, pipelined=False):
 
 @pytest.mark.parametrize("kind,slices,pipelined,world",
                          [("lr", 1, False, 2), ("lr", 2, False, 2), ("fm", 2, False, 2),
-                          ("mvm", 1, False, 2), ("lr", 2, True, 3), ("fm", 1, True, 2)])
+                          ("mvm", 1, False, 2), ("lr", 2, True, 3), ("fm", 1, True, 2),
+                          # > 32 slices per rank: slice groups, (source, slice) order
+                          ("lr", 64, True, 2), ("fm", 64, False, 2), ("mvm", 64, True, 2)])
 def test_sharded_equals_single_rank(tmp_path, kind, slices, pipelined, world):
     run_world(_sharded_worker, world, kind, slices, str(tmp_path), pipelined)
     # single-rank replay: concatenated batches, world*slices ordered slices
@@ -174,16 +176,17 @@ def test_trainer_two_workers_bundled_data(tmp_path):
     assert pred.shape == (200, 3)
 
 
-def _async_worker(rank, world, out_dir, staleness=1):
+def _async_worker(rank, world, out_dir, staleness=1, slices=1):
     from xflow_amd.parallel.async_p2p import AsyncShardedEngine
 
-    eng = _make_engine("lr", 1)
+    eng = _make_engine("lr", slices)
     sh = AsyncShardedEngine(eng, staleness=staleness)
-    bs = [to_batch(*_batches(rank, step), torch.device("cpu")) for step in range(STEPS + 2)]
+    bs = [to_batch(*_batches(rank, step), torch.device("cpu"), slice_rows=ROWS // slices)
+          for step in range(STEPS + 2)]
     for step in range(STEPS + 2):
         # pipelined (next batch prepared inside the step) from the second step on
         nxt = bs[step + 1] if 0 < step < STEPS + 1 else None
-        sh.train_step(bs[step], S=1, next_batch=nxt)
+        sh.train_step(bs[step], S=slices, next_batch=nxt)
     sh.flush()
     keys, _ = eng.export_table()
     np.save(os.path.join(out_dir, f"akeys{rank}.npy"), keys)
@@ -191,17 +194,18 @@ def _async_worker(rank, world, out_dir, staleness=1):
     assert sh.p2p_ops > 0
 
 
-@pytest.mark.parametrize("staleness", [1, 2, 3])
-def test_async_p2p_staleness_one_matches_simulation(tmp_path, staleness):
+@pytest.mark.parametrize("staleness,slices", [(1, 1), (2, 1), (3, 1), (1, 64)])
+def test_async_p2p_staleness_one_matches_simulation(tmp_path, staleness, slices):
     """AsyncShardedEngine == the reference step with pulls that miss exactly
-    the previous k steps' pushes (staleness k), pushes in (source) order."""
+    the previous k steps' pushes (staleness k), pushes in (source, slice)
+    order (64 slices per rank: two slice groups)."""
     from collections import deque
 
     from xflow_amd.testing import torch_ref
     from xflow_amd.testing.hashing import normal_init
 
     world = 2
-    run_world(_async_worker, world, str(tmp_path), staleness)
+    run_world(_async_worker, world, str(tmp_path), staleness, slices)
     ref = torch_ref.RefTable(1, 1, "ftrl", init_fn=lambda k, d: normal_init(k, d) * 1e-2)
     pending = deque()
     for step in range(STEPS + 2):
@@ -209,7 +213,7 @@ def test_async_p2p_staleness_one_matches_simulation(tmp_path, staleness):
         keys = np.concatenate([p[0] for p in parts])
         lab = np.concatenate([p[3] for p in parts])
         rp = np.concatenate([parts[0][1]] + [p[1][1:] + len(parts[0][0]) for p in parts[1:]])
-        _, cur = torch_ref.compute_step(ref, "lr", keys, lab, rp.astype(np.int32), ROWS)
+        _, cur = torch_ref.compute_step(ref, "lr", keys, lab, rp.astype(np.int32), ROWS // slices)
         if len(pending) == staleness:
             torch_ref.apply_step(ref, pending.popleft())
         pending.append(cur)

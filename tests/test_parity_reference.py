@@ -97,3 +97,60 @@ def test_mvm_predict_compat_emits_vdim_rows_per_slice(tmp_path):
                       model=ModelConfig(kind="mvm"), engine=EngineConfig(table_log2_cap=14))
     res = Trainer(cfg, device=torch.device("cpu")).train()
     assert res["n"] == 8 * 10  # v_multi.size() rows per slice (mvm_worker.cc:96)
+
+
+# ---- the reference's default slice count: hardware_concurrency threads ----
+# (lr_worker.h:40-41).  An MI355X host has far more than 32 hardware threads;
+# a block of fewer rows than threads trains (and predicts) nothing
+# (lr_worker.cc:190-199), a larger thread count than 32 runs as slice groups.
+
+@pytest.mark.parametrize("threads,epochs", [(64, 10), (40, 4)])
+def test_many_concurrent_slices_match_oracle(tmp_path, threads, epochs):
+    want = run_oracle("lr", "ftrl", epochs, threads=threads, concurrent=True)
+    res, pred = run_trainer(tmp_path, "lr", "ftrl", epochs, threads=threads, serial=False)
+    assert len(want) == pred.shape[0] == (200 // threads) * threads
+    np.testing.assert_allclose(pred[:, 0], [w[1] for w in want], rtol=2e-4, atol=2e-6)
+    ll, _ = oracle.calculate_auc(want)
+    assert abs(res["logloss_printed"] - ll) < 5e-4
+
+
+def test_default_threads_on_a_256_thread_host_python_cli(tmp_path, monkeypatch, capsys):
+    """`xflow_lr <train> <test> 0 10` with no --threads on a 256-thread host:
+    every 200-row block has fewer rows than threads, so -- like the
+    reference -- nothing is trained or predicted, and the run completes."""
+    from xflow_amd import cli
+
+    monkeypatch.setattr(os, "cpu_count", lambda: 256)
+    want = run_oracle("lr", "ftrl", 10, threads=256, concurrent=True)
+    assert want == []
+    rc = cli.main([TRAIN, TEST, "0", "10", "--cpu", "--pred-dir", str(tmp_path),
+                   "--log2-cap", "14"])
+    assert rc in (0, None)
+    out = capsys.readouterr().out
+    assert "logloss: 0\ttp_n = 0" in out and "train end......" in out
+    assert os.path.getsize(os.path.join(str(tmp_path), "pred_0_0.txt")) == 0
+
+
+@pytest.mark.parametrize("hw", [256, 48])
+def test_default_threads_native_cli(tmp_path, hw):
+    """The native xflow_lr binary with its default thread count
+    (hardware_concurrency, here XFLOW_HARDWARE_CONCURRENCY) on the bundled
+    data: 256 threads train nothing; 48 threads = two slice groups per block,
+    predictions equal to the oracle's."""
+    import subprocess
+
+    from xflow_amd import _build
+
+    binp = os.path.join(_build.BUILD, "bin", "xflow_lr")
+    env = dict(os.environ, XFLOW_HARDWARE_CONCURRENCY=str(hw), XFLOW_PRED_DIR=str(tmp_path))
+    r = subprocess.run([binp, TRAIN, TEST, "0", "4", "--device", "-1"], cwd=str(tmp_path),
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    want = run_oracle("lr", "ftrl", 4, threads=hw, concurrent=True)
+    pred = np.loadtxt(os.path.join(str(tmp_path), "pred_0_0.txt"), ndmin=2)
+    if hw == 256:
+        assert want == [] and pred.size == 0
+        assert "tp_n = 0" in r.stdout
+    else:
+        assert pred.shape[0] == len(want) == (200 // hw) * hw
+        np.testing.assert_allclose(pred[:, 0], [w[1] for w in want], rtol=2e-4, atol=2e-6)

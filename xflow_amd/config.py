@@ -130,7 +130,12 @@ class TrainConfig:
     engine: EngineConfig = field(default_factory=EngineConfig)
 
     def resolved_threads(self) -> int:
-        return self.threads if self.threads > 0 else (os.cpu_count() or 1)
+        if self.threads > 0:
+            return self.threads
+        # hardware_concurrency (lr_worker.h:40-41); the native trainer's
+        # XFLOW_HARDWARE_CONCURRENCY override applies here too
+        hc = int(os.environ.get("XFLOW_HARDWARE_CONCURRENCY", "0") or 0)
+        return hc if hc > 0 else (os.cpu_count() or 1)
 
     def resolved_test_block(self) -> int:
         if self.test_block_bytes > 0:

@@ -272,12 +272,14 @@ class Engine:
 
     def w_forward_backward(self, batch: Batch, pulled: torch.Tensor, n_send: int,
                            grads_out: torch.Tensor, masks_out: torch.Tensor | None,
-                           S: int = 0, wb: int = 0) -> None:
+                           S: int = 0, wb: int = 0, group: int = 0) -> None:
+        """S > SLICE_GROUP: slice group ``group`` of the step only (its rows;
+        grads_out holds group_slices(S, group) slices per key)."""
         self._sync_stream()
         self._e.w_forward_backward(batch.view(), pulled.data_ptr(), int(n_send),
                                    grads_out.data_ptr(),
                                    masks_out.data_ptr() if masks_out is not None else 0, int(S),
-                                   int(wb))
+                                   int(wb), int(group))
 
     def s_apply(self, recv_keys: torch.Tensor, recv_grads: torch.Tensor,
                 recv_masks: torch.Tensor | None, offsets, S: int, buf: int = 0) -> None:
@@ -293,6 +295,15 @@ class Engine:
     # ---- stats / checkpoint -------------------------------------------------
     def slices_of(self, batch: Batch) -> int:
         return int(self._e.slices_of(batch.view()))
+
+    @staticmethod
+    def slice_groups(S: int) -> list[int]:
+        """Slices of each slice group of an S-slice step (Engine::slice_groups:
+        more than 32 slices run in groups of 32, each group >= 2 slices)."""
+        from xflow_amd import native
+
+        n = native.load()
+        return [int(n.Engine.group_slices(int(S), g)) for g in range(int(n.Engine.slice_groups(int(S))))]
 
     def read_stats(self, reset: bool = False, which: int = 0) -> dict:
         self._sync_stream()

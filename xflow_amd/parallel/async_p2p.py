@@ -55,10 +55,12 @@ class AsyncShardedEngine(ShardedEngine):
         nbuf = self.staleness + 1  # step t's buffers live until its apply at step t+k
         self._nbuf = nbuf
         self._rk = [_Buf(torch.int64, dev) for _ in range(nbuf)]
-        self._gin = [_Buf(torch.float32, dev) for _ in range(nbuf)]
-        self._gout = [_Buf(torch.float32, dev) for _ in range(nbuf)]
-        self._min = [_Buf(torch.int32, dev) for _ in range(nbuf)]
-        self._mout = [_Buf(torch.int32, dev) for _ in range(nbuf)]
+        # per step buffer: one gradient / mask buffer per slice group
+        # (Engine.slice_groups: more than 32 slices run in groups of 32)
+        self._gin = [[_Buf(torch.float32, dev)] for _ in range(nbuf)]
+        self._gout = [[_Buf(torch.float32, dev)] for _ in range(nbuf)]
+        self._min = [[_Buf(torch.int32, dev)] for _ in range(nbuf)]
+        self._mout = [[_Buf(torch.int32, dev)] for _ in range(nbuf)]
         # compact-FM applies read the values their step's pull served
         self._vals_out = [_Buf(torch.float32, dev) for _ in range(nbuf)]
         self._step_no = 0
@@ -70,21 +72,25 @@ class AsyncShardedEngine(ShardedEngine):
     @staticmethod
     def _push_ops(p) -> list:
         """Exchange ops of a pending step's pushes: gradients (+ slice masks)
-        to their owners, the reverse of the step's key exchange."""
-        ops = [(p["gin"], p["gout"], p["recv_splits"], p["send_splits"])]
-        if p["min"] is not None:
-            ops.append((p["min"], p["mout"], p["recv_splits"], p["send_splits"]))
+        to their owners, the reverse of the step's key exchange (one pair per
+        slice group)."""
+        ops = []
+        for gin, gout, min_, mout, _ in p["groups"]:
+            ops.append((gin, gout, p["recv_splits"], p["send_splits"]))
+            if min_ is not None:
+                ops.append((min_, mout, p["recv_splits"], p["send_splits"]))
         return ops
 
     def _apply(self, p) -> None:
-        self.engine.s_apply(p["rk"], p["gin"], p["min"], p["offsets"], p["S"], buf=p["buf"])
+        self._apply_groups(p["rk"], [(gin, min_, Sg) for gin, _, min_, _, Sg in p["groups"]],
+                           p["offsets"], buf=p["buf"])
 
     def train_step(self, batch: Batch, S: Optional[int] = None, prefetch=None,
                    next_batch: Optional[Batch] = None) -> bool:
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.value_width  # floats per pulled value row
-        W = S * e.grad_width
+        gw = e.grad_width
         ordered_masks = S > 1 and not e.cfg.sum_slices
         wb, send_splits, recv_splits, prefetch, any_data = self._take(batch, prefetch)
         if not any_data:
@@ -121,20 +127,28 @@ class AsyncShardedEngine(ShardedEngine):
         # staleness k: step t-k's pushes land after this step's pull
         if due is not None:
             self._apply(self._pending.popleft())
-        grads_out = self._gout[buf].get(n_send * W).view(n_send, W)
-        masks_out = self._mout[buf].get(n_send) if ordered_masks else None
-        e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S, wb=wb)
-        if alias:  # world 1: the owner reads the pushes in place
-            grads_in, masks_in = grads_out, masks_out
-        else:
-            grads_in = self._gin[buf].get(n_recv * W).view(n_recv, W)
-            masks_in = self._min[buf].get(n_recv) if ordered_masks else None
-        self._pending.append(dict(rk=rk, gin=grads_in, gout=grads_out, min=masks_in,
-                                  mout=masks_out, recv_splits=recv_splits,
-                                  send_splits=send_splits, offsets=offsets, S=S, buf=buf))
+        groups = e.slice_groups(S)
+        for lst in (self._gin[buf], self._gout[buf], self._min[buf], self._mout[buf]):
+            while len(lst) < len(groups):
+                lst.append(_Buf(lst[0].dtype, lst[0].device))
+        pend = []
+        for k, Sg in enumerate(groups):
+            W = Sg * gw
+            om = ordered_masks and Sg > 1
+            grads_out = self._gout[buf][k].get(n_send * W).view(n_send, W)
+            masks_out = self._mout[buf][k].get(n_send) if om else None
+            e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S, wb=wb, group=k)
+            if alias:  # world 1: the owner reads the pushes in place
+                grads_in, masks_in = grads_out, masks_out
+            else:
+                grads_in = self._gin[buf][k].get(n_recv * W).view(n_recv, W)
+                masks_in = self._min[buf][k].get(n_recv) if om else None
+            pend.append((grads_in, grads_out, masks_in, masks_out, Sg))
+        self._pending.append(dict(rk=rk, groups=pend, recv_splits=recv_splits,
+                                  send_splits=send_splits, offsets=offsets, buf=buf))
         self._step_no += 1
         e.w_finish()
-        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)
+        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * S * gw)
         return True
 
     def flush(self) -> None:

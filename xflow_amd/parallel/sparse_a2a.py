@@ -119,10 +119,12 @@ class ShardedEngine:
         # by their step's pull (the async step applies after the next pull)
         self._vals_out = [_Buf(torch.float32, dev), _Buf(torch.float32, dev)]
         self._pulled = _Buf(torch.float32, dev)
-        self._grads_out = _Buf(torch.float32, dev)
-        self._grads_in = _Buf(torch.float32, dev)
-        self._masks_out = _Buf(torch.int32, dev)
-        self._masks_in = _Buf(torch.int32, dev)
+        # one gradient / mask buffer pair per slice group of a step (more
+        # than 32 Hogwild slices run as groups of 32: Engine.slice_groups)
+        self._grads_out = [_Buf(torch.float32, dev)]
+        self._grads_in = [_Buf(torch.float32, dev)]
+        self._masks_out = [_Buf(torch.int32, dev)]
+        self._masks_in = [_Buf(torch.int32, dev)]
         self.last_send = 0
         self.last_recv = 0
         self.bytes_moved = 0
@@ -385,11 +387,16 @@ class ShardedEngine:
             self.empty_steps += 1
             return False
         n_send, n_recv = self.last_send, self.last_recv
-        recv_keys = (ahead["keys"] if ahead is not None
+        # (keys received ahead belong to the announced batch only: another
+        # batch re-exchanges its own)
+        recv_keys = (ahead["keys"] if ahead is not None and ahead["batch"] is batch
                      else self._exchange_keys(wb, send_splits, recv_splits))
         offsets = self._offsets(recv_splits)
         vals = self._vals_out[0].get(n_recv * ps).view(n_recv, ps)
-        e.s_pull(recv_keys, n_recv, vals, insert=True, buf=0, offsets=offsets)
+        # (slice groups apply after each other: compact FM rows then expand
+        # with the kept pulled weights)
+        e.s_pull(recv_keys, n_recv, vals, insert=True, buf=0, offsets=offsets,
+                 keep_weights=len(e.slice_groups(S)) > 1)
         if prefetch is not None:
             prefetch()
         alias = self._self_only()
@@ -405,18 +412,33 @@ class ShardedEngine:
         if next_batch is not None and not self._self_only():
             self._counts_sent(self._prep[1])
 
-        W = S * e.grad_width  # (B, C) per slice for reference-math FM on the GPU
-        grads_out = self._grads_out.get(n_send * W).view(n_send, W)
-        masks_out = self._masks_out.get(n_send) if ordered_masks else None
-        e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S, wb=wb)
-        if alias:
-            grads_in, masks_in = grads_out, masks_out
-        else:
-            grads_in = self._grads_in.get(n_recv * W).view(n_recv, W)
-            masks_in = self._masks_in.get(n_recv) if ordered_masks else None
-            ops = [(grads_in, grads_out, recv_splits, send_splits)]
-            if ordered_masks:  # slice masks in the same group call
+        # one gradient exchange per step; a step of more than 32 slices sends
+        # one (gradients, masks) pair per slice group in that exchange and
+        # the owner applies the groups in order (every group's forward read
+        # the same pulled rows: one S-slice step)
+        gw = e.grad_width  # (B, C) per slice for reference-math FM on the GPU
+        groups = e.slice_groups(S)
+        for lst in (self._grads_out, self._grads_in, self._masks_out, self._masks_in):
+            while len(lst) < len(groups):
+                lst.append(_Buf(lst[0].dtype, lst[0].device))
+        outs, ins, ops = [], [], []
+        for k, Sg in enumerate(groups):
+            W = Sg * gw
+            om = ordered_masks and Sg > 1
+            grads_out = self._grads_out[k].get(n_send * W).view(n_send, W)
+            masks_out = self._masks_out[k].get(n_send) if om else None
+            e.w_forward_backward(batch, pulled, n_send, grads_out, masks_out, S, wb=wb, group=k)
+            outs.append((grads_out, masks_out))
+            if alias:
+                ins.append((grads_out, masks_out))
+                continue
+            grads_in = self._grads_in[k].get(n_recv * W).view(n_recv, W)
+            masks_in = self._masks_in[k].get(n_recv) if om else None
+            ins.append((grads_in, masks_in))
+            ops.append((grads_in, grads_out, recv_splits, send_splits))
+            if om:  # slice masks in the same group call
                 ops.append((masks_in, masks_out, recv_splits, send_splits))
+        if not alias:
             if next_batch is not None and self.early_keys:
                 # the next batch's keys ride in this group call: its split sizes
                 # came with the values exchange above, so the host reads them
@@ -432,10 +454,29 @@ class ShardedEngine:
                 self.early_key_exchanges += 1
                 self.last_send, self.last_recv = n_send, n_recv
             self._a2a_ops(ops)
-        e.s_apply(recv_keys, grads_in, masks_in, offsets, S)
+        self._apply_groups(recv_keys, [(g, m, Sg) for (g, m), Sg in zip(ins, groups)], offsets)
         e.w_finish()
-        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * W)  # W = S * grad_width
+        self.bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * S * gw)
         return True
+
+    def _apply_groups(self, recv_keys, groups, offsets, buf: int = 0) -> None:
+        """Owner apply of one step's pushes: groups = [(grads, masks, slices)]
+        per slice group.  One group: s_apply (sources in order).  Several: the
+        pushes go in (source, slice) order -- source by source, each source's
+        groups in order -- the order of one S-slice step."""
+        e = self.engine
+        if len(groups) == 1:
+            g, m, Sg = groups[0]
+            e.s_apply(recv_keys, g, m, offsets, Sg, buf=buf)
+            return
+        W = len(offsets) - 1
+        for src in range(W):
+            if offsets[src + 1] <= offsets[src]:
+                continue
+            # only this source's range is non-empty
+            offs = [offsets[src]] * (src + 1) + [offsets[src + 1]] * (W - src)
+            for g, m, Sg in groups:
+                e.s_apply(recv_keys, g, m, offs, Sg, buf=buf)
 
     def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Forward-only sharded step (keys looked up, never inserted).  Every

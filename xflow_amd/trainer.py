@@ -71,8 +71,8 @@ class Trainer:
         self.device = device or xdist.device_for_rank()
         self.threads = cfg.resolved_threads()
         self.concurrent = not cfg.serial_slices
-        if self.concurrent and self.threads > 32:
-            raise ValueError("concurrent slices: at most 32 per block; use serial_slices")
+        # any thread count: beyond 32 slices a step runs its slices in groups
+        # of 32 over one pull (Engine.slice_groups), the same semantics
         self.S = self.threads if self.concurrent else 1
         max_block = max(cfg.train_block_bytes, cfg.resolved_test_block())
         ecfg = cfg.engine
