@@ -91,3 +91,31 @@ def test_predictor_gpu_equals_cpu(gpu_device, tmp_path):
     a = Predictor(str(tmp_path / "ck"), device=gpu_device).predict_libffm(_test_text())
     b = Predictor(str(tmp_path / "ck"), device=torch.device("cpu")).predict_libffm(_test_text())
     np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
+
+
+def test_mvm_keys_api_needs_field_ids(tmp_path):
+    """An MVM model multiplies per-field sums: scoring hashed keys without
+    their field ids is refused (HTTP 400), and with them equals the libffm
+    path.  The Predictor sizes its table from the shard headers."""
+    from fastapi.testclient import TestClient
+
+    from xflow_amd import checkpoint, native
+    from xflow_amd.serve import Predictor, make_app
+
+    want = _train(tmp_path, "mvm")
+    p = Predictor(str(tmp_path / "ck"), device=torch.device("cpu"))
+    shards = [os.path.join(p.ckpt, f) for f in os.listdir(p.ckpt) if f.endswith(".xftb")]
+    assert sum(checkpoint.shard_keys(f) for f in shards) == p.keys == \
+        sum(len(checkpoint.read_shard(f)[1]) for f in shards)
+    c = TestClient(make_app(p))
+    lines = _test_text().decode().splitlines()[:6]
+    blk = native.load().parse_libffm(("\n".join(lines) + "\n").encode())
+    rp = np.asarray(blk["row_ptr"])
+    keys = np.asarray(blk["keys"]).view(np.uint64)
+    fg = np.asarray(blk["fgid"])
+    rows = [[int(k) for k in keys[rp[i]:rp[i + 1]]] for i in range(len(rp) - 1)]
+    fields = [[int(g) for g in fg[rp[i]:rp[i + 1]]] for i in range(len(rp) - 1)]
+    assert c.post("/predict", json={"keys": rows}).status_code == 400
+    r = c.post("/predict", json={"keys": rows, "fields": fields})
+    assert r.status_code == 200
+    np.testing.assert_allclose(r.json()["pctr"], want[:6, 0], rtol=2e-5, atol=1e-6)

@@ -39,6 +39,17 @@ def shard_name(rank: int, world: int) -> str:
     return f"shard-{rank:05d}-of-{world:05d}.xftb"
 
 
+def shard_keys(path: str) -> int:
+    """Number of keys in a native shard file, from its header only (48 bytes
+    read, not the keys and state words)."""
+    with open(path, "rb") as f:
+        if f.read(8) != MAGIC:
+            raise ValueError(f"{path}: not an xflow table shard")
+        f.seek(32, os.SEEK_CUR)
+        (n,) = struct.unpack("<Q", f.read(8))
+    return int(n)
+
+
 def read_shard(path: str):
     """(header ints, keys u64, words u32 [n, W]) of a native shard file."""
     with open(path, "rb") as f:

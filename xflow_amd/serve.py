@@ -65,9 +65,9 @@ class Predictor:
         self.model = _fields(ModelConfig, meta["model"])
         self.optim = _fields(OptimConfig, meta["optim"])
         self.meta = meta
-        n_keys = 0
-        for p in glob.glob(os.path.join(self.ckpt, "shard-*-of-%05d.xftb" % int(meta["world"]))):
-            n_keys += int(checkpoint.read_shard(p)[1].shape[0])
+        # (key counts from the shard headers: nothing else is read twice)
+        n_keys = sum(checkpoint.shard_keys(p) for p in glob.glob(
+            os.path.join(self.ckpt, "shard-*-of-%05d.xftb" % int(meta["world"]))))
         # every shard's keys in one table at load <= 0.5 (no growth while serving)
         lg = max(16, int(math.ceil(math.log2(max(2 * n_keys, 1)))))
         if device is None:
@@ -87,14 +87,20 @@ class Predictor:
     def predict_csr(self, keys: np.ndarray, row_ptr: np.ndarray,
                     fgid: Optional[np.ndarray] = None) -> np.ndarray:
         """pctr of every row of a CSR batch (keys u64, row_ptr rows+1 offsets;
-        fgid: the field ids MVM groups by, zeros when absent)."""
+        fgid: the field ids MVM groups by -- required for an MVM model, whose
+        field products would be wrong with every feature in one field)."""
         keys = np.ascontiguousarray(keys).view(np.uint64)
         row_ptr = np.asarray(row_ptr, dtype=np.int64)
         rows = len(row_ptr) - 1
         if rows < 0 or row_ptr[0] != 0 or row_ptr[-1] != len(keys):
             raise ValueError("row_ptr must hold rows+1 offsets from 0 to len(keys)")
         if fgid is None:
+            if self.model.kind == "mvm":
+                raise ValueError("an MVM model groups features by field: give the field ids "
+                                 "(fgid / 'fields') with the keys")
             fgid = np.zeros(len(keys), np.int32)
+        elif len(fgid) != len(keys):
+            raise ValueError("fgid must hold one field id per key")
         out = np.empty(rows, np.float32)
         cap_nnz = self.engine.cfg.max_nnz
         r = 0
@@ -127,13 +133,20 @@ class Predictor:
         return self.predict_csr(np.asarray(blk["keys"]).view(np.uint64),
                                 np.asarray(blk["row_ptr"], np.int64), np.asarray(blk["fgid"]))
 
-    def predict_keys(self, rows: Sequence[Sequence[int]]) -> np.ndarray:
-        """pctr of rows given as lists of (already hashed) u64 keys."""
+    def predict_keys(self, rows: Sequence[Sequence[int]],
+                     fields: Optional[Sequence[Sequence[int]]] = None) -> np.ndarray:
+        """pctr of rows given as lists of (already hashed) u64 keys, with the
+        keys' field ids (same shape; required for MVM)."""
         lens = np.array([len(r) for r in rows], np.int64)
         rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         keys = (np.array([k for r in rows for k in r], dtype=np.uint64) if len(rp) > 1 and rp[-1]
                 else np.zeros(0, np.uint64))
-        return self.predict_csr(keys, rp)
+        fg = None
+        if fields is not None:
+            if [len(f) for f in fields] != lens.tolist():
+                raise ValueError("'fields' must give one field id per key of every row")
+            fg = np.array([g for f in fields for g in f], dtype=np.int32)
+        return self.predict_csr(keys, rp, fg)
 
 
 # -------------------------------------------------------------------- service
@@ -145,7 +158,8 @@ def make_app(pred: Predictor):
     # (built with explicit types: this module's postponed annotations would
     # leave FastAPI a string to resolve in a function scope)
     Req = create_model("PredictRequest", libffm=(Optional[str], None),
-                       keys=(Optional[list[list[int]]], None))
+                       keys=(Optional[list[list[int]]], None),
+                       fields=(Optional[list[list[int]]], None))
 
     app = FastAPI(title="xflow-amd predictor")
 
@@ -159,7 +173,7 @@ def make_app(pred: Predictor):
             raise HTTPException(400, "give exactly one of 'libffm' or 'keys'")
         try:
             p = (pred.predict_libffm(req.libffm) if req.libffm is not None
-                 else pred.predict_keys(req.keys))
+                 else pred.predict_keys(req.keys, req.fields))
         except ValueError as e:
             raise HTTPException(400, str(e))
         return {"pctr": [float(x) for x in p]}
