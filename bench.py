@@ -202,6 +202,9 @@ def main():
     engine.read_stats(reset=True)
     if sharded is not None:
         sharded.host_waits = 0
+        sharded.mid_step_waits = 0
+        sharded.host_wait_s = 0.0
+    mon0 = engine.monitor_wait_seconds
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -209,6 +212,10 @@ def main():
     if hasattr(sharded, "flush"):
         sharded.flush()  # the last pushes are part of the timed work
     t_issue = time.perf_counter() - t0  # host time to queue the steps (bounded by monitor lag)
+    # of which blocked: on the monitor's run-ahead bound (the device is
+    # monitor_lag steps behind) and on split-size reads (multi-rank)
+    t_blocked = engine.monitor_wait_seconds - mon0 + (sharded.host_wait_s if sharded is not None
+                                                      else 0.0)
     sync()
     elapsed = time.perf_counter() - t0
     st = engine.read_stats(reset=True)
@@ -263,10 +270,16 @@ def main():
             "table_load": table_keys / float(world * 2 ** log2_cap),
             "prefilled_keys": int(prefill_tot),
             "host_waits": int(sharded.host_waits) if sharded is not None else 0,
+            # multi-rank: split-size reads of the next batch in the middle of a
+            # step (for its early key exchange) that found the copy in flight
+            "mid_step_waits": int(getattr(sharded, "mid_step_waits", 0)),
             # multi-rank: steps whose next batch's keys rode with the gradient
             # exchange (2 RCCL group calls per step instead of 3)
             "early_key_exchanges": int(getattr(sharded, "early_key_exchanges", 0)),
-            "host_issue_ms_per_step": 1000.0 * t_issue / a.steps,
+            # host time to issue a step, net of the time blocked (the device
+            # being behind is not host cost), and the blocked time itself
+            "host_issue_ms_per_step": 1000.0 * (t_issue - t_blocked) / a.steps,
+            "host_blocked_ms_per_step": 1000.0 * t_blocked / a.steps,
             "monitor_lag": a.monitor_lag,
         }
         if a.model == "fm":

@@ -428,8 +428,14 @@ void Engine::train_step(const BatchView& b) {
   // the unique-order outputs of a multi-slice step and their slice bits
   const bool uq = Sf > 1 && (lr16 || fmu || fsu);
   if (uq && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
-  dedup_(b, 1, nullptr, lr16 || fmu || rowu);
+  // unique-index positions (Backend::remap_pos, FwdArgs::red_nuq): pulled
+  // rows, gradient destinations and every gradient / mask buffer in unique
+  // order -- the reductions span the unique keys, not the scratch slots
+  const bool upos = be_->remaps_positions() && red_pairs_;
+  if (upos) ensure_inv();
+  dedup_(b, 1, nullptr, upos || lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)
+  if (upos) be_->remap_pos(pos_, b.nnz, inv_, (u32)scratch_.cap);
   guard_inserts(b.nnz);  // (<= nnz new keys; may grow the table first)
 
   PullArgs pa;
@@ -441,7 +447,7 @@ void Engine::train_step(const BatchView& b) {
   pa.insert = true;
   pa.out_slot = uniq_slot_;
   pa.out_vals = wpull_;
-  pa.out_map = uniq_pos_;
+  pa.out_map = upos ? nullptr : uniq_pos_;
   pa.pstride = ps;
   pa.fm_vals = fm_vals_;
   if (fm_keep_w) pa.out_w = fm_w_;
@@ -486,6 +492,7 @@ void Engine::train_step(const BatchView& b) {
     fa.agg_ok = (double)scratch_.cap * Sg * ps < 4294967295.0;
     fa.fx_bad = overflow_;
     set_reduction(fa);
+    if (upos) fa.red_nuq = n_uniq_;
     // slice bits from the reduction (unique order with the outputs, else
     // slot-indexed), else per occurrence
     if (uq) fa.red_masks = lr_mask_;
@@ -496,18 +503,20 @@ void Engine::train_step(const BatchView& b) {
                     cfg_.model.fm_math == kFmReference;
     fa.fm_vals = fm_vals_;
     if (fm_vals_ && !fa.fm_compact) throw std::logic_error("train_step: compact FM rows need the reduction");
+    // (unique-index positions: the outputs' rows are the dests' own)
+    const u32* oinv = upos ? nullptr : inv_;
     if (lr16) {
       fa.red_out = lr_grad_;
-      fa.red_inv = inv_;
+      fa.red_inv = oinv;
       fa.red_rows = srk;
     }
     if (fmu) {
       fa.red_out = fm_grad_;
-      fa.red_inv = inv_;
+      fa.red_inv = oinv;
     }
     if (rowu) {
       fa.red_out = row_grad_;
-      fa.red_inv = inv_;
+      fa.red_inv = oinv;
     }
     be_->forward_backward(fa);
 
@@ -519,7 +528,7 @@ void Engine::train_step(const BatchView& b) {
     aa.n_dev = n_uniq_;
     aa.n_max = b.nnz;
     aa.grads = grad_;
-    aa.grad_map = uniq_pos_;
+    aa.grad_map = upos ? nullptr : uniq_pos_;  // (slot- or unique-indexed rows)
     aa.masks = masks ? tmask_ : nullptr;
     aa.masks_rw = masks ? tmask_ : nullptr;
     aa.zero_after = true;
@@ -1085,10 +1094,12 @@ void Engine::poll_snapshots(int64_t wait_upto) {
     if (!snap_ready(seq)) {
       if (seq > wait_upto) break;
       ++monitor_waits_;
+      const auto t0 = std::chrono::steady_clock::now();
       for (int spin = 0; !snap_ready(seq); ++spin) {
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
         else std::this_thread::yield();
       }
+      monitor_wait_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     const unsigned long long w = *reinterpret_cast<volatile unsigned long long*>(&snaps_[i].word);
     const int64_t size = (int64_t)(w & 0xFFFFFFFFull);

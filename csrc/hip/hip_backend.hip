@@ -183,6 +183,10 @@ class HipBackend final : public Backend {
   void slice_masks(const BatchView& b, const u32* pos, u32* tmask) override {
     hip::launch_slice_masks(b, pos, tmask, stream_);
   }
+  bool remaps_positions() const override { return true; }
+  void remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none) override {
+    hip::launch_remap_pos(pos, nnz, inv, none, stream_);
+  }
   void bucket(const BucketArgs& a) override { hip::launch_bucket(a, stream_); }
   bool partitioned_dedup() const override { return true; }
   void partition_counts(const ScratchView& s, const u32* chunk_offsets, const int64_t* n_uniq,

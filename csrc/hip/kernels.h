@@ -17,6 +17,7 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st);
 void launch_gather_grads(const GatherGradArgs& a, hipStream_t st);
 void launch_owner_group(const OwnerGroupArgs& a, hipStream_t st);
 void launch_bucket(const BucketArgs& a, hipStream_t st);
+void launch_remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none, hipStream_t st);
 void launch_partition_counts(const ScratchView& s, const u32* chunk_offsets,
                              const int64_t* n_uniq, int64_t* counts, int64_t seq, hipStream_t st);
 void launch_scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,

@@ -18,6 +18,10 @@
 namespace xflow {
 namespace hip {
 
+// unique index of a gradient row: through the slot -> unique map, or the row
+// itself when the positions already are unique indices (inv == null)
+__device__ __forceinline__ u32 uix(const u32* inv, u64 x) { return inv ? inv[x] : (u32)x; }
+
 __device__ __forceinline__ int slice_of(const BatchView& b, int64_t r, int S) {
   if (b.slice_rows <= 0) return 0;
   int64_t s = r / b.slice_rows;
@@ -31,8 +35,14 @@ struct RedGeom {
   const unsigned long long* bcap;
   u64 cap;
   int S;
+  // unique-index positions (FwdArgs::red_nuq): dests = unique * S + s lie
+  // below the batch's unique count times S
+  const int64_t* nuq;
+  __device__ __forceinline__ u64 rows() const {
+    return nuq ? (u64)*nuq : (bcap ? (u64)*bcap : cap);
+  }
   __device__ __forceinline__ int shift(int base) const {
-    const u64 dests = (bcap ? (u64)*bcap : cap) * (u64)S;
+    const u64 dests = rows() * (u64)S;
     int sh = base;
     while (((dests + (1ull << sh) - 1) >> sh) > (u64)kRedMaxBuckets) ++sh;
     return sh;
@@ -40,14 +50,14 @@ struct RedGeom {
   // buckets this step's dests reach (of the nb allocated for the full
   // capacity): producers, scans and sums skip the rest
   __device__ __forceinline__ int active(int shift, int nb) const {
-    const u64 dests = (bcap ? (u64)*bcap : cap) * (u64)S;
+    const u64 dests = rows() * (u64)S;
     const u64 n = (dests + (1ull << shift) - 1) >> shift;
     return n < (u64)nb ? (int)n : nb;
   }
 };
 
 __host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
-  return RedGeom{a.red_bcap, a.red_cap, a.S};
+  return RedGeom{a.red_bcap, a.red_cap, a.S, a.red_nuq};
 }
 
 __device__ __forceinline__ int red_active(const FwdArgs& a, int base) {
@@ -809,7 +819,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
   auto put_mask = [&](u64 slot, u32 bits) {
     u64 m = slot;
     if (f.out) {  // (NV == 1, S > 1) unique order
-      m = f.inv[slot];
+      m = uix(f.inv, slot);
       if (m == 0xFFFFFFFFu) return;
     }
     if (slot * S >= lo && slot * S + S <= lo + kR) f.masks[m] = bits;
@@ -827,7 +837,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
         // normalised like the gather would (lr_worker.cc:116-118, in double);
         // S > 1: [unique][slice], per-slice rows
         const u64 slot = dest / S, sl = dest - slot * S;
-        const u32 o = f.inv[slot];
+        const u32 o = uix(f.inv, slot);
         if (o != 0xFFFFFFFFu)  // (not the trash slot)
           f.out[(u64)o * S + sl] = (float)(fx_to_double<kFx>(a) / (double)f.rows[sl]);
       } else {
@@ -842,7 +852,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
       if (f.compact) {  // expanded by the apply (k_apply_group)
         if (f.out) {    // unique (send) order; S > 1: [unique][slice]
           const u64 slot = dest / S, sl = dest - slot * S;
-          const u32 o0 = f.inv[slot];
+          const u32 o0 = uix(f.inv, slot);
           if (o0 == 0xFFFFFFFFu) return;
           const u64 o = (u64)o0 * S + sl;
           if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
@@ -1418,7 +1428,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
       float* row = grad + (lo + l) * PS;
       if (out) {  // the unique-order row (FwdArgs::red_out); S > 1: [unique][slice]
         const u64 slot = (lo + l) / (u64)S;
-        const u32 u = inv[slot];
+        const u32 u = uix(inv, slot);
         if (u == 0xFFFFFFFFu) continue;
         row = out + ((u64)u * (u64)S + (lo + l - slot * (u64)S)) * PS;
       }
@@ -1498,8 +1508,8 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
   const int groups = (int)((a.batch.rows + BLOCK - 1) / BLOCK);
   const RedGeom geom = red_geom(a);
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
-  if (a.red_out && (!a.red_inv || (a.S != 1 && !a.red_masks)))
-    throw std::runtime_error("standard FM red_out: the slot -> unique map (S > 1: and slice bits)");
+  if (a.red_out && a.S != 1 && !a.red_masks)
+    throw std::runtime_error("standard FM red_out with several slices needs the slice bits");
   u32* masks = a.S > 1 ? a.red_masks : nullptr;
   // scatter-free form: the sub-range starts ([nb][groups] u32) live in red_sorted
   const bool seg = groups <= kSegMaxGroups &&
@@ -1970,7 +1980,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           const u32 pj = pos[rs.at(j)];
           float* g = a.grad + ((size_t)pj * S + s) * PS;
           if (a.red_out) {  // (one slice: the unique-order rows k_mvm_red_sum adds to)
-            const u32 o = a.red_inv[pj];
+            const u32 o = uix(a.red_inv, pj);
             if (o == 0xFFFFFFFFu) continue;
             g = a.red_out + (size_t)o * PS;
           }
@@ -2142,7 +2152,7 @@ __global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict
 #pragma unroll
       for (int k = 0; k < D; ++k) any = any || acc[l * D + k] != 0.0f;
       if (!any) continue;
-      const u32 o = f.inv[dest];
+      const u32 o = uix(f.inv, dest);
       if (o == 0xFFFFFFFFu) continue;
       g = f.out + (u64)o * PS;
     }
@@ -2172,8 +2182,8 @@ static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
                      red_geom(a));
   const int nsubt = mvm_nsub(D) * a.red_nsub;
   const int grid = ((a.red_nb + 7) / 8) * 8 * nsubt;
-  if (a.red_out && (a.S != 1 || !a.red_inv))
-    throw std::runtime_error("MVM red_out: one slice and the slot -> unique map");
+  if (a.red_out && a.S != 1)
+    throw std::runtime_error("MVM red_out: one slice");
   MvmRedFinal f{a.grad, a.S > 1 ? a.red_masks : nullptr, a.red_out, a.red_inv, a.wpull,
                 a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
   hipLaunchKernelGGL(k_mvm_red_sum<D>, dim3(grid), dim3(kRedBlock), 0, st,

@@ -383,6 +383,38 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
   }
 }
 
+// Unique-index positions (the fused single-rank step): each occurrence's
+// scratch slot becomes its index in the batch's unique list (inv, written by
+// the compaction), the trash slot's occurrences get `none`.  Pulled rows,
+// gradient destinations (unique * S + s) and the unique-order outputs then
+// share one dense index space: the reductions span the batch's unique keys
+// instead of the 4x-headroom scratch capacity, the pulled rows are 4x denser
+// in the caches, and no slot -> unique map is read at the output.  Four
+// occurrences per lane (dwordx4 in and out, four independent gathers).
+__global__ void __launch_bounds__(kBlock) k_remap_pos(u32* __restrict__ pos, int64_t nnz,
+                                                      const u32* __restrict__ inv, u32 none) {
+  const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+  auto map = [&](u32 p) {
+    const u32 u = inv[p];
+    return u == 0xFFFFFFFFu ? none : u;
+  };
+  if (i + 4 <= nnz) {
+    const uint4 p = *reinterpret_cast<const uint4*>(pos + i);
+    *reinterpret_cast<uint4*>(pos + i) = make_uint4(map(p.x), map(p.y), map(p.z), map(p.w));
+  } else {
+    for (int64_t j = i; j < nnz; ++j) pos[j] = map(pos[j]);
+  }
+}
+
+void launch_remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none, hipStream_t st) {
+  if (nnz <= 0) return;
+  if (reinterpret_cast<uintptr_t>(pos) & 15) throw std::runtime_error("remap_pos: pos must be 16-byte aligned");
+  const int64_t lanes = (nnz + 3) / 4;
+  hipLaunchKernelGGL(k_remap_pos, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     st, pos, nnz, inv, none);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
 // Owner-partitioned dedup: the unique list is in slot order, so owner o's
 // keys start at the number of stamped slots below o*R = the compaction offset
 // of the chunk holding o*R plus the hits in that chunk below it (one wave per

@@ -145,6 +145,11 @@ struct FwdArgs {
   // summed by several workgroups (red_nsub: the most that can be needed).
   const unsigned long long* red_bcap = nullptr;
   uint64_t red_cap = 0;            // allocated scratch capacity (upper bound)
+  // Unique-index positions (Engine's fused step, Backend::remap_pos): pos
+  // holds each occurrence's index in the batch's unique list, wpull is in
+  // unique order, dests = unique * S + s lie below red_nuq[0] * S, and the
+  // unique-order outputs take dest / S directly (red_inv == null)
+  const int64_t* red_nuq = nullptr;
   int red_nsub = 1;
   // S > 1: the reduction also writes each slot's slice-presence bits
   // (red_masks[slot] |= 1 << s for every (key, slice) with an occurrence),
@@ -435,6 +440,14 @@ class Backend {
   virtual void table_apply(const ApplyArgs& a) = 0;
   virtual void forward_backward(const FwdArgs& a) = 0;
   virtual void slice_masks(const BatchView& b, const u32* pos, u32* tmask) = 0;
+  // pos[i] = inv[pos[i]] for i < nnz (scratch slot -> unique-list index; the
+  // trash slot's occurrences get `none`): the fused step's unique-index
+  // positions (FwdArgs::red_nuq).  HIP only (the compaction writes inv).
+  virtual bool remaps_positions() const { return false; }
+  virtual void remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none) {
+    (void)pos, (void)nnz, (void)inv, (void)none;
+    throw std::runtime_error("remap_pos is not supported by this backend");
+  }
   virtual void bucket(const BucketArgs& a) = 0;
   // Owner-partitioned dedup (ScratchView::parts > 1, HIP only): per-owner
   // counts of the unique list from the compaction's chunk offsets.

@@ -147,6 +147,9 @@ class Engine {
   // waits the monitor needed, and an explicit growth to 2^log2_cap slots
   int64_t table_growths() const { return growths_; }
   int64_t monitor_waits() const { return monitor_waits_; }
+  // host seconds spent blocked on the monitor's run-ahead bound (the device
+  // was monitor_lag steps behind): subtracted from the host's issue time
+  double monitor_wait_seconds() const { return monitor_wait_s_; }
   void grow_table(int log2_cap);
   // queue a snapshot of (table size, overflow flags) behind the step's
   // work; called at the end of every training step (fused or sharded)
@@ -375,6 +378,7 @@ class Engine {
   int64_t known_adds_ = 0;          // cumulative insert bound queued before it
   int64_t queued_adds_ = 0;         // cumulative insert bound queued so far
   int64_t growths_ = 0, monitor_waits_ = 0;
+  double monitor_wait_s_ = 0.0;
   int log2_cap_ = 0, max_log2_cap_ = 31;
   void poll_snapshots(int64_t wait_upto);
   void guard_inserts(int64_t n);   // before an inserting pull of <= n new keys

@@ -251,6 +251,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("monitor_lag") = 2, py::arg("owner_group") = 0)
       .def_property_readonly("table_growths", &Engine::table_growths)
       .def_property_readonly("monitor_waits", &Engine::monitor_waits)
+      .def_property_readonly("monitor_wait_seconds", &Engine::monitor_wait_seconds)
       .def("grow_table", &Engine::grow_table, py::call_guard<py::gil_scoped_release>())
       .def("end_step", &Engine::end_step, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("is_gpu", &Engine::is_gpu)

@@ -333,6 +333,11 @@ class Engine:
         """Host waits of the capacity monitor (bounded run-ahead, exact-size reads)."""
         return int(self._e.monitor_waits)
 
+    @property
+    def monitor_wait_seconds(self) -> float:
+        """Host seconds blocked by the monitor's run-ahead bound."""
+        return float(self._e.monitor_wait_seconds)
+
     def grow_table(self, log2_cap: int) -> None:
         """Rehash the table into 2^log2_cap slots now (normally automatic)."""
         self._sync_stream()

@@ -161,6 +161,6 @@ class AsyncShardedEngine(ShardedEngine):
             self.p2p_ops += 1
             self._apply(p)
 
-    def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         self.flush()
         return super().eval_step(batch, pctr)

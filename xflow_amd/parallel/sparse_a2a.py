@@ -115,6 +115,7 @@ class ShardedEngine:
         self._ahead_no = 0
         self.early_key_exchanges = 0  # steps whose next keys rode with the gradients
         self.mid_step_waits = 0       # of those, split-size reads that waited
+        self.host_wait_s = 0.0        # host seconds blocked on split-size reads (both kinds)
         # one per server buffer: compact-FM applies read the values served
         # by their step's pull (the async step applies after the next pull)
         self._vals_out = [_Buf(torch.float32, dev), _Buf(torch.float32, dev)]
@@ -313,7 +314,9 @@ class ShardedEngine:
                     self.mid_step_waits += 1
                 else:
                     self.host_waits += 1
+                tw = time.perf_counter()
                 ev.synchronize()
+                self.host_wait_s += time.perf_counter() - tw
             both = self._counts_host[wb].tolist()
         else:
             both = both.tolist()
@@ -478,16 +481,20 @@ class ShardedEngine:
             for g, m, Sg in groups:
                 e.s_apply(recv_keys, g, m, offs, Sg, buf=buf)
 
-    def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def eval_step(self, batch: Batch, pctr: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         """Forward-only sharded step (keys looked up, never inserted).  Every
-        rank must call it (a rank without test data passes an empty batch)."""
+        rank must call it (a rank without test data passes an empty batch);
+        returns None on every rank when no rank had rows (the counts exchange
+        says so: the evaluation loop's end, without another collective)."""
         e = self.engine
-        if pctr is None:
-            pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
         # (keys exchanged ahead for a training batch no step will take now:
         # every rank drops them at the same point)
         self._ahead = None
-        wb, send_splits, recv_splits, _, _ = self._take(batch)
+        wb, send_splits, recv_splits, _, any_data = self._take(batch)
+        if not any_data:
+            return None
+        if pctr is None:
+            pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
         recv_keys = self._exchange_keys(wb, send_splits, recv_splits)
         ps = e.value_width  # floats per pulled value row
         vals = self._vals_out[0].get(self.last_recv * ps).view(self.last_recv, ps)

@@ -235,9 +235,12 @@ class Trainer:
                     nxt = stream.next
                 record = [] if cfg.resident else None
             t0 = time.perf_counter()
+            steps0 = self.steps
             ep_samples = 0
             sh = self.sharded
-            w0 = (sh.host_waits, sh.inline_prepares) if sh is not None else (0, 0)
+            w0 = ((sh.host_waits, sh.inline_prepares, sh.mid_step_waits, sh.host_wait_s)
+                  if sh is not None else (0, 0, 0, 0.0))
+            mw0 = self.engine.monitor_wait_seconds
             it = self._epoch_batches(nxt, record)
             empty = self._empty_batch()
             cur = next(it, None)
@@ -298,11 +301,21 @@ class Trainer:
                        monitor_waits=self.engine.monitor_waits)
             if timeline is not None:
                 rec["timeline"] = {k: round(v, 3) for k, v in timeline.items()}
+            # host time per step net of the time it sat blocked (monitor
+            # run-ahead bound, split-size reads): what issuing a step costs
+            ep_wall = time.perf_counter() - t0
+            blocked = self.engine.monitor_wait_seconds - mw0 + (
+                sh.host_wait_s - w0[3] if sh is not None else 0.0)
+            n_ep = max(1, self.steps - steps0)
+            rec["host_issue_ms_per_step"] = round(1000.0 * (ep_wall - blocked) / n_ep, 4)
+            rec["host_blocked_ms_per_step"] = round(1000.0 * blocked / n_ep, 4)
             if sh is not None:
                 # split-size reads that found the device copy in flight, and
                 # steps whose batch was not prepared ahead (the epoch's first)
                 rec["host_waits"] = sh.host_waits - w0[0]
                 rec["inline_prepares"] = sh.inline_prepares - w0[1]
+                # next-batch split-size reads inside a step that had to wait
+                rec["mid_step_waits"] = sh.mid_step_waits - w0[2]
                 rec["early_key_exchanges"] = getattr(sh, "early_key_exchanges", 0)
             if self.cfg.optim.lambda1 > 0 and os.environ.get("XFLOW_REPORT_NNZ"):
                 rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
@@ -342,18 +355,28 @@ class Trainer:
                       else nat.BlockReader(tpath, cfg.resolved_test_block()))
         compat_mvm = model_kind(cfg.model.kind) == 2 and cfg.mvm_predict_compat
         while True:
-            blk = reader.next() if reader is not None else None
-            if not xdist.all_any(blk is not None, self.device):
+            blk, used, sr = None, 0, 0
+            while reader is not None:
+                # (a block whose rows the slicing rule drops entirely -- fewer
+                # rows than threads -- predicts nothing: skipped here, without
+                # an exchange)
+                blk = reader.next()
+                if blk is None:
+                    break
+                used, sr = self._split(len(blk["labels"]))
+                if used > 0:
+                    break
+            if self.sharded is None and blk is None:
                 break
-            rows = 0 if blk is None else len(blk["labels"])
-            used, sr = self._split(rows)
             b = self._to_batch(blk, used, sr)
             if self.sharded is not None:
+                # every rank joins; "no test data left anywhere" travels in the
+                # eval exchange's counts (no per-block collective)
                 pctr = self.sharded.eval_step(b)
-            elif b.rows > 0:
-                pctr = self.engine.eval_step(b)
+                if pctr is None:
+                    break
             else:
-                continue
+                pctr = self.engine.eval_step(b)
             if b.rows == 0:
                 continue
             p, y = pctr[:used], b.labels[:used]

@@ -9,9 +9,14 @@
 * Fault injection for tests, from the environment (never set in production):
     XFLOW_FAULT=kill:<rank>:<step>      rank exits abruptly before that step
     XFLOW_FAULT=hang:<rank>:<step>      rank stops making progress (sleeps)
-    XFLOW_FAULT=drop_a2a:<rank>:<step>  rank skips one exchange of that step (its
-                                        peers detect the out-of-step counts or
-                                        time out)
+    XFLOW_FAULT=drop_a2a:<rank>:<step>  rank skips one exchange of that step.  On
+                                        the gloo / loopback transports its peers
+                                        detect the out-of-step counts at the next
+                                        exchange; on the native RCCL transport the
+                                        skipped exchange is one send/recv inside a
+                                        group call, so the peers block in that call
+                                        and the fault surfaces only through the
+                                        collective timeout / the watchdog
 """
 from __future__ import annotations
 
