@@ -430,8 +430,14 @@ void Engine::train_step(const BatchView& b) {
   if (uq && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
   // unique-index positions (Backend::remap_pos, FwdArgs::red_nuq): pulled
   // rows, gradient destinations and every gradient / mask buffer in unique
-  // order -- the reductions span the unique keys, not the scratch slots
-  const bool upos = be_->remaps_positions() && red_pairs_;
+  // order -- the reductions span the unique keys (S x that with S slices),
+  // not the 4x-headroom scratch slots.  The remap pass costs ~40 us per
+  // 10.2 M occurrences; same-box A/B (profiles/r4_unique_positions_ab.txt):
+  // a win with several slices (FM-8 std S = 8 143 -> 222 M samples/s, FM-8
+  // S = 8 +1.9 %, LR S = 8 +0.8 %) and for standard FM (+10.5 %), a loss for
+  // one-slice LR (-5.1 %), MVM (-3.5 %) and reference FM (-1.4 %).
+  const bool upos = be_->remaps_positions() && red_pairs_ &&
+                    (Sf > 1 || (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard));
   if (upos) ensure_inv();
   dedup_(b, 1, nullptr, upos || lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)

@@ -390,26 +390,39 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(ScratchView sv,
 // share one dense index space: the reductions span the batch's unique keys
 // instead of the 4x-headroom scratch capacity, the pulled rows are 4x denser
 // in the caches, and no slot -> unique map is read at the output.  Four
-// occurrences per lane (dwordx4 in and out, four independent gathers).
+// occurrences per lane (dwordx4 in and out, four independent gathers: 39.7 us
+// per 10.2 M occurrences; sixteen per lane measured 44.7 us).
+constexpr int kRemapPer = 4;
+
 __global__ void __launch_bounds__(kBlock) k_remap_pos(u32* __restrict__ pos, int64_t nnz,
                                                       const u32* __restrict__ inv, u32 none) {
-  const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
-  auto map = [&](u32 p) {
-    const u32 u = inv[p];
-    return u == 0xFFFFFFFFu ? none : u;
-  };
-  if (i + 4 <= nnz) {
-    const uint4 p = *reinterpret_cast<const uint4*>(pos + i);
-    *reinterpret_cast<uint4*>(pos + i) = make_uint4(map(p.x), map(p.y), map(p.z), map(p.w));
+  const int64_t i = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kRemapPer;
+  auto map = [&](u32 u) { return u == 0xFFFFFFFFu ? none : u; };
+  if (i + kRemapPer <= nnz) {
+    uint4 p[kRemapPer / 4];
+#pragma unroll
+    for (int q = 0; q < kRemapPer / 4; ++q) p[q] = reinterpret_cast<const uint4*>(pos + i)[q];
+    u32 u[kRemapPer];
+#pragma unroll
+    for (int q = 0; q < kRemapPer / 4; ++q) {
+      u[4 * q] = inv[p[q].x];
+      u[4 * q + 1] = inv[p[q].y];
+      u[4 * q + 2] = inv[p[q].z];
+      u[4 * q + 3] = inv[p[q].w];
+    }
+#pragma unroll
+    for (int q = 0; q < kRemapPer / 4; ++q)
+      reinterpret_cast<uint4*>(pos + i)[q] =
+          make_uint4(map(u[4 * q]), map(u[4 * q + 1]), map(u[4 * q + 2]), map(u[4 * q + 3]));
   } else {
-    for (int64_t j = i; j < nnz; ++j) pos[j] = map(pos[j]);
+    for (int64_t j = i; j < nnz; ++j) pos[j] = map(inv[pos[j]]);
   }
 }
 
 void launch_remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none, hipStream_t st) {
   if (nnz <= 0) return;
   if (reinterpret_cast<uintptr_t>(pos) & 15) throw std::runtime_error("remap_pos: pos must be 16-byte aligned");
-  const int64_t lanes = (nnz + 3) / 4;
+  const int64_t lanes = (nnz + kRemapPer - 1) / kRemapPer;
   hipLaunchKernelGGL(k_remap_pos, dim3((unsigned)((lanes + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      st, pos, nnz, inv, none);
   XF_HIP_CHECK(hipGetLastError());
