@@ -69,6 +69,12 @@ def parse():
                     help="config 4: bounded-staleness steps, pushes over RCCL send/recv riding in "
                          "the next step's key exchange")
     ap.add_argument("--staleness", type=int, default=1, help="--async: staleness in steps")
+    ap.add_argument("--sgd-v-init", type=float, default=1e-3,
+                    help="SGD latent init (sgd.h:69: the constant 0.001); MVM-SGD with 1.0 keeps "
+                         "the field product live (FTRL's first push shrinks v by ~|g|)")
+    ap.add_argument("--fields", type=int, default=39,
+                    help="fields (= features) per row: 13 int + (F-13) categorical Criteo fields; "
+                         "e.g. 18 like the bundled data (MVM's field product stays live)")
     ap.add_argument("--v-init-scale", type=float, default=1e-2,
                     help="latent init N(0,1)*scale (ftrl.h:114-120: 1e-2).  MVM on 39 fields "
                          "at 1e-2 has a field product that underflows to 0 (no gradient "
@@ -127,11 +133,12 @@ def main():
     if not use_gpu:
         log2_cap = min(log2_cap, 24)
         a.batch = min(a.batch, 4096)
-    synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed)
+    synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed,
+                        n_fields=a.fields)
     nnz = a.batch * synth.fields
     model = ModelConfig(kind=a.model, v_dim=a.v_dim, fm_math=a.fm_math, fm_mfma=a.fm_mfma)
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
-                                       v_init_scale=a.v_init_scale),
+                                       v_init_scale=a.v_init_scale, sgd_v_init=a.sgd_v_init),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
                                  max_slices=a.slices, monitor_lag=a.monitor_lag),
                     device=device)
@@ -220,6 +227,17 @@ def main():
     elapsed = time.perf_counter() - t0
     st = engine.read_stats(reset=True)
     tbl = engine.table_size()
+    # one more (untimed) step with the reduction's records counted: how much
+    # gradient work a step of this model does (MVM: none for rows whose field
+    # product vanished)
+    records = -1
+    if use_gpu:
+        engine.count_records(True)
+        step()
+        sync()
+        records = engine.take_records()
+        engine.count_records(False)
+        engine.read_stats(reset=True)
     nnzw = engine.nonzero_weights() if a.async_p2p else 0
     ovf = float(engine.overflowed())  # table probe wrap / dedup scratch overflow
     red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw), ovf,
@@ -250,10 +268,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic Criteo-1TB-shaped (39 fields: 13 log-binned int + 26 categorical, "
+            "data": "synthetic Criteo-1TB-shaped (%d fields: %d log-binned int + %d categorical, "
                     "power-law values, 1e9 hashed features, planted-logistic labels); FTRL table "
                     "prefilled (untimed) with %d keys the batches never touch (a long run's "
-                    "table occupancy), trained keys zero-init" % int(prefill_tot),
+                    "table occupancy), trained keys zero-init" % (
+                        synth.fields, min(synth.fields, 13), max(0, synth.fields - 13),
+                        int(prefill_tot)),
             "config": {"model": f"{a.model.upper()}-{a.optimizer.upper()}",
                        "global_batch": a.batch * world, "seq_len": synth.fields,
                        "parallelism": f"dp{world}+table-shard{world}",
@@ -267,6 +287,7 @@ def main():
             **({"shared_gpu_rehearsal": True} if shared_gpu else {}),
             "logloss": ln_loss / max(rows, 1.0),
             "table_keys": int(table_keys),
+            "reduction_records_per_step": int(records),
             "table_load": table_keys / float(world * 2 ** log2_cap),
             "prefilled_keys": int(prefill_tot),
             "host_waits": int(sharded.host_waits) if sharded is not None else 0,
@@ -289,6 +310,12 @@ def main():
             # MFMA form is an A/B option, slower on this sparse gather shape)
             out["config"]["fm_interaction"] = ("mfma" if a.fm_mfma and a.fm_math == "standard"
                                                else "valu")
+        if a.model == "mvm":
+            out["config"]["v_dim"] = a.v_dim
+            # a live MVM: the field products did not all vanish (logloss != ln 2)
+            out["mvm_live"] = abs(out["logloss"] - 0.6931471805599453) > 1e-4
+        if a.optimizer == "sgd":
+            out["config"]["sgd_v_init"] = a.sgd_v_init
         if a.async_p2p:
             out["config"]["parallelism"] += "+async-p2p(staleness=%d)" % a.staleness
             out["config"]["lambda1"] = a.lambda1

@@ -123,11 +123,14 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   const bool fm_std = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard;
   const bool mvm = cfg_.model.kind == kMVM;
   if (be.is_gpu() && (cfg_.model.kind == kLR || fm_ref || fm_std || mvm)) {
-    const int nv = fm_ref ? 2 : (fm_std ? 1 + cfg_.model.v_dim : 1), shift = red_shift(nv);
-    // u64 words per record slot: nv for LR / reference FM, the vector record for standard FM
-    const int recw = fm_std ? vec_rec_words(nv) / 2 : nv;
-    const int group_rows = fm_ref ? kFmGroupRows
-                                  : (mvm ? kMvmGroupRows : (fm_std ? kFmStdMinGroupRows : kLrGroupRows));
+    // values per record: 1 (LR), 2 (reference FM), the vector records of
+    // standard FM (1 + D) and MVM (D: per-row T = loss*M sums)
+    const bool vec = fm_std || mvm;
+    const int nv = fm_ref ? 2 : (fm_std ? 1 + cfg_.model.v_dim : (mvm ? cfg_.model.v_dim : 1));
+    const int shift = red_shift(nv);
+    // u64 words per record slot: nv for LR / reference FM, the vector record otherwise
+    const int recw = vec ? vec_rec_words(nv) / 2 : nv;
+    const int group_rows = fm_ref ? kFmGroupRows : (vec ? kFmStdMinGroupRows : kLrGroupRows);
     // (the trash slot's occurrences are never reduced: FwdArgs::trash_pos)
     // Buckets of 2^shift dests at the allocated capacity; beyond
     // kRedMaxBuckets the device widens the buckets (FwdArgs::red_bcap) and
@@ -181,7 +184,7 @@ Engine::~Engine() {
                   host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_, row_grad_,
-                  lr_mask_, fm_w_};
+                  lr_mask_, fm_w_, rec_count_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
   for (SrvBuf& b : srv_) {
@@ -241,9 +244,26 @@ bool Engine::reduction_masks() const {
          (cfg_.model.kind == kMVM && red_rowv_ != nullptr);
 }
 
+void Engine::count_records(bool on) {
+  if (on && !rec_count_) {
+    rec_count_ = balloc<unsigned long long>(*be_, 1);
+    be_->memset(rec_count_, 0, sizeof(unsigned long long));
+  }
+  rec_on_ = on;
+}
+
+int64_t Engine::take_records() {
+  if (!rec_count_) return -1;
+  unsigned long long n = 0;
+  be_->copy_d2h(&n, rec_count_, sizeof(n));
+  be_->memset(rec_count_, 0, sizeof(n));
+  return (int64_t)n;
+}
+
 void Engine::set_reduction(FwdArgs& fa) const {
   fa.trash_pos = (u32)scratch_.cap;
   if (!red_pairs_) return;
+  if (rec_on_) fa.red_records = rec_count_;
   fa.red_bcap = bcap_;
   fa.red_cap = scratch_.cap;
   fa.red_nsub = red_nsub_;

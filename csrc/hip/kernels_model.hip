@@ -12,6 +12,7 @@
 //   FM   fm_worker.cc:159-202 (loss), :126-157 (gradient)      [kFmReference]
 //   MVM  mvm_worker.cc:172-218 (loss), :137-170 (gradient)
 #include <cstdlib>
+#include <type_traits>
 #include "kernels.h"
 #include "hip_util.h"
 
@@ -438,7 +439,10 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   }
   if constexpr (kRed) {
     __syncthreads();
-    if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
+    if (threadIdx.x == 0) {
+      a.red_count[blockIdx.x] = lagg.written;
+      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.written);
+    }
     for (int i = threadIdx.x, n = red_active(a, red_shift(1)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
@@ -1052,7 +1056,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
     lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
   }
   __syncthreads();
-  if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
+  if (threadIdx.x == 0) {
+      a.red_count[blockIdx.x] = lagg.written;
+      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.written);
+    }
   for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
     a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   st.bad |= lagg.bad;
@@ -1086,15 +1093,19 @@ constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128);
 // kernel's LDS tables leave a CU two waves per SIMD for the row gathers), which
 // left (loss, loss*vs_k) per row in red_rowv -- the same floats the fused form
 // computes here, so both forms sum identical fixed-point values.
-template <int D, int BLOCK, bool kSeg = false, bool kSplit = false>
+// kFloat (MVM): float sums instead of fixed point -- MVM's T = loss*M spans
+// many orders of magnitude (a product over fields), beyond any one int64
+// fixed-point scale; the sums are then order-dependent in the last bits.
+template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kFloat = false>
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int NV = 1 + D;
   constexpr int LOG2 = ilog2c(2 * BLOCK);
   constexpr int kSlots = 1 << LOG2;
   constexpr int kFx = FxBits<1>::kFx;
+  using Acc = typename std::conditional<kFloat, float, long long>::type;
   __shared__ u64 s_tag[1][kSlots];
-  __shared__ long long s_acc[1][kSlots * NV];
+  __shared__ Acc s_acc[1][kSlots * NV];
   __shared__ unsigned short s_list[1][BLOCK];
   __shared__ u32 s_hist[kRedMaxBuckets];
   __shared__ u32 s_off[kSeg ? kRedMaxBuckets : 1];
@@ -1118,7 +1129,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   for (int i = threadIdx.x; i < kSlots; i += BLOCK) {
     s_tag[0][i] = ~0ull;
 #pragma unroll
-    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = 0ll;
+    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = (Acc)0;
   }
   for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) s_hist[i] = 0u;
   if (threadIdx.x < 3) s_nlist[threadIdx.x] = 0u;
@@ -1136,9 +1147,30 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   }
   const u32 S = (u32)a.S;
   const u32 sl = active ? (u32)slice_of(b, r, a.S) : 0u;
+  // kSplit: the row's vector (FM: loss, loss*vs_k; MVM: T_k = loss*M_k); a
+  // one-slice step emits nothing for an all-zero one (a zero contribution --
+  // every unique key is pushed anyway), several slices need every occurrence
+  // (the records' presence gives the slice bits)
+  float t[PS];
+  bool live = active;
+  if (kSplit && active) {
+    const float4* rv = reinterpret_cast<const float4*>(a.red_rowv + (size_t)r * PS);
+#pragma unroll
+    for (int q = 0; q < PS / 4; ++q) {
+      const float4 v4 = rv[q];
+      t[4 * q] = v4.x;
+      t[4 * q + 1] = v4.y;
+      t[4 * q + 2] = v4.z;
+      t[4 * q + 3] = v4.w;
+    }
+    bool nz = false;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) nz |= t[c] != 0.0f;
+    live = nz || S > 1u;
+  }
   if constexpr (kSeg) {
     // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (s_off)
-    for (int j = 0; j < len; ++j) {
+    for (int j = 0; j < len && live; ++j) {
       const u32 pj = pos[rs.at(j)];
       if (pj != a.trash_pos) atomicAdd(&s_hist[(pj * S + sl) >> shift], 1u);
     }
@@ -1173,16 +1205,6 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 #pragma unroll
   for (int k = 0; k < D; ++k) vs[k] = 0.0f;
   if (kSplit && active) {
-    const float4* rv = reinterpret_cast<const float4*>(a.red_rowv + (size_t)r * PS);
-    float t[PS];
-#pragma unroll
-    for (int q = 0; q < PS / 4; ++q) {
-      const float4 v4 = rv[q];
-      t[4 * q] = v4.x;
-      t[4 * q + 1] = v4.y;
-      t[4 * q + 2] = v4.z;
-      t[4 * q + 3] = v4.w;
-    }
     loss = t[0];
 #pragma unroll
     for (int k = 0; k < D; ++k) vs[k] = t[1 + k];
@@ -1220,13 +1242,13 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   for (int j = 0; j < maxlen; ++j) {
     const int t = 0;
     if (threadIdx.x == 0) s_nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
-    const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
+    const u32 pj = j < len && live ? pos[rs.at(j)] : a.trash_pos;
     const bool has = pj != a.trash_pos;
     bool claimed = false;
     u32 h = 0;
-    long long vals[NV];
+    Acc vals[NV];
 #pragma unroll
-    for (int c = 0; c < NV; ++c) vals[c] = 0ll;
+    for (int c = 0; c < NV; ++c) vals[c] = (Acc)0;
     if (has) {
       const u32 dest = pj * S + sl;
       const u64 key = ((u64)(u32)j << 32) | dest;
@@ -1249,16 +1271,24 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       // C_k = Σ loss*vs_k (v_k is the key's pulled value, one per step), so the
       // column walk needs no second gather of the pulled row; k_red_sum_vec
       // expands C - v*B once per dest
-      vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
+      if constexpr (kFloat) {
+        vals[0] = loss;
 #pragma unroll
-      for (int k = 0; k < D; ++k)
-        vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(kSplit ? vs[k] : loss * vs[k], bad));
+        for (int k = 0; k < D; ++k) vals[1 + k] = vs[k];  // (kSplit: the row's vector)
+      } else {
+        vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(kSplit ? vs[k] : loss * vs[k], bad));
+      }
     }
     if (has) {
-      long long* acc = &s_acc[t][h * NV];
+      Acc* acc = &s_acc[t][h * NV];
 #pragma unroll
-      for (int c = 0; c < NV; ++c)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)vals[c]);
+      for (int c = 0; c < NV; ++c) {
+        if constexpr (kFloat) atomicAdd(&acc[c], vals[c]);
+        else atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)vals[c]);
+      }
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -1277,9 +1307,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       wv[0] = d;
 #pragma unroll
       for (int c = 0; c < NV; ++c) {
-        long long* ap = &s_acc[t][hh * NV + c];
-        wv[1 + c] = __float_as_uint((float)fx_to_double<kFx>(*ap));
-        *ap = 0ll;
+        Acc* ap = &s_acc[t][hh * NV + c];
+        if constexpr (kFloat) wv[1 + c] = __float_as_uint(*ap);
+        else wv[1 + c] = __float_as_uint((float)fx_to_double<kFx>(*ap));
+        *ap = (Acc)0;
       }
 #pragma unroll
       for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
@@ -1299,7 +1330,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     lds_barrier();  // (one table: flushed before the next column inserts)
   }
   __syncthreads();
-  if (threadIdx.x == 0) a.red_count[blockIdx.x] = written;
+  if (threadIdx.x == 0) {
+    a.red_count[blockIdx.x] = written;
+    if (a.red_records) atomicAdd(a.red_records, (unsigned long long)written);
+  }
   for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK)
     a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   st.bad |= bad;
@@ -1326,7 +1360,12 @@ struct SegSrc {
 
 // G: segment-table capacity (groups); 512 keeps the rank-8 form at 76 KB of
 // LDS, two workgroups per CU (the per-unit phases are latency chains)
-template <int D, bool kSeg = false, int G = kSegMaxGroups>
+// kMvm: the records are MVM's per-row T = loss*M sums (NV = 1 + D = the MVM
+// latent dim) and the final gradient is g_k += Σ T_k / (1 + v_k), none where
+// v_k == 0 (mvm_worker.cc:137-170: the occurrence's field sum S is the key's
+// own v in a row without repeated fields); added to the rows (a repeated-field
+// row's gradients arrive there by atomics first).
+template <int D, bool kSeg = false, int G = kSegMaxGroups, bool kMvm = false>
 __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restrict__ sorted,
                                                            const u32* __restrict__ start,
                                                            float* __restrict__ grad,
@@ -1343,7 +1382,8 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   constexpr int kFx = FxBits<1>::kFx;
   constexpr int W = vec_rec_words(NV);
   using Rec = typename VecRedRec<NV>::T;
-  __shared__ long long acc[kR * NV];
+  using Acc = typename std::conditional<kMvm, float, long long>::type;  // (k_fm_std_red kFloat)
+  __shared__ Acc acc[kR * NV];
   __shared__ u32 seen[kR / 32];
   __shared__ u32 s_pre[kSeg ? G : 1];
   __shared__ u32 s_seg[kSeg ? G : 1];
@@ -1363,7 +1403,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
     }
     if (beg == end) continue;  // (block-uniform)
     const u64 lo = ((u64)bk << shift) + ((u64)sub << kShift);
-    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
+    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = (Acc)0;
     for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) seen[i] = 0u;
     if constexpr (kSeg) {
       // segment g: records [s_pre[g], s_pre[g+1]) of the bucket, at s_seg[g] + i
@@ -1399,16 +1439,35 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
         wv[4 * q + 2] = r.q[q].z;
         wv[4 * q + 3] = r.q[q].w;
       }
-      long long* ap = acc + l * NV;
+      Acc* ap = acc + l * NV;
 #pragma unroll
-      for (int c = 0; c < NV; ++c)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
-                  (unsigned long long)fx_from<kFx>(__uint_as_float(wv[1 + c])));
+      for (int c = 0; c < NV; ++c) {
+        if constexpr (kMvm) atomicAdd(&ap[c], __uint_as_float(wv[1 + c]));
+        else atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
+                       (unsigned long long)fx_from<kFx>(__uint_as_float(wv[1 + c])));
+      }
       atomicOr(&seen[l >> 5], 1u << (l & 31));
     }
     lds_barrier();
     for (u32 l = threadIdx.x; l < kR; l += kRedBlock) {
       if (!((seen[l >> 5] >> (l & 31)) & 1u)) continue;
+      if constexpr (kMvm) {
+        const u64 slot = (lo + l) / (u64)S;
+        float* row = grad + (lo + l) * PS;
+        if (out) {
+          const u32 u = uix(inv, slot);
+          if (u == 0xFFFFFFFFu) continue;
+          row = out + ((u64)u * (u64)S + (lo + l - slot * (u64)S)) * PS;
+        }
+        const float* w = wpull + slot * PS;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) {
+          const float t = acc[l * NV + c];
+          const float wk = w[c];
+          if (t != 0.0f && wk != 0.0f) row[c] += (float)((double)t / (1.0 + (double)wk));
+        }
+        continue;
+      }
       // (B, C_0..C_{D-1}) -> g_w = B, g_v[k] = C_k - v_k*B (k_fm_std_red)
       const double B = fx_to_double<kFx>(acc[l * NV]);
       const float4* v4 = reinterpret_cast<const float4*>(wpull + ((lo + l) / (u64)S) * PS);
@@ -1501,26 +1560,30 @@ __global__ void __launch_bounds__(kBlock) k_fm_std_fwd(FwdArgs a) {
 
 
 
-template <int D>
-static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
+// Vector-record reduction of NV = 1 + D sums per (key, slice): standard FM
+// (rows (loss, loss*vs_k) from k_fm_std_fwd, expanded with the pulled v) or,
+// kMvm, MVM (rows T_k = loss*M_k from k_mvm2<.., kRed>, divided by 1 + v_k).
+template <int D, bool kMvm = false>
+static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   constexpr int BLOCK = fmstd_block(D);
   constexpr int NV = 1 + D;
+  if (kMvm && !a.red_rowv) throw std::runtime_error("MVM vector reduction needs red_rowv");
   const int groups = (int)((a.batch.rows + BLOCK - 1) / BLOCK);
   const RedGeom geom = red_geom(a);
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
   if (a.red_out && a.S != 1 && !a.red_masks)
-    throw std::runtime_error("standard FM red_out with several slices needs the slice bits");
+    throw std::runtime_error("vector-record red_out with several slices needs the slice bits");
   u32* masks = a.S > 1 ? a.red_masks : nullptr;
   // scatter-free form: the sub-range starts ([nb][groups] u32) live in red_sorted
   const bool seg = groups <= kSegMaxGroups &&
                    (int64_t)a.red_nb * groups <= 2 * a.red_sorted_words &&
                    a.red_sorted_words * 8 / (vec_rec_words(NV) * 4) < (1ll << 32);
   const bool split = a.red_rowv != nullptr;
-  if (split)
+  if (split && !kMvm)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a);
   if (seg) {
-    if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true>), dim3(groups), dim3(BLOCK), 0, st, a);
+    if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true, kMvm>), dim3(groups), dim3(BLOCK), 0, st, a);
     else hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true>), dim3(groups), dim3(BLOCK), 0, st, a);
     hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
                        a.red_tot, geom, red_shift(NV));
@@ -1528,17 +1591,17 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                     BLOCK, groups};
     if (groups <= 512) {
       const u32 grid2 = std::min<u32>((u32)(a.red_nb * a.red_nsub), 2u * (u32)device_cus());
-      hipLaunchKernelGGL((k_red_sum_vec<D, true, 512>), dim3(grid2), dim3(kRedBlock), 0, st,
+      hipLaunchKernelGGL((k_red_sum_vec<D, true, 512, kMvm>), dim3(grid2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
                          a.red_out, a.red_inv, a.wpull, a.S, sg, masks);
     } else {
-      hipLaunchKernelGGL((k_red_sum_vec<D, true>), dim3(grid), dim3(kRedBlock), 0, st,
+      hipLaunchKernelGGL((k_red_sum_vec<D, true, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
                          a.red_out, a.red_inv, a.wpull, a.S, sg, masks);
     }
     return;
   }
-  if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, false, true>), dim3(groups), dim3(BLOCK), 0, st, a);
+  if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, false, true, kMvm>), dim3(groups), dim3(BLOCK), 0, st, a);
   else hipLaunchKernelGGL((k_fm_std_red<D, BLOCK>), dim3(groups), dim3(BLOCK), 0, st, a);
   hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
                      a.red_tot, geom, red_shift(NV));
@@ -1547,7 +1610,7 @@ static void launch_fmstd_reduction(const FwdArgs& a, hipStream_t st) {
                      a.batch, BLOCK, static_cast<const void*>(a.red_pairs), a.red_count,
                      a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
                      geom);
-  hipLaunchKernelGGL(k_red_sum_vec<D>, dim3(grid), dim3(kRedBlock), 0, st,
+  hipLaunchKernelGGL((k_red_sum_vec<D, false, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
                      a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks);
 }
@@ -1633,7 +1696,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
       lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
     }
     __syncthreads();
-    if (threadIdx.x == 0) a.red_count[blockIdx.x] = lagg.written;
+    if (threadIdx.x == 0) {
+      a.red_count[blockIdx.x] = lagg.written;
+      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.written);
+    }
     for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
   }
@@ -1774,7 +1840,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     constexpr int B = fm_block(DD);                                                      \
     int g = (int)((a.batch.rows + B - 1) / B);                                           \
     if (red_std) {                                                                       \
-      launch_fmstd_reduction<DD>(a, st);                                                 \
+      launch_vec_reduction<DD>(a, st);                                                 \
     } else if (red) {                                                                    \
       constexpr int R = kFmGroupRows;                                                    \
       const int gr = (int)((a.batch.rows + R - 1) / R);                                  \
@@ -1836,12 +1902,6 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
   __shared__ u32 s_tag[kAgg ? 2 : 1][kAgg ? (1 << LOG2) : 1];
   __shared__ float s_acc[kAgg ? 2 : 1][kAgg ? (1 << LOG2) * PS : 1];
   __shared__ int s_wmax[BLOCK / kWave];
-  __shared__ u32 s_hist[kRed ? kRedMaxBuckets : 1];
-  __shared__ u32 s_cnt;
-  if constexpr (kRed) {  // published by the barrier before the record loop
-    for (int i = threadIdx.x, n = red_active(a, kRedShift); i < n; i += BLOCK) s_hist[i] = 0u;
-    if (threadIdx.x == 0) s_cnt = 0u;
-  }
   const BatchView& b = a.batch;
   const bool compat = a.model.mvm_math == kMvmCompat;
   const u32* __restrict__ pos = a.pos;
@@ -1955,23 +2015,16 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
     };
     if constexpr (kRed) {
       // Dup-free rows: S of an occurrence is the key's own v, so the gradient
-      // factorises as T_k/(1+v_k) with T = loss*M per row -- one 8-byte
-      // record (dest, row) per occurrence, summed per key by k_mvm_red_sum.
-      // Rows with a repeated field (S = field sum): global atomics.
-      // S > 1 with slice bits from the reduction: a record for EVERY
-      // occurrence (T = 0 where the product vanished, and for repeated-field
-      // rows, whose gradients go by atomics), so that the bits show every
-      // slice that touched a key -- such a slice pushes, even a zero gradient
-      const bool all = a.red_masks != nullptr && S > 1u;
-      bool emit = false;
-      if (active && (all || (!dup && loss != 0.0f))) {
+      // factorises as T_k/(1+v_k) with T = loss*M per row: the row's T goes
+      // to red_rowv and the vector-record reduction (k_fm_std_red<D-1, ..,
+      // kSplit> + k_red_sum_vec<.., kMvm>) sums T per (key, slice) and
+      // divides once.  Rows with a repeated field (S = field sum): global
+      // atomics, and T = 0 (their occurrences still leave records, for the
+      // slice bits of a multi-slice step).
+      if (active) {
         float* t = a.red_rowv + (size_t)r * PS;
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-          t[k] = dup ? 0.0f : loss * M[k];
-          emit |= M[k] != 0.0f;
-        }
-        emit |= all;
+        for (int k = 0; k < PS; ++k) t[k] = (!dup && k < D) ? loss * M[k] : 0.0f;
       }
       if (active && dup) {
         for (int j = 0; j < len; ++j) {
@@ -1979,7 +2032,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           contrib(j, c);
           const u32 pj = pos[rs.at(j)];
           float* g = a.grad + ((size_t)pj * S + s) * PS;
-          if (a.red_out) {  // (one slice: the unique-order rows k_mvm_red_sum adds to)
+          if (a.red_out) {  // (one slice: the unique-order rows the reduction adds to)
             const u32 o = uix(a.red_inv, pj);
             if (o == 0xFFFFFFFFu) continue;
             g = a.red_out + (size_t)o * PS;
@@ -1988,38 +2041,6 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           for (int k = 0; k < D; ++k) atomicAdd(&g[k], c[k]);
         }
       }
-      const int m = wave_max(len);
-      if (threadIdx.x % kWave == 0) s_wmax[threadIdx.x / kWave] = m;
-      __syncthreads();
-      int maxlen = 0;
-#pragma unroll
-      for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
-      const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
-      u64* region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
-      const int lane = lane_id();
-      const int hshift = red_geom(a).shift(kRedShift);
-      for (int j = 0; j < maxlen; ++j) {
-        const u32 pj = emit && j < len ? pos[rs.at(j)] : a.trash_pos;
-        const bool has = pj != a.trash_pos;
-        const u32 dest = has ? pj * S + s : 0u;
-        const unsigned long long bm = __ballot(has);
-        if (bm) {
-          const int leader = __ffsll((long long)bm) - 1;
-          u32 base = 0;
-          if (lane == leader) base = atomicAdd(&s_cnt, (u32)__popcll(bm));
-          base = __shfl(base, leader);
-          if (has) {
-            region[base + (u32)__popcll(bm & ((1ull << lane) - 1ull))] =
-                (u64)dest | ((u64)(u32)r << 32);
-            XF_DASSERT((int)(dest >> hshift) < a.red_nb);
-            atomicAdd(&s_hist[dest >> hshift], 1u);
-          }
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) a.red_count[blockIdx.x] = s_cnt;
-      for (int i = threadIdx.x, n = red_active(a, kRedShift); i < n; i += BLOCK)
-        a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
     } else if constexpr (!kAgg) {
       for (int j = 0; j < len; ++j) {
         float c[D];
@@ -2054,160 +2075,25 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }
 
-// MVM bucket sums.  A bucket's 2^kRedShift destinations x D floats do not fit
-// in LDS, so NSUB workgroups share a bucket, each accumulating the records of
-// its 2^kRedShift/NSUB destinations (Σ T[row], D LDS atomics per record) and
-// skipping the rest.  The NSUB workgroups of a bucket are dispatched back to
-// back on the same XCD (workgroup i runs on XCD i % 8), so the bucket's
-// records come from HBM once and from that XCD's L2 after.  The final
-// gradient (mvm_worker.cc:137-170) is Σ T / (1 + v), 0 where v == 0, added to
-// grad (the duplicate-field rows' atomics may already be there).
-constexpr int mvm_nsub(int D) { return D <= 16 ? 16 : 32; }
-
-struct MvmRedFinal {
-  float* grad;
-  u32* masks;        // S > 1: slice bits of each slot (FwdArgs::red_masks), or null
-  float* out;        // one slice: unique-order rows out[inv[dest]] (FwdArgs::red_out), or null
-  const u32* inv;
-  const float* wpull;
-  const float* rowv;
-  int S, nb;
-  RedGeom geom;
-  int nsubt;  // sub-buckets per bucket in the grid (NSUB x the largest bucket widening)
-};
-
-template <int D>
-__global__ void __launch_bounds__(kRedBlock) k_mvm_red_sum(const u64* __restrict__ sorted,
-                                                           const u32* __restrict__ start,
-                                                           MvmRedFinal f) {
-  constexpr int PS = mvm_ps(D);
-  constexpr int NSUB = mvm_nsub(D);
-  constexpr int kSubShift = kRedShift - ilog2c(NSUB);
-  constexpr u32 kSub = 1u << kSubShift;
-  __shared__ float acc[kSub * D];
-  __shared__ u32 pbits[kSub / 32];  // (f.masks) dests some record reached
-  const u32 q = blockIdx.x >> 3;
-  const u32 sub = q % (u32)f.nsubt;
-  const int bucket = (int)((q / (u32)f.nsubt) * 8 + (blockIdx.x & 7));
-  if (bucket >= f.nb) return;
-  // a bucket of 2^shift dests (RedGeom) has NSUB << (shift - kRedShift) subs
-  const int shift = f.geom.shift(kRedShift);
-  if (sub >= ((u32)NSUB << (shift - kRedShift)) || bucket >= f.geom.active(shift, f.nb)) return;
-  const u64 lo = ((u64)bucket << shift) + ((u64)sub << kSubShift);
-  const u32 beg = start[bucket], end = start[bucket + 1];
-  if (beg == end) return;
-  for (u32 i = threadIdx.x; i < kSub * D; i += kRedBlock) acc[i] = 0.0f;
-  for (u32 i = threadIdx.x; i < kSub / 32; i += kRedBlock) pbits[i] = 0u;
-  __syncthreads();
-  const int lane = lane_id();
-  // block-uniform trip count: every lane takes part in the wave-level combine
-  for (u32 c0 = beg; c0 < end; c0 += kRedUnroll * kRedBlock) {
-    u64 pr[kRedUnroll];
-#pragma unroll
-    for (int u = 0; u < kRedUnroll; ++u) {
-      const u32 i = c0 + (u32)u * kRedBlock + threadIdx.x;
-      pr[u] = i < end ? sorted[i] : ~0ull;
-    }
-#pragma unroll
-    for (int u = 0; u < kRedUnroll; ++u) {
-      const u32 d = (u32)pr[u];
-      bool pending = pr[u] != ~0ull && (u64)d - lo < (u64)kSub;
-      if (f.masks && pending) atomicOr(&pbits[(d - (u32)lo) >> 5], 1u << ((d - (u32)lo) & 31));
-      float t[PS];
-      if (pending) load_row<PS>(f.rowv, (u32)(pr[u] >> 32), t);
-      // Power-law keys: a hot key's records arrive many to a wave and would
-      // serialise D LDS atomics per record on one address.  While some
-      // destination holds >= 4 of the wave's pending records, sum those
-      // across the wave and let one lane add them.
-#pragma unroll 1
-      for (int it = 0; it < 4; ++it) {
-        const unsigned long long m = __ballot(pending);
-        if (!m) break;
-        const int leader = __ffsll((long long)m) - 1;
-        const u32 dl = __shfl(d, leader);
-        const bool in = pending && d == dl;
-        if (__popcll(__ballot(in)) < 4) break;
-        float* a = acc + (dl & (kSub - 1)) * D;
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-          const float v = wave_sum(in ? t[k] : 0.0f);
-          if (lane == leader) atomicAdd(&a[k], v);
-        }
-        pending = pending && !in;
-      }
-      if (pending) {
-        float* a = acc + (d & (kSub - 1)) * D;
-#pragma unroll
-        for (int k = 0; k < D; ++k) atomicAdd(&a[k], t[k]);
-      }
-    }
-  }
-  __syncthreads();
-  const u64 d0 = lo;
-  for (u32 l = threadIdx.x; l < kSub; l += kRedBlock) {
-    const u64 dest = d0 + l;
-    float* g = f.grad + dest * PS;
-    if (f.out) {  // (one slice: dest = slot; keys of this step only reach acc)
-      bool any = false;
-#pragma unroll
-      for (int k = 0; k < D; ++k) any = any || acc[l * D + k] != 0.0f;
-      if (!any) continue;
-      const u32 o = uix(f.inv, dest);
-      if (o == 0xFFFFFFFFu) continue;
-      g = f.out + (u64)o * PS;
-    }
-    const float* w = f.wpull + (dest / (u64)f.S) * PS;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      const float v = acc[l * D + k];
-      if (v == 0.0f) continue;
-      const float wk = w[k];
-      if (wk != 0.0f) g[k] += (float)((double)v / (1.0 + (double)wk));
-    }
-  }
-  if (f.masks) {
-    __syncthreads();
-    unit_masks<kSub>(pbits, lo, (u64)f.S, f.masks, f.out ? f.inv : nullptr);
-  }
-}
-
-template <int D>
-static void launch_mvm_reduction(const FwdArgs& a, int groups, hipStream_t st) {
-  hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
-                     a.red_tot, red_geom(a), kRedShift);
-  u32* start = a.red_tot + a.red_nb + 1;
-  hipLaunchKernelGGL(k_red_scatter<1>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
-                     kMvmGroupRows, static_cast<const void*>(a.red_pairs), a.red_count,
-                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
-                     red_geom(a));
-  const int nsubt = mvm_nsub(D) * a.red_nsub;
-  const int grid = ((a.red_nb + 7) / 8) * 8 * nsubt;
-  if (a.red_out && a.S != 1)
-    throw std::runtime_error("MVM red_out: one slice");
-  MvmRedFinal f{a.grad, a.S > 1 ? a.red_masks : nullptr, a.red_out, a.red_inv, a.wpull,
-                a.red_rowv, a.S, a.red_nb, red_geom(a), nsubt};
-  hipLaunchKernelGGL(k_mvm_red_sum<D>, dim3(grid), dim3(kRedBlock), 0, st,
-                     reinterpret_cast<const u64*>(a.red_sorted), static_cast<const u32*>(start), f);
-}
-
 template <bool kGrad>
 static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.red_pairs && a.red_rowv && a.red_nb > 0 &&
                    a.red_nb <= kRedMaxBuckets;
-  if (a.red_masks && a.S > 1 && !red) throw std::runtime_error("red_masks need the MVM reduction path");
+  if (a.red_masks && a.S > 1 && !(red && a.model.v_dim >= 2))
+    throw std::runtime_error("red_masks need the MVM reduction path");
   switch (a.model.v_dim) {
 #define XF_MVM_CASE(DD)                                                                  \
   case DD: {                                                                             \
     constexpr int B = mvm_block(DD);                                                     \
     const int g = (int)((a.batch.rows + B - 1) / B);                                     \
-    if (a.red_out && !red)                                                               \
+    if (a.red_out && !(red && DD >= 2))                                                  \
       throw std::runtime_error("MVM red_out needs the bucket reduction");                \
-    if (red) {                                                                           \
+    if (red && DD >= 2) {                                                                \
       constexpr int R = kMvmGroupRows;                                                   \
       const int gr = (int)((a.batch.rows + R - 1) / R);                                  \
       hipLaunchKernelGGL((k_mvm2<DD, kGrad, false, true>), dim3(gr), dim3(R), 0, st, a); \
-      launch_mvm_reduction<DD>(a, gr, st);                                               \
+      launch_vec_reduction<(DD >= 2 ? DD - 1 : 1), true>(a, st);                          \
     } else if (agg) {                                                                    \
       hipLaunchKernelGGL((k_mvm2<DD, kGrad, true>), dim3(g), dim3(B), 0, st, a);         \
     } else {                                                                             \

@@ -150,6 +150,8 @@ struct FwdArgs {
   // unique order, dests = unique * S + s lie below red_nuq[0] * S, and the
   // unique-order outputs take dest / S directly (red_inv == null)
   const int64_t* red_nuq = nullptr;
+  // optional: the producers add the records they wrote (Engine::count_records)
+  unsigned long long* red_records = nullptr;
   int red_nsub = 1;
   // S > 1: the reduction also writes each slot's slice-presence bits
   // (red_masks[slot] |= 1 << s for every (key, slice) with an occurrence),
@@ -193,7 +195,7 @@ constexpr int kFmGroupRows = 1024;  // rows per reference-FM workgroup on the re
 // smallest rows per standard-FM producer workgroup (v_dim > 16; 256 up to
 // v_dim 10): sizes the reduction's per-workgroup histogram
 constexpr int kFmStdMinGroupRows = 128;
-constexpr int kMvmGroupRows = 512;  // rows per MVM workgroup on the reduction path (A/B: 256 -1.5 %, 1024 same)
+constexpr int kMvmGroupRows = 512;  // rows per MVM forward workgroup on the reduction path (k_mvm2: T rows)
 
 struct PullArgs {
   TableView table;

@@ -150,6 +150,10 @@ class Engine {
   // host seconds spent blocked on the monitor's run-ahead bound (the device
   // was monitor_lag steps behind): subtracted from the host's issue time
   double monitor_wait_seconds() const { return monitor_wait_s_; }
+  // gradient-reduction records written by the producers since the last call
+  // (counting on: one atomic per producer workgroup; off: -1).  Syncs.
+  void count_records(bool on);
+  int64_t take_records();
   void grow_table(int log2_cap);
   // queue a snapshot of (table size, overflow flags) behind the step's
   // work; called at the end of every training step (fused or sharded)
@@ -379,6 +383,8 @@ class Engine {
   int64_t queued_adds_ = 0;         // cumulative insert bound queued so far
   int64_t growths_ = 0, monitor_waits_ = 0;
   double monitor_wait_s_ = 0.0;
+  unsigned long long* rec_count_ = nullptr;  // (count_records) device counter
+  bool rec_on_ = false;
   int log2_cap_ = 0, max_log2_cap_ = 31;
   void poll_snapshots(int64_t wait_upto);
   void guard_inserts(int64_t n);   // before an inserting pull of <= n new keys

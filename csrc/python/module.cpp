@@ -252,6 +252,8 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_property_readonly("table_growths", &Engine::table_growths)
       .def_property_readonly("monitor_waits", &Engine::monitor_waits)
       .def_property_readonly("monitor_wait_seconds", &Engine::monitor_wait_seconds)
+      .def("count_records", &Engine::count_records)
+      .def("take_records", &Engine::take_records, py::call_guard<py::gil_scoped_release>())
       .def("grow_table", &Engine::grow_table, py::call_guard<py::gil_scoped_release>())
       .def("end_step", &Engine::end_step, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("is_gpu", &Engine::is_gpu)

@@ -333,6 +333,15 @@ class Engine:
         """Host waits of the capacity monitor (bounded run-ahead, exact-size reads)."""
         return int(self._e.monitor_waits)
 
+    def count_records(self, on: bool = True) -> None:
+        """Count the gradient-reduction records the producers write."""
+        self._e.count_records(bool(on))
+
+    def take_records(self) -> int:
+        """Records written since the last call (-1: never counted)."""
+        self._sync_stream()
+        return int(self._e.take_records())
+
     @property
     def monitor_wait_seconds(self) -> float:
         """Host seconds blocked by the monitor's run-ahead bound."""
