@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "xflow/backend.h"
+#include "xflow/reader.h"
 #include "xflow/synth.h"
 
 namespace xflow {
@@ -290,6 +291,33 @@ class CpuBackend final : public Backend {
         }
       }
     }
+  }
+
+  void parse_text(const TextParseArgs& a) override {
+    CsrBlock blk;
+    parse_libffm(a.text, (size_t)a.n, blk);
+    long long* c = a.counts;
+    c[0] = blk.rows();
+    c[1] = (long long)blk.keys.size();
+    c[2] = 0x7FFFFFFFll;
+    c[3] = 0;
+    c[4] = 0;
+    c[5] = 0;
+    const int64_t used = c[0] - c[0] % a.row_mod;
+    c[6] = blk.row_ptr[used];
+    for (int64_t i = 0; i < a.n; ++i) c[4] += a.text[i] == '\n';
+    if (a.n > 0 && a.text[a.n - 1] != '\n') ++c[4];
+    a.row_ptr[0] = 0;
+    if (c[0] > a.max_rows || c[1] > a.max_nnz) return;  // (the caller checks the counts)
+    for (int64_t r = 0; r < blk.rows(); ++r) {
+      a.labels[r] = blk.labels[r];
+      a.row_ptr[r + 1] = blk.row_ptr[r + 1];
+      const long long len = blk.row_ptr[r + 1] - blk.row_ptr[r];
+      c[2] = std::min<long long>(c[2], len);
+      c[3] = std::max<long long>(c[3], len);
+    }
+    std::copy(blk.keys.begin(), blk.keys.end(), a.keys);
+    std::copy(blk.fgid.begin(), blk.fgid.end(), a.fgid);
   }
 
   void slice_masks(const BatchView& b, const u32* pos, u32* tmask) override {

@@ -154,6 +154,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       red_count_ = balloc<u32>(be, groups);
       // MVM: T = loss*M per row; standard FM: (loss, loss*vs) per row (k_fm_std_fwd)
       if (mvm || fm_std) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
+      if (mvm) {
+        red_vmax_ = balloc<u32>(be, 2);
+        be.memset(red_vmax_, 0, 2 * sizeof(u32));
+      }
     }
   }
   // reference-math FM with the GPU reduction: compact (w, Σv, Σv^2, 0) value rows
@@ -184,7 +188,7 @@ Engine::~Engine() {
                   host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_, row_grad_,
-                  lr_mask_, fm_w_, rec_count_};
+                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
   for (SrvBuf& b : srv_) {
@@ -244,6 +248,40 @@ bool Engine::reduction_masks() const {
          (cfg_.model.kind == kMVM && red_rowv_ != nullptr);
 }
 
+std::vector<int64_t> Engine::parse_text(const char* text, int64_t n, u64* keys, int32_t* fgid,
+                                        int32_t* row_ptr, float* labels, int64_t max_rows,
+                                        int64_t max_nnz, int64_t row_mod) {
+  const int64_t need = text_ws_words(n);
+  if (need > text_ws_words_) {
+    be_->synchronize();
+    be_->free(text_ws_);
+    text_ws_words_ = need + need / 4;
+    text_ws_ = balloc<u32>(*be_, (size_t)text_ws_words_);
+  }
+  if (!text_counts_) text_counts_ = balloc<long long>(*be_, 8);
+  TextParseArgs a;
+  a.text = text;
+  a.n = n;
+  a.keys = keys;
+  a.fgid = fgid;
+  a.row_ptr = row_ptr;
+  a.labels = labels;
+  a.max_rows = max_rows;
+  a.max_nnz = max_nnz;
+  a.max_lines = text_max_lines(n);
+  a.ws = text_ws_;
+  a.ws_words = text_ws_words_;
+  a.row_mod = row_mod;
+  a.counts = text_counts_;
+  be_->parse_text(a);
+  long long c[7];
+  be_->copy_d2h(c, text_counts_, sizeof(c));
+  if (c[5]) throw std::runtime_error("parse_text: more lines than n/2 + 2 (a block of empty lines?)");
+  if (c[0] > max_rows || c[1] > max_nnz)
+    throw std::runtime_error("parse_text: the block holds more rows / features than the arrays");
+  return {c[0], c[1], c[0] > 0 ? c[2] : 0, c[3], c[6]};
+}
+
 void Engine::count_records(bool on) {
   if (on && !rec_count_) {
     rec_count_ = balloc<unsigned long long>(*be_, 1);
@@ -264,6 +302,11 @@ void Engine::set_reduction(FwdArgs& fa) const {
   fa.trash_pos = (u32)scratch_.cap;
   if (!red_pairs_) return;
   if (rec_on_) fa.red_records = rec_count_;
+  if (red_vmax_) {  // (MVM: two alternating words, see FwdArgs::red_vmax)
+    fa.red_vmax = red_vmax_ + vmax_parity_;
+    fa.red_vmax_next = red_vmax_ + (vmax_parity_ ^ 1);
+    vmax_parity_ ^= 1;
+  }
   fa.red_bcap = bcap_;
   fa.red_cap = scratch_.cap;
   fa.red_nsub = red_nsub_;
@@ -457,7 +500,8 @@ void Engine::train_step(const BatchView& b) {
   // S = 8 +1.9 %, LR S = 8 +0.8 %) and for standard FM (+10.5 %), a loss for
   // one-slice LR (-5.1 %), MVM (-3.5 %) and reference FM (-1.4 %).
   const bool upos = be_->remaps_positions() && red_pairs_ &&
-                    (Sf > 1 || (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard));
+                    (Sf > 1 || cfg_.model.kind == kMVM ||
+                     (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard));
   if (upos) ensure_inv();
   dedup_(b, 1, nullptr, upos || lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)

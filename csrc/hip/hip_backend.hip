@@ -183,6 +183,7 @@ class HipBackend final : public Backend {
   void slice_masks(const BatchView& b, const u32* pos, u32* tmask) override {
     hip::launch_slice_masks(b, pos, tmask, stream_);
   }
+  void parse_text(const TextParseArgs& a) override { hip::launch_parse_text(a, stream_); }
   bool remaps_positions() const override { return true; }
   void remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none) override {
     hip::launch_remap_pos(pos, nnz, inv, none, stream_);

@@ -111,6 +111,11 @@ __device__ __forceinline__ int wave_max(int v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
   return v;
 }
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
 
 // Block-wide exclusive scan of one value per lane; returns the exclusive
 // prefix and writes the block total to *total.
@@ -194,6 +199,28 @@ template <int FX>
 __device__ __forceinline__ double fx_to_double(long long a) {
   return (double)a * (1.0 / (double)(1ull << FX));
 }
+// Fixed point with a per-step scale (MVM's T = loss*M: a product over
+// fields, no static range fits): the step's largest |input| (vmax, float
+// bits, found by the forward) sets 2^fx so that 2^18 inputs of that size
+// still sum inside int64 -- resolution vmax * 2^-44, i.e. float's relative
+// precision on the largest values and deterministic, order-free sums.
+__device__ __forceinline__ int fx_scale_bits(const u32* vmax) {
+  int e = 0;
+  const float m = vmax ? __uint_as_float(*vmax) : 0.0f;
+  if (m > 0.0f && m == m && m <= 3.0e38f) frexpf(m, &e);
+  const int fx = 44 - e;
+  return fx < 0 ? 0 : (fx > 60 ? 60 : fx);
+}
+__device__ __forceinline__ long long fx_from_rt(float v, int fx) {
+  const double d = ldexp((double)v, fx);
+  // (a non-finite or out-of-range input -- a diverged step, flagged by the
+  // forward -- converts to 0 instead of an undefined int64 conversion)
+  return (d == d && fabs(d) < 4.6e18) ? (long long)__builtin_rint(d) : 0ll;
+}
+__device__ __forceinline__ double fx_to_double_rt(long long a, int fx) {
+  return ldexp((double)a, -fx);
+}
+
 template <int NV>
 struct FxBits {
   static constexpr int kFx = NV == 1 ? 36 : 32;

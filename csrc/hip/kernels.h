@@ -51,6 +51,9 @@ void launch_field_major(const void* src, void* dst, int64_t rows, int F, int ele
 void launch_forward_backward(const FwdArgs& a, hipStream_t st);
 void launch_slice_masks(const BatchView& b, const u32* pos, u32* tmask, hipStream_t st);
 
+// kernels_parse.hip
+void launch_parse_text(const TextParseArgs& a, hipStream_t st);
+
 // kernels_eval.hip
 void launch_eval_metrics(const float* pctr, const float* labels, int64_t n, EvalMetrics* out,
                          hipStream_t st);

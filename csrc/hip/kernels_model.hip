@@ -1093,19 +1093,19 @@ constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128);
 // kernel's LDS tables leave a CU two waves per SIMD for the row gathers), which
 // left (loss, loss*vs_k) per row in red_rowv -- the same floats the fused form
 // computes here, so both forms sum identical fixed-point values.
-// kFloat (MVM): float sums instead of fixed point -- MVM's T = loss*M spans
-// many orders of magnitude (a product over fields), beyond any one int64
-// fixed-point scale; the sums are then order-dependent in the last bits.
-template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kFloat = false>
+// kScaled (MVM): T = loss*M spans many orders of magnitude (a product over
+// fields), beyond any one static fixed-point scale: the int64 sums use the
+// step's scale (fx_scale_bits of FwdArgs::red_vmax, set by the forward).
+template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kScaled = false>
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int NV = 1 + D;
   constexpr int LOG2 = ilog2c(2 * BLOCK);
   constexpr int kSlots = 1 << LOG2;
   constexpr int kFx = FxBits<1>::kFx;
-  using Acc = typename std::conditional<kFloat, float, long long>::type;
   __shared__ u64 s_tag[1][kSlots];
-  __shared__ Acc s_acc[1][kSlots * NV];
+  __shared__ long long s_acc[1][kSlots * NV];
+  const int fxs = kScaled ? fx_scale_bits(a.red_vmax) : kFx;
   __shared__ unsigned short s_list[1][BLOCK];
   __shared__ u32 s_hist[kRedMaxBuckets];
   __shared__ u32 s_off[kSeg ? kRedMaxBuckets : 1];
@@ -1129,7 +1129,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   for (int i = threadIdx.x; i < kSlots; i += BLOCK) {
     s_tag[0][i] = ~0ull;
 #pragma unroll
-    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = (Acc)0;
+    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = 0ll;
   }
   for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) s_hist[i] = 0u;
   if (threadIdx.x < 3) s_nlist[threadIdx.x] = 0u;
@@ -1246,9 +1246,9 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     const bool has = pj != a.trash_pos;
     bool claimed = false;
     u32 h = 0;
-    Acc vals[NV];
+    long long vals[NV];
 #pragma unroll
-    for (int c = 0; c < NV; ++c) vals[c] = (Acc)0;
+    for (int c = 0; c < NV; ++c) vals[c] = 0ll;
     if (has) {
       const u32 dest = pj * S + sl;
       const u64 key = ((u64)(u32)j << 32) | dest;
@@ -1271,10 +1271,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       // C_k = Σ loss*vs_k (v_k is the key's pulled value, one per step), so the
       // column walk needs no second gather of the pulled row; k_red_sum_vec
       // expands C - v*B once per dest
-      if constexpr (kFloat) {
-        vals[0] = loss;
+      if constexpr (kScaled) {  // (kSplit: the row's vector, |.| <= the step's vmax)
+        vals[0] = fx_from_rt(loss, fxs);
 #pragma unroll
-        for (int k = 0; k < D; ++k) vals[1 + k] = vs[k];  // (kSplit: the row's vector)
+        for (int k = 0; k < D; ++k) vals[1 + k] = fx_from_rt(vs[k], fxs);
       } else {
         vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
 #pragma unroll
@@ -1283,12 +1283,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       }
     }
     if (has) {
-      Acc* acc = &s_acc[t][h * NV];
+      long long* acc = &s_acc[t][h * NV];
 #pragma unroll
-      for (int c = 0; c < NV; ++c) {
-        if constexpr (kFloat) atomicAdd(&acc[c], vals[c]);
-        else atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)vals[c]);
-      }
+      for (int c = 0; c < NV; ++c)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)vals[c]);
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -1307,10 +1305,9 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       wv[0] = d;
 #pragma unroll
       for (int c = 0; c < NV; ++c) {
-        Acc* ap = &s_acc[t][hh * NV + c];
-        if constexpr (kFloat) wv[1 + c] = __float_as_uint(*ap);
-        else wv[1 + c] = __float_as_uint((float)fx_to_double<kFx>(*ap));
-        *ap = (Acc)0;
+        long long* ap = &s_acc[t][hh * NV + c];
+        wv[1 + c] = __float_as_uint((float)fx_to_double_rt(*ap, fxs));
+        *ap = 0ll;
       }
 #pragma unroll
       for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
@@ -1374,7 +1371,8 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
                                                            const u32* __restrict__ inv,
                                                            const float* __restrict__ wpull,
                                                            int S, SegSrc sg,
-                                                           u32* __restrict__ masks) {
+                                                           u32* __restrict__ masks,
+                                                           const u32* __restrict__ vmax) {
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
@@ -1382,8 +1380,9 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   constexpr int kFx = FxBits<1>::kFx;
   constexpr int W = vec_rec_words(NV);
   using Rec = typename VecRedRec<NV>::T;
-  using Acc = typename std::conditional<kMvm, float, long long>::type;  // (k_fm_std_red kFloat)
-  __shared__ Acc acc[kR * NV];
+  __shared__ long long acc[kR * NV];
+  // MVM: the step's fixed-point scale (k_fm_std_red kScaled)
+  const int fxs = kMvm ? fx_scale_bits(vmax) : kFx;
   __shared__ u32 seen[kR / 32];
   __shared__ u32 s_pre[kSeg ? G : 1];
   __shared__ u32 s_seg[kSeg ? G : 1];
@@ -1403,7 +1402,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
     }
     if (beg == end) continue;  // (block-uniform)
     const u64 lo = ((u64)bk << shift) + ((u64)sub << kShift);
-    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = (Acc)0;
+    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
     for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) seen[i] = 0u;
     if constexpr (kSeg) {
       // segment g: records [s_pre[g], s_pre[g+1]) of the bucket, at s_seg[g] + i
@@ -1439,13 +1438,11 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
         wv[4 * q + 2] = r.q[q].z;
         wv[4 * q + 3] = r.q[q].w;
       }
-      Acc* ap = acc + l * NV;
+      long long* ap = acc + l * NV;
 #pragma unroll
-      for (int c = 0; c < NV; ++c) {
-        if constexpr (kMvm) atomicAdd(&ap[c], __uint_as_float(wv[1 + c]));
-        else atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
-                       (unsigned long long)fx_from<kFx>(__uint_as_float(wv[1 + c])));
-      }
+      for (int c = 0; c < NV; ++c)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
+                  (unsigned long long)fx_from_rt(__uint_as_float(wv[1 + c]), fxs));
       atomicOr(&seen[l >> 5], 1u << (l & 31));
     }
     lds_barrier();
@@ -1462,14 +1459,14 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
         const float* w = wpull + slot * PS;
 #pragma unroll
         for (int c = 0; c < NV; ++c) {
-          const float t = acc[l * NV + c];
+          const long long t = acc[l * NV + c];
           const float wk = w[c];
-          if (t != 0.0f && wk != 0.0f) row[c] += (float)((double)t / (1.0 + (double)wk));
+          if (t != 0 && wk != 0.0f) row[c] += (float)(fx_to_double_rt(t, fxs) / (1.0 + (double)wk));
         }
         continue;
       }
       // (B, C_0..C_{D-1}) -> g_w = B, g_v[k] = C_k - v_k*B (k_fm_std_red)
-      const double B = fx_to_double<kFx>(acc[l * NV]);
+      const double B = fx_to_double_rt(acc[l * NV], fxs);
       const float4* v4 = reinterpret_cast<const float4*>(wpull + ((lo + l) / (u64)S) * PS);
       float o[PS];
 #pragma unroll
@@ -1483,7 +1480,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
       o[0] = (float)B;
 #pragma unroll
       for (int c = 1; c < PS; ++c)
-        o[c] = c < NV ? (float)(fx_to_double<kFx>(acc[l * NV + c]) - (double)o[c] * B) : 0.0f;
+        o[c] = c < NV ? (float)(fx_to_double_rt(acc[l * NV + c], fxs) - (double)o[c] * B) : 0.0f;
       float* row = grad + (lo + l) * PS;
       if (out) {  // the unique-order row (FwdArgs::red_out); S > 1: [unique][slice]
         const u64 slot = (lo + l) / (u64)S;
@@ -1567,7 +1564,8 @@ template <int D, bool kMvm = false>
 static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   constexpr int BLOCK = fmstd_block(D);
   constexpr int NV = 1 + D;
-  if (kMvm && !a.red_rowv) throw std::runtime_error("MVM vector reduction needs red_rowv");
+  if (kMvm && (!a.red_rowv || !a.red_vmax))
+    throw std::runtime_error("MVM vector reduction needs red_rowv and red_vmax");
   const int groups = (int)((a.batch.rows + BLOCK - 1) / BLOCK);
   const RedGeom geom = red_geom(a);
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
@@ -1593,11 +1591,11 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
       const u32 grid2 = std::min<u32>((u32)(a.red_nb * a.red_nsub), 2u * (u32)device_cus());
       hipLaunchKernelGGL((k_red_sum_vec<D, true, 512, kMvm>), dim3(grid2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks);
+                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax);
     } else {
       hipLaunchKernelGGL((k_red_sum_vec<D, true, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks);
+                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax);
     }
     return;
   }
@@ -1612,7 +1610,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
                      geom);
   hipLaunchKernelGGL((k_red_sum_vec<D, false, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
-                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks);
+                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks, a.red_vmax);
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
@@ -2021,10 +2019,31 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
       // divides once.  Rows with a repeated field (S = field sum): global
       // atomics, and T = 0 (their occurrences still leave records, for the
       // slice bits of a multi-slice step).
+      float tmax = 0.0f;  // |T| of the row (the step's fixed-point scale)
       if (active) {
         float* t = a.red_rowv + (size_t)r * PS;
 #pragma unroll
-        for (int k = 0; k < PS; ++k) t[k] = (!dup && k < D) ? loss * M[k] : 0.0f;
+        for (int k = 0; k < PS; ++k) {
+          const float v = (!dup && k < D) ? loss * M[k] : 0.0f;
+          t[k] = v;
+          // (a non-finite T maxes to inf: fx_scale_bits then keeps the
+          // static 2^44 scale and the clamp flags the step)
+          tmax = fmaxf(tmax, v == v ? fabsf(v) : INFINITY);
+        }
+      }
+      {
+        __shared__ float s_tmax[BLOCK / kWave];
+        tmax = wave_max(tmax);
+        if (threadIdx.x % kWave == 0) s_tmax[threadIdx.x / kWave] = tmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          float m = 0.0f;
+#pragma unroll
+          for (int w = 0; w < BLOCK / kWave; ++w) m = fmaxf(m, s_tmax[w]);
+          if (m > 0.0f) atomicMax(a.red_vmax, __float_as_uint(m));  // (>= 0: bits order as values)
+          if (!(m <= 3.0e38f)) atomicOr(a.fx_bad, 2u);  // non-finite T: a diverged model
+          if (blockIdx.x == 0) *a.red_vmax_next = 0u;  // (the next step's word)
+        }
       }
       if (active && dup) {
         for (int j = 0; j < len; ++j) {

@@ -152,6 +152,11 @@ struct FwdArgs {
   const int64_t* red_nuq = nullptr;
   // optional: the producers add the records they wrote (Engine::count_records)
   unsigned long long* red_records = nullptr;
+  // MVM's per-step fixed-point scale: the forward atomically maxes |T| into
+  // red_vmax[0] (float bits) and clears red_vmax_next for the next step (two
+  // alternating words); the vector reduction scales its int64 sums by it
+  u32* red_vmax = nullptr;
+  u32* red_vmax_next = nullptr;
   int red_nsub = 1;
   // S > 1: the reduction also writes each slot's slice-presence bits
   // (red_masks[slot] |= 1 << s for every (key, slice) with an occurrence),
@@ -248,6 +253,35 @@ struct OwnerGroupArgs {
   SrcGroups g;                 // nsrc, epoch, offs
   u32* overflow = nullptr;
 };
+
+// libffm text -> CSR batch on the device (Backend::parse_text; HIP:
+// kernels_parse.hip, CPU: reader.cpp's parser).  Rules of reader.cpp.
+struct TextParseArgs {
+  const char* text = nullptr;      // block bytes (backend memory, 16-byte aligned)
+  int64_t n = 0;
+  u64* keys = nullptr;             // [max_nnz]
+  int32_t* fgid = nullptr;         // [max_nnz]
+  int32_t* row_ptr = nullptr;      // [max_rows + 1]
+  float* labels = nullptr;         // [max_rows]
+  int64_t max_rows = 0, max_nnz = 0;
+  int64_t max_lines = 0;           // text_max_lines(n)
+  u32* ws = nullptr;               // text_ws_words(n) words of workspace
+  int64_t ws_words = 0;
+  // rows the caller will use: the first rows - rows % row_mod (the slicing
+  // rule, lr_worker.cc:190); counts[6] = their occurrences
+  int64_t row_mod = 1;
+  // backend [7]: rows, occurrences, shortest / longest row, lines, line
+  // overflow, occurrences of the used rows (nothing is written past max_rows
+  // / max_nnz: the caller checks)
+  long long* counts = nullptr;
+};
+// lines of n bytes: at most n/2 + 2 ("x\n" per line; a block of mostly empty
+// lines overflows the workspace and is flagged)
+XF_HD int64_t text_max_lines(int64_t n) { return n / 2 + 2; }
+XF_HD int64_t text_ws_words(int64_t n) {
+  const int64_t L = text_max_lines(n), nwg = (n + 4095) / 4096;
+  return ((nwg + 3) & ~3ll) + ((L + 1 + 3) & ~3ll) + 2 * L + 2 * (L / 1024 + 2);
+}
 
 // A step's capacity snapshot (Engine's monitor) in coherent pinned host
 // memory, packed into ONE 64-bit word so a single store publishes it whole:
@@ -445,6 +479,8 @@ class Backend {
   // pos[i] = inv[pos[i]] for i < nnz (scratch slot -> unique-list index; the
   // trash slot's occurrences get `none`): the fused step's unique-index
   // positions (FwdArgs::red_nuq).  HIP only (the compaction writes inv).
+  // libffm text -> CSR (see TextParseArgs); counts stay in backend memory
+  virtual void parse_text(const TextParseArgs& a) = 0;
   virtual bool remaps_positions() const { return false; }
   virtual void remap_pos(u32* pos, int64_t nnz, const u32* inv, u32 none) {
     (void)pos, (void)nnz, (void)inv, (void)none;

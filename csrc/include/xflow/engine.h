@@ -202,6 +202,15 @@ class Engine {
   void save(const std::string& path);
   void load(const std::string& path);
 
+  // libffm text block (backend memory, 16-byte aligned) -> CSR arrays in
+  // backend memory, on the device (Backend::parse_text).  Returns {rows,
+  // occurrences, shortest row, longest row, occurrences of the first rows -
+  // rows % row_mod rows}; syncs once (the counts).  Throws when the block
+  // holds more rows / occurrences than the arrays (max_rows / max_nnz).
+  std::vector<int64_t> parse_text(const char* text, int64_t n, u64* keys, int32_t* fgid,
+                                  int32_t* row_ptr, float* labels, int64_t max_rows,
+                                  int64_t max_nnz, int64_t row_mod = 1);
+
   // Synthetic Criteo-shaped batch into engine-owned staging buffers.
   BatchView synth_batch(const SynthArgs& a, int64_t slice_rows);
   // Copy a host CSR batch into engine-owned staging buffers.
@@ -384,6 +393,11 @@ class Engine {
   int64_t growths_ = 0, monitor_waits_ = 0;
   double monitor_wait_s_ = 0.0;
   unsigned long long* rec_count_ = nullptr;  // (count_records) device counter
+  u32* red_vmax_ = nullptr;                   // MVM: per-step fixed-point scale words [2]
+  u32* text_ws_ = nullptr;                    // parse_text workspace
+  int64_t text_ws_words_ = 0;
+  long long* text_counts_ = nullptr;          // parse_text counts [7]
+  mutable int vmax_parity_ = 0;
   bool rec_on_ = false;
   int log2_cap_ = 0, max_log2_cap_ = 31;
   void poll_snapshots(int64_t wait_upto);

@@ -252,6 +252,17 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_property_readonly("table_growths", &Engine::table_growths)
       .def_property_readonly("monitor_waits", &Engine::monitor_waits)
       .def_property_readonly("monitor_wait_seconds", &Engine::monitor_wait_seconds)
+      .def("parse_text",
+           [](Engine& e, uintptr_t text, int64_t n, uintptr_t keys, uintptr_t fgid,
+              uintptr_t row_ptr, uintptr_t labels, int64_t max_rows, int64_t max_nnz,
+              int64_t row_mod) {
+             return e.parse_text(P<const char>(text), n, P<u64>(keys), P<int32_t>(fgid),
+                                 P<int32_t>(row_ptr), P<float>(labels), max_rows, max_nnz,
+                                 row_mod);
+           },
+           py::arg("text"), py::arg("n"), py::arg("keys"), py::arg("fgid"), py::arg("row_ptr"),
+           py::arg("labels"), py::arg("max_rows"), py::arg("max_nnz"), py::arg("row_mod") = 1,
+           py::call_guard<py::gil_scoped_release>())
       .def("count_records", &Engine::count_records)
       .def("take_records", &Engine::take_records, py::call_guard<py::gil_scoped_release>())
       .def("grow_table", &Engine::grow_table, py::call_guard<py::gil_scoped_release>())

@@ -16,7 +16,7 @@ for m in "${MLIST[@]}"; do
   f=$(find $d -name "*kernel_stats.csv" | head -1)
   cp "$f" gpurun_out/${TAG}_${i}_kernel_stats.csv
   echo "== $m"
-  tail -1 $d.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e6,1), 'M samples/s', round(d['ms_per_step'],3), 'ms/step')"
+  grep '^{' $d.log | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value']/1e6,1), 'M samples/s', round(d['ms_per_step'],3), 'ms/step', 'records/step', d.get('reduction_records_per_step'), 'logloss', round(d['logloss'],4))"
   python3 - "$f" <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))

@@ -59,6 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="fixed table capacity: an overflow raises within two steps")
     ap.add_argument("--train-block-bytes", type=int, default=2 << 20)
     ap.add_argument("--test-block-bytes", type=int, default=0)
+    ap.add_argument("--gpu-parse", action="store_true",
+                    help="tokenise libffm text on the GPU (raw blocks uploaded; keys, labels and "
+                         "field ids bit-equal to the host parser)")
     ap.add_argument("--resident", action="store_true",
                     help="keep the training shard in HBM after the first epoch (no re-read)")
     ap.add_argument("--csr-only", action="store_true",
@@ -90,7 +93,7 @@ def config_from_args(a) -> TrainConfig:
     return TrainConfig(
         train_prefix=a.train_prefix, test_prefix=a.test_prefix, epochs=a.epochs,
         threads=a.threads, train_block_bytes=a.train_block_bytes, block_rows=a.block_rows,
-        resident=a.resident, fixed_width=not a.csr_only,
+        resident=a.resident, fixed_width=not a.csr_only, gpu_parse=a.gpu_parse,
         test_block_bytes=a.test_block_bytes, serial_slices=a.serial_slices,
         keep_remainder=a.keep_remainder, mvm_predict_compat=a.mvm_predict_compat,
         init_push=not a.no_init_push, pred_dir=a.pred_dir, write_pred=not a.no_pred_file,

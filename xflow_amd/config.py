@@ -112,6 +112,7 @@ class TrainConfig:
     fixed_width: bool = True     # blocks whose rows all hold F features train field-major
     resident: bool = False       # keep the first epoch's device batches in HBM for the rest
     copy_threads: int = 8        # host threads staging a block into pinned memory
+    gpu_parse: bool = False      # libffm text shards tokenised on the GPU (data/textstream.py)
     test_block_bytes: int = 0    # 0 => 4 MB LR, 2 MB FM/MVM
     serial_slices: bool = False
     keep_remainder: bool = False

@@ -333,6 +333,17 @@ class Engine:
         """Host waits of the capacity monitor (bounded run-ahead, exact-size reads)."""
         return int(self._e.monitor_waits)
 
+    def parse_text(self, text: torch.Tensor, n: int, out: dict, row_mod: int = 1):
+        """libffm bytes text[:n] (uint8, engine device, 16-byte aligned) ->
+        out["keys"/"fgid"/"row_ptr"/"labels"] on the device (kernels_parse.hip;
+        reader.cpp's rules).  Returns (rows, occurrences, shortest row,
+        longest row, occurrences of the first rows - rows % row_mod rows)."""
+        self._sync_stream()
+        return tuple(int(x) for x in self._e.parse_text(
+            text.data_ptr(), int(n), out["keys"].data_ptr(), out["fgid"].data_ptr(),
+            out["row_ptr"].data_ptr(), out["labels"].data_ptr(), int(out["labels"].numel()),
+            int(out["keys"].numel()), int(row_mod)))
+
     def count_records(self, on: bool = True) -> None:
         """Count the gradient-reduction records the producers write."""
         self._e.count_records(bool(on))

@@ -38,6 +38,7 @@ from xflow_amd import checkpoint
 from xflow_amd import native as _native
 from xflow_amd.config import TrainConfig, model_kind
 from xflow_amd.data import binfmt
+from xflow_amd.data.textstream import TextStream
 from xflow_amd.data.upload import BlockStream
 from xflow_amd.engine import Batch, Engine, widen_keys
 from xflow_amd.metrics import MetricsLogger, reference_auc
@@ -143,8 +144,14 @@ class Trainer:
                      fgid=fgid, slice_rows=slice_rows)
 
     def _device_batch(self, blk: dict, used: int, slice_rows: int) -> Batch:
-        """Batch over a block already on the device (data.upload.BlockStream)."""
-        nnz = int(blk["row_ptr_host"][used])
+        """Batch over a block already on the device (data.upload.BlockStream,
+        or data.textstream.TextStream: its parse counted the used rows' nnz)."""
+        if "row_ptr_host" in blk:
+            nnz = int(blk["row_ptr_host"][used])
+        else:
+            if used != blk["rows"] - blk["rows"] % (1 if self.cfg.keep_remainder else self.threads):
+                raise ValueError("text-stream block: used rows differ from the parse's")
+            nnz = int(blk["nnz_used"])
         fgid = blk["fgid"][:nnz] if self._with_fgid else None
         F = blk["nnz_per_row"] if self.cfg.fixed_width else 0
         if F:
@@ -222,10 +229,23 @@ class Trainer:
                 nxt = lambda: next(blocks, None)  # noqa: E731
             else:
                 xfb = binfmt.shard_file(path)
+                gpu_text = (cfg.gpu_parse and not xfb and self.device.type == "cuda"
+                            and self.concurrent)
                 reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
+                          else None if gpu_text
                           else nat.PrefetchReader(path, cfg.train_block_bytes))
-                nxt = reader.next
-                if self.device.type == "cuda" and self.concurrent:
+                if gpu_text:
+                    # libffm text tokenised on the GPU (data/textstream.py):
+                    # the reference's blocks, parsed where they are trained
+                    tl = (StreamTimeline(self.device)
+                          if os.environ.get("XFLOW_STREAM_TIMELINE") else None)
+                    stream = TextStream(self.engine, path, cfg.train_block_bytes,
+                                        row_mod=1 if cfg.keep_remainder else self.threads,
+                                        timeline=tl)
+                    nxt = stream.next
+                else:
+                    nxt = reader.next
+                if reader is not None and self.device.type == "cuda" and self.concurrent:
                     # XFLOW_STREAM_TIMELINE=1: H2D vs step intervals from HIP
                     # events, reported in the epoch record (overlap evidence)
                     tl = (StreamTimeline(self.device)
