@@ -181,6 +181,34 @@ __device__ __forceinline__ u64 std_hash_bytes(const char* __restrict__ p, int64_
   return shift_mix(h);
 }
 
+// Sequential reader of a line's bytes from aligned 16-byte chunks held in
+// registers, the next chunk loaded one ahead: a lane scanning its line byte by
+// byte waits on one load per 16 bytes (latency hidden by the look-ahead)
+// instead of one dependent byte load per byte.  Reads stay inside the text
+// allocation: callers give >= 32 bytes of allocation beyond the block.
+struct ByteStream {
+  const char* __restrict__ t;
+  int64_t base;  // 16-byte aligned offset of cur
+  uint4 cur, nxt;
+  __device__ __forceinline__ void start(const char* __restrict__ text, int64_t i) {
+    t = text;
+    base = i & ~(int64_t)15;
+    cur = *reinterpret_cast<const uint4*>(t + base);
+    nxt = *reinterpret_cast<const uint4*>(t + base + 16);
+  }
+  // byte i (i >= the previous i: sequential, forward)
+  __device__ __forceinline__ char at(int64_t i) {
+    while (i >= base + 16) {
+      base += 16;
+      cur = nxt;
+      nxt = *reinterpret_cast<const uint4*>(t + base + 16);
+    }
+    const int o = (int)(i - base);
+    const u32 w = o < 8 ? (o < 4 ? cur.x : cur.y) : (o < 12 ? cur.z : cur.w);
+    return (char)(w >> ((o & 3) * 8));
+  }
+};
+
 // [start, end) of line l (end: its '\n' or the text end)
 __device__ __forceinline__ void line_span(const u32* __restrict__ line_end, int64_t l,
                                           int64_t& s, int64_t& e) {
@@ -188,12 +216,6 @@ __device__ __forceinline__ void line_span(const u32* __restrict__ line_end, int6
   e = line_end[l];
 }
 
-__device__ __forceinline__ int64_t find_char(const char* __restrict__ t, int64_t b, int64_t e,
-                                             char c) {
-  for (int64_t i = b; i < e; ++i)
-    if (t[i] == c) return i;
-  return -1;
-}
 
 // row flag << 40 | feature tokens of each line
 constexpr int kTokBits = 40;
@@ -209,20 +231,27 @@ __global__ void __launch_bounds__(kPBlock) k_line_count(const char* __restrict__
   if (l >= nl) return;
   int64_t s, e;
   line_span(line_end, l, s, e);
-  const int64_t tab = find_char(text, s, e, '\t');
-  if (tab < 0) {
-    lv[l] = 0ull;
-    return;
-  }
+  // one forward pass: the first TAB starts the tokens; a token (a run
+  // between ' ') counts when it holds a ':'
+  ByteStream bs;
+  bs.start(text, s);
+  bool row = false, colon = false;
   unsigned long long tok = 0;
-  int64_t q = tab + 1;
-  while (q < e) {
-    int64_t te = find_char(text, q, e, ' ');
-    if (te < 0) te = e;
-    if (te > q && find_char(text, q, te, ':') >= 0) ++tok;
-    q = te + 1;
+  for (int64_t i = s; i < e; ++i) {
+    const char c = bs.at(i);
+    if (!row) {
+      row = c == '\t';
+      continue;
+    }
+    if (c == ' ') {
+      tok += colon;
+      colon = false;
+    } else {
+      colon |= c == ':';
+    }
   }
-  lv[l] = (1ull << kTokBits) | tok;
+  tok += colon;
+  lv[l] = row ? ((1ull << kTokBits) | tok) : 0ull;
 }
 
 // exclusive scan of n u64 values in place: per-workgroup totals, one
@@ -327,26 +356,32 @@ __global__ void __launch_bounds__(kPBlock) k_line_emit(const char* __restrict__ 
     const int64_t o0 = o;
     int64_t s, e;
     line_span(line_end, l, s, e);
-    const int64_t tab = find_char(text, s, e, '\t');
-    a.labels[row] = dev_atof(text + s, text + tab) > 0.0000001 ? 1.0f : 0.0f;
-    int64_t q = tab + 1;
-    while (q < e) {
-      int64_t te = find_char(text, q, e, ' ');
-      if (te < 0) te = e;
-      if (te > q) {
-        const int64_t c1 = find_char(text, q, te, ':');
-        if (c1 >= 0) {
-          const int64_t fb = c1 + 1;
-          const int64_t c2 = find_char(text, fb, te, ':');
-          int64_t fe = c2 >= 0 ? c2 : te;
-          if (c2 < 0)
-            while (fe > fb && text[fe - 1] == '\r') --fe;  // 2-part token at a CRLF line end
-          a.fgid[o] = (int32_t)dev_atof(text + q, text + c1);
-          a.keys[o] = std_hash_bytes(text + fb, fe - fb);
-          ++o;
-        }
+    ByteStream bs;
+    bs.start(text, s);
+    int64_t i = s;
+    while (i < e && bs.at(i) != '\t') ++i;  // (a row: there is a TAB)
+    a.labels[row] = dev_atof(text + s, text + i) > 0.0000001 ? 1.0f : 0.0f;
+    // token [q, i) at each ' ' / the line end: its first ':' (c1) and second (c2)
+    int64_t q = ++i, c1 = -1, c2 = -1;
+    for (; i <= e; ++i) {
+      const char c = i < e ? bs.at(i) : ' ';
+      if (c == ':') {
+        if (c1 < 0) c1 = i;
+        else if (c2 < 0) c2 = i;
+        continue;
       }
-      q = te + 1;
+      if (c != ' ') continue;
+      if (c1 >= 0) {  // a feature token (empty tokens have no ':')
+        const int64_t fb = c1 + 1;
+        int64_t fe = c2 >= 0 ? c2 : i;
+        if (c2 < 0)
+          while (fe > fb && text[fe - 1] == '\r') --fe;  // 2-part token at a CRLF line end
+        a.fgid[o] = (int32_t)dev_atof(text + q, text + c1);
+        a.keys[o] = std_hash_bytes(text + fb, fe - fb);
+        ++o;
+      }
+      q = i + 1;
+      c1 = c2 = -1;
     }
     a.row_ptr[row + 1] = (int32_t)o;
     const long long rows = a.counts[0];

@@ -257,7 +257,7 @@ struct OwnerGroupArgs {
 // libffm text -> CSR batch on the device (Backend::parse_text; HIP:
 // kernels_parse.hip, CPU: reader.cpp's parser).  Rules of reader.cpp.
 struct TextParseArgs {
-  const char* text = nullptr;      // block bytes (backend memory, 16-byte aligned)
+  const char* text = nullptr;      // block bytes (backend memory, 16-byte aligned, allocated >= n + 32)
   int64_t n = 0;
   u64* keys = nullptr;             // [max_nnz]
   int32_t* fgid = nullptr;         // [max_nnz]

@@ -77,11 +77,14 @@ def gen_file(tmp_path_factory):
     return p
 
 
-def test_text_blocks_protocol_matches_block_reader(gen_file):
-    """Block boundaries (and the carried tails) equal BlockReader's."""
+@pytest.mark.parametrize("threads", [1, 4])
+def test_text_blocks_protocol_matches_block_reader(gen_file, threads, monkeypatch):
+    """Block boundaries (and the carried tails) equal BlockReader's, with
+    one reader or parallel positional reads of small pieces."""
+    monkeypatch.setattr(TextBlocks, "min_piece", 1000)
     for bb in (4096, 65536, 1 << 20):
         want = [len(b["labels"]) for b in _host_blocks(gen_file, bb)]
-        tb = TextBlocks(gen_file, bb)
+        tb = TextBlocks(gen_file, bb, read_threads=threads)
         buf = np.empty(bb + 16, np.uint8)
         got = []
         while True:

@@ -28,22 +28,64 @@ import threading
 import time
 from typing import Optional
 
+from concurrent.futures import ThreadPoolExecutor
+
 import numpy as np
 import torch
 
 
 class TextBlocks:
-    """Raw text blocks of a file with BlockReader::fill_block's protocol."""
+    """Raw text blocks of a file with BlockReader::fill_block's protocol.  A
+    block's fresh bytes are read with ``read_threads`` positional reads of
+    contiguous pieces in parallel (the page-cache copy is the bound of a
+    single reader: ~15 GB/s here)."""
 
-    def __init__(self, path: str, block_bytes: int):
+    min_piece = 4 << 20  # bytes per parallel read at least
+
+    def __init__(self, path: str, block_bytes: int, read_threads: int = 8):
         self.path = path
         self.block_bytes = max(2, int(block_bytes))
-        self.f = open(path, "rb", buffering=0)
+        self.fd = os.open(path, os.O_RDONLY)
+        self.pos = 0
         self.carry = b""
         self.eof = False
+        self.read_threads = max(1, int(read_threads))
+        self.pool = (ThreadPoolExecutor(self.read_threads) if self.read_threads > 1 else None)
 
     def close(self) -> None:
-        self.f.close()
+        if self.pool is not None:
+            self.pool.shutdown(wait=True)
+        os.close(self.fd)
+
+    def _pread(self, mv, off: int) -> int:
+        got = 0
+        while got < len(mv):
+            k = os.preadv(self.fd, [mv[got:]], off + got)
+            if k <= 0:
+                break
+            got += k
+        return got
+
+    def _read(self, mv) -> int:
+        """Fill mv from the file position (parallel pieces); bytes read."""
+        want = len(mv)
+        piece = max(self.min_piece, -(-want // self.read_threads))
+        if self.pool is None or want <= piece:
+            got = self._pread(mv, self.pos)
+        else:
+            cuts = list(range(0, want, piece)) + [want]
+            futs = [self.pool.submit(self._pread, mv[a:b], self.pos + a)
+                    for a, b in zip(cuts[:-1], cuts[1:])]
+            sizes = [f.result() for f in futs]
+            got = 0
+            for (a, b), k in zip(zip(cuts[:-1], cuts[1:]), sizes):
+                got += k
+                if k < b - a:  # end of file inside this piece
+                    break
+        self.pos += got
+        if got < want:
+            self.eof = True
+        return got
 
     def read_into(self, buf: np.ndarray) -> int:
         """Next block into buf[:block_bytes] (uint8); returns its length (0: end)."""
@@ -53,12 +95,8 @@ class TextBlocks:
             buf[:c] = np.frombuffer(self.carry, dtype=np.uint8)
         top = c
         mv = memoryview(buf)
-        while top < B - 1 and not self.eof:
-            got = self.f.readinto(mv[top:B - 1])
-            if not got:
-                self.eof = True
-                break
-            top += got
+        if top < B - 1 and not self.eof:
+            top += self._read(mv[top:B - 1])
         n = top
         self.carry = b""
         if top + 1 == B:  # buffer full: cut after the last newline
@@ -84,13 +122,13 @@ class TextStream:
     used rows' occurrence count comes back with the parse)."""
 
     def __init__(self, engine, path: str, block_bytes: int, row_mod: int = 1, nbuf: int = 3,
-                 timeline=None):
+                 timeline=None, read_threads: int = 8):
         self.engine = engine
         self.device = engine.device
-        self.blocks = TextBlocks(path, block_bytes)
+        self.blocks = TextBlocks(path, block_bytes, read_threads)
         self.row_mod = max(1, int(row_mod))
         self.timeline = timeline
-        cap = self.blocks.block_bytes + 16
+        cap = self.blocks.block_bytes + 64
         self.pinned = [torch.empty(cap, dtype=torch.uint8, pin_memory=self.device.type == "cuda")
                        for _ in range(nbuf)]
         self.copy = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
@@ -105,7 +143,9 @@ class TextStream:
         # device output arrays, grown as needed: a line needs >= 2 bytes, a
         # feature token >= 4 (" a:b")
         self._out = None
-        self._text = None
+        self._texts = [None, None]  # device text buffers (block t parses while t+1 uploads)
+        self._tb = 0
+        self._pending = None        # an uploaded block not yet parsed
         self.thread = threading.Thread(target=self._produce, daemon=True)
         self.thread.start()
 
@@ -141,46 +181,64 @@ class TextStream:
 
     def next(self) -> Optional[dict]:
         while True:
-            item = self.ready.get()
-            if item is None:
-                if self.error is not None:
-                    raise self.error
-                self.ready.put(None)
-                return None
-            slot, n = item
-            blk = self._parse(slot, n)
+            if self._pending is None:
+                item = self.ready.get()
+                if item is None:
+                    if self.error is not None:
+                        raise self.error
+                    self.ready.put(None)
+                    return None
+                self._pending = self._upload(*item)
+            cur, self._pending = self._pending, None
+            if self.device.type == "cuda":
+                # the next block's upload goes out now when it is read already:
+                # its DMA then overlaps this block's parse and step
+                try:
+                    item = self.ready.get_nowait()
+                except queue.Empty:
+                    item = False
+                if item is None:
+                    self.ready.put(None)
+                elif item is not False:
+                    self._pending = self._upload(*item)
+            blk = self._parse(*cur)
             if blk is not None:
                 return blk
             # (a block of only malformed lines: the next one, as BlockReader)
 
-    def _parse(self, slot: int, n: int) -> Optional[dict]:
-        e = self.engine
+    def _upload(self, slot: int, n: int):
+        """H2D of a read slot into the next of two device text buffers (copy
+        stream); the host synced on that buffer's previous parse already
+        (parse_text waits for its counts)."""
         src = self.pinned[slot]
-        if self.device.type == "cuda":
-            if self._text is None or self._text.numel() < n + 16:
-                self._text = torch.empty(self.blocks.block_bytes + 16, dtype=torch.uint8,
-                                         device=self.device)
-            compute = torch.cuda.current_stream(self.device)
-            # the text buffer is reused: its previous parse must be done
-            self.copy.wait_stream(compute)
-            with torch.cuda.stream(self.copy):
-                if self.timeline is not None:
-                    self.timeline.begin("h2d", self.copy)
-                self._text[:n].copy_(src[:n], non_blocking=True)
-                if self.timeline is not None:
-                    self.timeline.end("h2d", self.copy)
-                ev = torch.cuda.Event()
-                ev.record(self.copy)
-            self.free.put((slot, ev))
-            compute.wait_stream(self.copy)
-            text = self._text
-        else:
-            text = src
+        if self.device.type != "cuda":
+            return (src, n, None, slot)
+        self._tb ^= 1
+        buf = self._texts[self._tb]
+        if buf is None or buf.numel() < n + 64:
+            # (the parse kernels read aligned 16-byte chunks up to 32 bytes past the block)
+            buf = torch.empty(self.blocks.block_bytes + 64, dtype=torch.uint8, device=self.device)
+            self._texts[self._tb] = buf
+        with torch.cuda.stream(self.copy):
+            if self.timeline is not None:
+                self.timeline.begin("h2d", self.copy)
+            buf[:n].copy_(src[:n], non_blocking=True)
+            if self.timeline is not None:
+                self.timeline.end("h2d", self.copy)
+            ev = torch.cuda.Event()
+            ev.record(self.copy)
+        self.free.put((slot, ev))
+        return (buf, n, ev, slot)
+
+    def _parse(self, text: torch.Tensor, n: int, ev, slot: int) -> Optional[dict]:
+        e = self.engine
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
         o = self._arrays(n)
         t0 = time.perf_counter()
         rows, nnz, lmin, lmax, nused = e.parse_text(text, n, o, self.row_mod)
         self.parse_s += time.perf_counter() - t0
-        if self.device.type != "cuda":
+        if ev is None:  # (CPU: parsed from the slot itself)
             self.free.put((slot, None))
         if rows == 0:
             return None
@@ -219,4 +277,3 @@ def parse_text_file(engine, path: str, block_bytes: int = 2 << 20):
 
 
 __all__ = ["TextBlocks", "TextStream", "parse_text_file"]
-_ = os

@@ -334,11 +334,14 @@ class Engine:
         return int(self._e.monitor_waits)
 
     def parse_text(self, text: torch.Tensor, n: int, out: dict, row_mod: int = 1):
-        """libffm bytes text[:n] (uint8, engine device, 16-byte aligned) ->
+        """libffm bytes text[:n] (uint8, engine device, 16-byte aligned,
+        allocated >= n + 32 bytes) ->
         out["keys"/"fgid"/"row_ptr"/"labels"] on the device (kernels_parse.hip;
         reader.cpp's rules).  Returns (rows, occurrences, shortest row,
         longest row, occurrences of the first rows - rows % row_mod rows)."""
         self._sync_stream()
+        if text.numel() < n + 32 and text.is_cuda:
+            raise ValueError("parse_text: the text tensor needs >= n + 32 bytes")
         return tuple(int(x) for x in self._e.parse_text(
             text.data_ptr(), int(n), out["keys"].data_ptr(), out["fgid"].data_ptr(),
             out["row_ptr"].data_ptr(), out["labels"].data_ptr(), int(out["labels"].numel()),

@@ -241,7 +241,7 @@ class Trainer:
                           if os.environ.get("XFLOW_STREAM_TIMELINE") else None)
                     stream = TextStream(self.engine, path, cfg.train_block_bytes,
                                         row_mod=1 if cfg.keep_remainder else self.threads,
-                                        timeline=tl)
+                                        timeline=tl, read_threads=cfg.copy_threads)
                     nxt = stream.next
                 else:
                     nxt = reader.next
