@@ -225,10 +225,12 @@ __global__ void __launch_bounds__(kPBlock) k_line_count(const char* __restrict__
                                                         const long long* __restrict__ counts,
                                                         unsigned long long* __restrict__ lv,
                                                         int64_t max_lines) {
-  const int64_t l = (int64_t)blockIdx.x * kPBlock + threadIdx.x;
   int64_t nl = counts[4];
   nl = nl < max_lines ? nl : max_lines;
-  if (l >= nl) return;
+  // (grid-stride: the grid is sized for the workspace bound, the lines are
+  // counted on the device)
+  for (int64_t l = (int64_t)blockIdx.x * kPBlock + threadIdx.x; l < nl;
+       l += (int64_t)gridDim.x * kPBlock) {
   int64_t s, e;
   line_span(line_end, l, s, e);
   // one forward pass: the first TAB starts the tokens; a token (a run
@@ -252,6 +254,7 @@ __global__ void __launch_bounds__(kPBlock) k_line_count(const char* __restrict__
   }
   tok += colon;
   lv[l] = row ? ((1ull << kTokBits) | tok) : 0ull;
+  }
 }
 
 // exclusive scan of n u64 values in place: per-workgroup totals, one
@@ -288,17 +291,22 @@ __global__ void __launch_bounds__(kPBlock) k_scan_reduce(const unsigned long lon
                                                          unsigned long long* __restrict__ wg) {
   int64_t n = counts[4];
   n = n < max_n ? n : max_n;
-  const int64_t i0 = (int64_t)blockIdx.x * kScanWg + (int64_t)threadIdx.x * kScanPer;
-  unsigned long long s = 0;
+  for (int64_t c = blockIdx.x; c * kScanWg < n; c += gridDim.x) {  // (block-uniform)
+    const int64_t i0 = c * kScanWg + (int64_t)threadIdx.x * kScanPer;
+    unsigned long long s = 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k) s += i0 + k < n ? v[i0 + k] : 0ull;
-  unsigned long long tot;
-  (void)block_excl_u64(s, &tot);
-  if (threadIdx.x == 0) wg[blockIdx.x] = tot;
+    for (int k = 0; k < kScanPer; ++k) s += i0 + k < n ? v[i0 + k] : 0ull;
+    unsigned long long tot;
+    (void)block_excl_u64(s, &tot);
+    if (threadIdx.x == 0) wg[c] = tot;
+  }
 }
 
-__global__ void __launch_bounds__(kPBlock) k_scan_top(unsigned long long* __restrict__ wg, int nwg,
+__global__ void __launch_bounds__(kPBlock) k_scan_top(unsigned long long* __restrict__ wg, int64_t max_n,
                                                       long long* __restrict__ counts) {
+  int64_t n = counts[4];
+  n = n < max_n ? n : max_n;
+  const int nwg = (int)((n + kScanWg - 1) / kScanWg);  // (the chunks that hold lines)
   unsigned long long carry = 0;
   for (int c0 = 0; c0 < nwg; c0 += kPBlock) {
     const int i = c0 + (int)threadIdx.x;
@@ -320,22 +328,24 @@ __global__ void __launch_bounds__(kPBlock) k_scan_apply(unsigned long long* __re
                                                         const unsigned long long* __restrict__ wg) {
   int64_t n = counts[4];
   n = n < max_n ? n : max_n;
-  const int64_t i0 = (int64_t)blockIdx.x * kScanWg + (int64_t)threadIdx.x * kScanPer;
-  unsigned long long x[kScanPer], s = 0;
+  for (int64_t c = blockIdx.x; c * kScanWg < n; c += gridDim.x) {  // (block-uniform)
+    const int64_t i0 = c * kScanWg + (int64_t)threadIdx.x * kScanPer;
+    unsigned long long x[kScanPer], s = 0;
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    x[k] = i0 + k < n ? v[i0 + k] : 0ull;
-    s += x[k];
-  }
-  unsigned long long tot;
-  unsigned long long off = wg[blockIdx.x] + block_excl_u64(s, &tot);
+    for (int k = 0; k < kScanPer; ++k) {
+      x[k] = i0 + k < n ? v[i0 + k] : 0ull;
+      s += x[k];
+    }
+    unsigned long long tot;
+    unsigned long long off = wg[c] + block_excl_u64(s, &tot);
 #pragma unroll
-  for (int k = 0; k < kScanPer; ++k) {
-    if (i0 + k < n) {
-      const unsigned long long own = x[k];
-      v[i0 + k] = off;  // exclusive prefix; (own's flag tells a row apart)
-      off += own;
-      if (!(own >> kTokBits)) v[i0 + k] |= 1ull << 63;  // no row
+    for (int k = 0; k < kScanPer; ++k) {
+      if (i0 + k < n) {
+        const unsigned long long own = x[k];
+        v[i0 + k] = off;  // exclusive prefix; (own's flag tells a row apart)
+        off += own;
+        if (!(own >> kTokBits)) v[i0 + k] |= 1ull << 63;  // no row
+      }
     }
   }
 }
@@ -344,12 +354,13 @@ __global__ void __launch_bounds__(kPBlock) k_line_emit(const char* __restrict__ 
                                                        const u32* __restrict__ line_end,
                                                        const unsigned long long* __restrict__ lv,
                                                        TextParseArgs a) {
-  const int64_t l = (int64_t)blockIdx.x * kPBlock + threadIdx.x;
   int64_t nl = a.counts[4];
   nl = nl < a.max_lines ? nl : a.max_lines;
   const bool rows_ok = a.counts[0] <= a.max_rows && a.counts[1] <= a.max_nnz && a.counts[5] == 0;
   int mn = 0x7FFFFFFF, mx = 0;
-  if (l < nl && rows_ok && !(lv[l] >> 63)) {
+  for (int64_t l = (int64_t)blockIdx.x * kPBlock + threadIdx.x; l < nl && rows_ok;
+       l += (int64_t)gridDim.x * kPBlock) {
+    if (lv[l] >> 63) continue;  // (no row)
     const unsigned long long off = lv[l];
     const int64_t row = (int64_t)(off >> kTokBits);
     int64_t o = (int64_t)(off & ((1ull << kTokBits) - 1ull));
@@ -361,33 +372,100 @@ __global__ void __launch_bounds__(kPBlock) k_line_emit(const char* __restrict__ 
     int64_t i = s;
     while (i < e && bs.at(i) != '\t') ++i;  // (a row: there is a TAB)
     a.labels[row] = dev_atof(text + s, text + i) > 0.0000001 ? 1.0f : 0.0f;
-    // token [q, i) at each ' ' / the line end: its first ':' (c1) and second (c2)
-    int64_t q = ++i, c1 = -1, c2 = -1;
+    // One forward pass over the tokens, from registers: a token ends at ' '
+    // or the line end; part 0 (before the first ':') is the field id -- an
+    // optionally signed decimal integer is accumulated on the fly, anything
+    // else takes atof from memory --, part 1 (to the second ':') the feature
+    // text, kept in two 64-bit words up to 16 bytes and hashed from them
+    // (longer: hashed from memory), part 2 (the value) is ignored.
+    int64_t q = ++i, c1 = -1;
+    int part = 0, flen = 0;
+    long long fval = 0;
+    bool fneg = false, fsign = false, fdig = false, fslow = false;
+    u64 w0 = 0, w1 = 0;
     for (; i <= e; ++i) {
       const char c = i < e ? bs.at(i) : ' ';
-      if (c == ':') {
-        if (c1 < 0) c1 = i;
-        else if (c2 < 0) c2 = i;
+      if (c == ' ') {
+        if (c1 >= 0) {  // a feature token (empty tokens have no ':')
+          int n = flen;
+          const int64_t fb = c1 + 1;
+          auto byte_at = [&](int j) -> char {
+            return (char)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xFF);
+          };
+          if (part == 1) {  // 2-part token: trailing '\r' (a CRLF line end) stripped
+            if (n <= 16) {
+              while (n > 0 && byte_at(n - 1) == '\r') --n;
+            } else {
+              while (n > 0 && text[fb + n - 1] == '\r') --n;
+            }
+          }
+          u64 key;
+          if (n <= 16) {
+            const u64 mul = (0xc6a4a793ull << 32) + 0x5bd1e995ull;
+            auto shift_mix = [](u64 v) { return v ^ (v >> 47); };
+            u64 h = 0xc70f6907ull ^ ((u64)n * mul);
+            if (n >= 8) {
+              h ^= shift_mix(w0 * mul) * mul;
+              h *= mul;
+            }
+            if (n >= 16) {
+              h ^= shift_mix(w1 * mul) * mul;
+              h *= mul;
+            }
+            const int rem = n & 7;
+            if (rem) {
+              h ^= (n >= 8 ? w1 : w0) & ((1ull << (8 * rem)) - 1ull);
+              h *= mul;
+            }
+            h = shift_mix(h) * mul;
+            key = shift_mix(h);
+          } else {
+            key = std_hash_bytes(text + fb, n);
+          }
+          a.fgid[o] = fslow ? (int32_t)dev_atof(text + q, text + c1)
+                            : (int32_t)(fneg ? -fval : fval);
+          a.keys[o] = key;
+          ++o;
+        }
+        q = i + 1;
+        c1 = -1;
+        part = flen = 0;
+        fval = 0;
+        fneg = fsign = fdig = fslow = false;
+        w0 = w1 = 0;
         continue;
       }
-      if (c != ' ') continue;
-      if (c1 >= 0) {  // a feature token (empty tokens have no ':')
-        const int64_t fb = c1 + 1;
-        int64_t fe = c2 >= 0 ? c2 : i;
-        if (c2 < 0)
-          while (fe > fb && text[fe - 1] == '\r') --fe;  // 2-part token at a CRLF line end
-        a.fgid[o] = (int32_t)dev_atof(text + q, text + c1);
-        a.keys[o] = std_hash_bytes(text + fb, fe - fb);
-        ++o;
+      if (part == 0) {
+        if (c == ':') {
+          part = 1;
+          c1 = i;
+        } else if (c >= '0' && c <= '9') {
+          if (!fslow) {
+            fval = fval * 10 + (c - '0');
+            fslow = fval > 0x7FFFFFFFll;  // (beyond int32: atof from memory)
+          }
+          fdig = true;
+        } else if ((c == '-' || c == '+') && !fdig && !fsign) {
+          fsign = true;
+          fneg = c == '-';
+        } else if (!(is_space(c) && !fdig && !fsign)) {
+          fslow = true;  // fraction, exponent, text...: atof from memory
+        }
+      } else if (part == 1) {
+        if (c == ':') {
+          part = 2;
+        } else {
+          if (flen < 8) w0 |= (u64)(unsigned char)c << (8 * flen);
+          else if (flen < 16) w1 |= (u64)(unsigned char)c << (8 * (flen - 8));
+          ++flen;
+        }
       }
-      q = i + 1;
-      c1 = c2 = -1;
     }
     a.row_ptr[row + 1] = (int32_t)o;
     const long long rows = a.counts[0];
     if (row + 1 == rows - rows % a.row_mod) a.counts[6] = o;  // (the used rows' end)
-    mn = (int)(o - o0);
-    mx = mn;
+    mn = min(mn, (int)(o - o0));
+    mx = max(mx, (int)(o - o0));
   }
   // the rows' shortest / longest feature counts (fixed-width blocks go
   // field-major on the device)
@@ -446,15 +524,14 @@ void launch_parse_text(const TextParseArgs& a, hipStream_t st) {
                        max_lines, a.counts);
     hipLaunchKernelGGL(k_nl_write, dim3((unsigned)nwg), dim3(kPBlock), 0, st, a.text, a.n, wg_cnt,
                        line_end, max_lines);
-    const unsigned lg = (unsigned)((max_lines + kPBlock - 1) / kPBlock);
+    // grid-stride kernels: at most 8 K workgroups (the lines are counted on the device)
+    const unsigned lg = (unsigned)std::min<int64_t>((max_lines + kPBlock - 1) / kPBlock, 8192);
     hipLaunchKernelGGL(k_line_count, dim3(lg), dim3(kPBlock), 0, st, a.text, line_end, a.counts, lv,
                        max_lines);
-    const int64_t sw = (max_lines + kScanWg - 1) / kScanWg;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)sw), dim3(kPBlock), 0, st, lv, a.counts,
-                       max_lines, swg);
-    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kPBlock), 0, st, swg, (int)sw, a.counts);
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)sw), dim3(kPBlock), 0, st, lv, a.counts,
-                       max_lines, swg);
+    const unsigned sw = (unsigned)std::min<int64_t>((max_lines + kScanWg - 1) / kScanWg, 4096);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(sw), dim3(kPBlock), 0, st, lv, a.counts, max_lines, swg);
+    hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kPBlock), 0, st, swg, max_lines, a.counts);
+    hipLaunchKernelGGL(k_scan_apply, dim3(sw), dim3(kPBlock), 0, st, lv, a.counts, max_lines, swg);
     hipLaunchKernelGGL(k_line_emit, dim3(lg), dim3(kPBlock), 0, st, a.text, line_end, lv, a);
   }
   XF_HIP_CHECK(hipGetLastError());
