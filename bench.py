@@ -249,6 +249,14 @@ def main():
         dist.all_reduce(red, op=dist.ReduceOp.SUM)
         elapsed = float(mx.item())
     vals = red.tolist()
+    # per-rank host time per step (issue net of blocked, and blocked)
+    host_rank = [1000.0 * (t_issue - t_blocked) / a.steps, 1000.0 * t_blocked / a.steps,
+                 int(getattr(sharded, "mid_step_waits", 0)), int(getattr(sharded, "host_waits", 0))]
+    if world > 1:
+        allh = [None] * world
+        dist.all_gather_object(allh, host_rank)
+    else:
+        allh = [host_rank]
     ln_loss, rows, table_keys, nonzero = vals[1], vals[2], vals[3], vals[4]
     prefill_tot = vals[6]
     if vals[5] > 0:
@@ -301,6 +309,9 @@ def main():
             # being behind is not host cost), and the blocked time itself
             "host_issue_ms_per_step": 1000.0 * (t_issue - t_blocked) / a.steps,
             "host_blocked_ms_per_step": 1000.0 * t_blocked / a.steps,
+            # every rank's [issue ms, blocked ms, mid-step waits, host waits]
+            **({"host_per_rank": [[round(x, 4) if isinstance(x, float) else x for x in h]
+                                  for h in allh]} if world > 1 else {}),
             "monitor_lag": a.monitor_lag,
         }
         if a.model == "fm":

@@ -18,6 +18,6 @@ for n in ${NS:-2}; do
         --steps ${STEPS:-5} --warmup 2 --batch ${BATCH:-65536} --log2-cap ${LOG2CAP:-26} $extra \
         > $log 2>&1 || { echo "shared-GPU bench n=$n '$extra' failed"; tail -40 $log; exit 1; }
     grep '"metric"' $log | cut -c1-200
-    grep -o '"a2a_transport": "[a-z]*"\|"logloss": [0-9.]*\|"host_waits": [0-9]*\|"shared_gpu_rehearsal": true' $log | tr '\n' ' '; echo
+    grep -o '"a2a_transport": "[a-z]*"\|"logloss": [0-9.]*\|"host_waits": [0-9]*\|"mid_step_waits": [0-9]*\|"host_per_rank": [^}]*\]\]\|"shared_gpu_rehearsal": true' $log | tr '\n' ' '; echo
   done
 done

@@ -4,6 +4,9 @@ idle gaps that follow each kernel (the host-side stalls between launches).
 
     python tools/trace_gaps.py gpurun_out/prof_x/run_kernel_trace.csv [--skip F]
     python tools/trace_gaps.py <trace> --marker k_synth --steps 18
+    python tools/trace_gaps.py <trace rank 0> <trace rank 1> ...   (several
+        processes sharing one GPU: the union of their kernels, i.e. whether
+        the DEVICE idles; kernel names carry their rank)
 
 --skip drops the first fraction of the trace (warmup, setup); --marker instead
 cuts the trace at the dispatches of the step's first kernel and analyses the
@@ -18,7 +21,7 @@ import csv
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("trace")
+    ap.add_argument("trace", nargs="+")
     ap.add_argument("--skip", type=float, default=0.3,
                     help="fraction of the trace (by time) to skip as warmup")
     ap.add_argument("--top", type=int, default=12)
@@ -28,9 +31,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     a = ap.parse_args()
     rows = []
-    with open(a.trace) as f:
-        for r in csv.DictReader(f):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))
+    for k, path in enumerate(a.trace):
+        tag = f"[r{k}] " if len(a.trace) > 1 else ""
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                             tag + r["Kernel_Name"][:60]))
     rows.sort()
     if not rows:
         return
