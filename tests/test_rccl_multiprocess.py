@@ -159,3 +159,72 @@ def test_rccl_processes_trainer_equals_cpu_gloo(gpu_device, tmp_path):
     c = np.loadtxt(cdir / "pred_0_0.txt")
     assert g.shape == c.shape == (200, 3)
     np.testing.assert_allclose(g, c, rtol=1e-5, atol=1e-6)
+
+
+# ---- bench scale over RCCL between processes: W = 4 x 32 768 Criteo-shaped
+# rows x 39 fields x 5 pipelined steps (the loopback test's shape,
+# tests/test_w8_loopback.py, now through real RCCL group calls)
+BS_ROWS, BS_STEPS, BS_W = 32768, 5, 4
+
+
+def _bs_batches(rank, dev):
+    from xflow_amd.data.synth import SynthConfig, SyntheticCriteo
+
+    gen_eng = Engine(ModelConfig(), OptimConfig(),
+                     EngineConfig(table_log2_cap=10, max_rows=BS_ROWS, max_nnz=BS_ROWS * 39),
+                     device=dev)
+    g = SyntheticCriteo(gen_eng, BS_ROWS, SynthConfig(seed=4242), rank=rank)
+    out = []
+    for _ in range(BS_STEPS):
+        b = g.alloc_batch()
+        g.next(out=b)
+        out.append(b)
+    return out
+
+
+def _bs_engine(dev, rows, log2_cap, slices=1, kind="lr"):
+    return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
+                  EngineConfig(table_log2_cap=log2_cap, max_rows=rows, max_nnz=rows * 39,
+                               max_slices=slices), device=dev)
+
+
+def _bs_worker(rank, world, kind, out_dir):
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    dev = torch.device("cuda", 0)
+    eng = _bs_engine(dev, BS_ROWS, 22, kind=kind)
+    sh = ShardedEngine(eng)
+    assert sh.transport == "rccl", sh.transport
+    bs = _bs_batches(rank, dev)
+    for s in range(BS_STEPS):
+        assert sh.train_step(bs[s], S=1, next_batch=bs[s + 1] if s + 1 < BS_STEPS else None)
+    torch.cuda.synchronize(dev)
+    assert not eng.overflowed()
+    assert sh.inline_prepares == 1 and sh.early_key_exchanges == BS_STEPS - 1
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"bk{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"bv{rank}.npy"), eng.pull(keys))
+
+
+@pytest.mark.parametrize("kind", ["lr", "fm"])
+def test_rccl_processes_bench_scale_equals_single_engine(gpu_device, tmp_path, kind):
+    """4 processes x 32 768 Criteo-shaped rows x 39 fields x 5 pipelined steps
+    over RCCL == one engine trained on the 4 ranks' batches as 4 ordered
+    slices per step (rtol 1e-4)."""
+    from xflow_amd.engine import Batch
+
+    run_world_gpu(_bs_worker, BS_W, kind, str(tmp_path))
+    data = [_bs_batches(r, gpu_device) for r in range(BS_W)]
+    ref = _bs_engine(gpu_device, BS_W * BS_ROWS, 25, slices=BS_W, kind=kind)
+    for s in range(BS_STEPS):
+        keys = torch.cat([data[r][s].keys.view(39, BS_ROWS) for r in range(BS_W)],
+                         dim=1).reshape(-1)
+        lab = torch.cat([data[r][s].labels for r in range(BS_W)])
+        ref.train_step(Batch(keys=keys.contiguous(), labels=lab, nnz_per_row=39,
+                             field_major=True, slice_rows=BS_ROWS))
+    k = np.concatenate([np.load(tmp_path / f"bk{r}.npy") for r in range(BS_W)])
+    v = np.concatenate([np.load(tmp_path / f"bv{r}.npy") for r in range(BS_W)])
+    for r in range(BS_W):
+        assert (owner_of(np.load(tmp_path / f"bk{r}.npy"), BS_W) == r).all()
+    assert len(np.unique(k)) == len(k) == ref.table_size()
+    np.testing.assert_allclose(v, ref.pull(k), rtol=1e-4, atol=1e-6)
