@@ -10,6 +10,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <vector>
+#include <sys/mman.h>
 
 #include "xflow/backend.h"
 #include "xflow/reader.h"
@@ -47,8 +48,7 @@ void add_stats(LossStats* st, float p, float y) {
 }
 
 u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
-  const u64 mask = t.cap - 1;
-  u64 s = fmix64(key) & mask;
+  u64 s = table_home(t, fmix64(key));
   for (u64 n = 0; n < t.probe_limit; ++n) {
     u64* kp = reinterpret_cast<u64*>(t.words + s * (u64)t.L.stride);
     if (*kp == key) return (u32)s;
@@ -58,7 +58,7 @@ u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
       claimed = true;
       return (u32)s;
     }
-    s = (s + 1) & mask;
+    s = table_next(t, s);
   }
   if (insert) *t.overflow = 1u;
   return kNoSlot;
@@ -464,18 +464,93 @@ class CpuBackend final : public Backend {
       if (slot != kNoSlot && t.L.has_flag) t.words[(u64)slot * t.L.stride + t.L.flag_word] = 1u;
     }
   }
-  void table_rehash(const TableView& from, const TableView& to) override {
-    const int W = from.L.stride;
-    for (u64 s = 0; s < from.cap; ++s) {
-      const u32* sp = from.words + s * (u64)W;
-      const u64 key = *reinterpret_cast<const u64*>(sp);
-      if (key == kEmptyKey) continue;
-      bool claimed = false;
-      const u32 slot = probe(to, key, true, claimed);
-      if (claimed) ++*to.size;
-      if (slot != kNoSlot) std::memcpy(to.words + (u64)slot * W + 2, sp + 2, sizeof(u32) * (W - 2));
+  // The HIP split kernels' algorithm (kernels_table.hip k_table_split_marks /
+  // k_table_split), one cluster after the other: cluster starts are marked
+  // before any slot changes, then each cluster is walked with backward-shift
+  // placement of its staying keys.
+  void table_split(const TableView& t, u64 s0, u64 k) override {
+    const int W = t.L.stride;
+    const int g = t.seg_log2;
+    const u64 G = 1ull << g, m = G - 1, n = k << g;
+    const u64 move_bit = 1ull << (g + t.level), buddy = (1ull << t.level) << g;
+    auto key_at = [&](u64 s) { return *reinterpret_cast<const u64*>(t.words + s * (u64)W); };
+    std::vector<u64> starts;
+    for (u64 i = 0; i < n; ++i) {
+      const u64 base = (s0 << g) + (i & ~m), c = i & m;
+      if (key_at(base + c) != kEmptyKey && key_at(base + ((c - 1) & m)) == kEmptyKey)
+        starts.push_back(i);
+    }
+    auto free_slot = [&](u32* sp) {
+      sp[0] = sp[1] = 0xFFFFFFFFu;
+      for (int w = 2; w < W; ++w) sp[w] = 0u;
+    };
+    for (u64 i : starts) {
+      const u64 base = (s0 << g) + (i & ~m), c = i & m;
+      auto at = [&](u64 off) { return base + ((c + off) & m); };
+      for (u64 d = 0; d < G; ++d) {
+        u32* sp = t.words + at(d) * (u64)W;
+        const u64 key = *reinterpret_cast<const u64*>(sp);
+        if (key == kEmptyKey) break;
+        const u64 h = fmix64(key);
+        if (h & move_bit) {
+          u64 q = base + buddy + (h & m);
+          u64 r = 0;
+          for (; r < t.probe_limit && key_at(q) != kEmptyKey; ++r) q = table_next(t, q);
+          if (r < t.probe_limit) std::memcpy(t.words + q * (u64)W, sp, sizeof(u32) * W);
+          else *t.overflow = 1u;
+          free_slot(sp);
+        } else {
+          u64 off = ((h & m) - c) & m;
+          while (off < d && key_at(at(off)) != kEmptyKey) ++off;
+          if (off != d) {
+            std::memcpy(t.words + at(off) * (u64)W, sp, sizeof(u32) * W);
+            free_slot(sp);
+          }
+        }
+      }
     }
   }
+  // The table's range: address space reserved with mmap (pages get memory
+  // when first touched), so growth never copies; a plain allocation that is
+  // re-allocated on growth when the reservation fails.
+  void* table_reserve(size_t max_bytes, bool growable) override {
+    (void)growable;
+    void* p = mmap(nullptr, max_bytes, PROT_READ | PROT_WRITE,
+                   MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (p == MAP_FAILED) {
+      mm_bytes_ = 0;
+      fb_bytes_ = 0;
+      return nullptr;
+    }
+    mm_bytes_ = max_bytes;
+    committed_ = 0;
+    return p;
+  }
+  void* table_commit(void* base, size_t bytes) override {
+    if (mm_bytes_) {
+      if (bytes > mm_bytes_) throw std::runtime_error("xflow: table beyond its reserved range");
+      if (bytes > committed_) committed_ = bytes;
+      return base;
+    }
+    if (bytes <= fb_bytes_) return base;
+    void* p = alloc(bytes);
+    if (base) {
+      std::memcpy(p, base, fb_bytes_);
+      std::free(base);
+    }
+    fb_bytes_ = bytes;
+    return p;
+  }
+  void table_release(void* base) override {
+    if (mm_bytes_) {
+      if (base) munmap(base, mm_bytes_);
+      mm_bytes_ = 0;
+    } else {
+      std::free(base);
+    }
+    committed_ = fb_bytes_ = 0;
+  }
+  size_t table_committed() const override { return mm_bytes_ ? committed_ : fb_bytes_; }
   EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {
     // same definition as the HIP kernels: stable order by pctr descending
     EvalMetrics m;
@@ -512,6 +587,7 @@ class CpuBackend final : public Backend {
 
  private:
   std::vector<char> stage_buf_[2];
+  size_t mm_bytes_ = 0, committed_ = 0, fb_bytes_ = 0;
 };
 
 }  // namespace

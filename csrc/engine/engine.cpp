@@ -4,6 +4,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <thread>
@@ -57,10 +58,22 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   log2_cap_ = cfg_.table_log2_cap;
   max_log2_cap_ = cfg_.max_log2_cap > 0 ? (cfg_.max_log2_cap < 31 ? cfg_.max_log2_cap : 31) : 31;
   if (max_log2_cap_ < log2_cap_) max_log2_cap_ = log2_cap_;
+  if (!(cfg_.grow_start > 0.0 && cfg_.grow_start < cfg_.grow_load))
+    cfg_.grow_start = 0.75 * cfg_.grow_load;
+  // geometry (backend.h TableView): segments of at most 2^24 slots
+  table_.seg_log2 = log2_cap_ < kMaxSegLog2 ? log2_cap_ : kMaxSegLog2;
+  table_.level = log2_cap_ - table_.seg_log2;
+  table_.split = 0;
   table_.cap = 1ull << log2_cap_;
-  table_.probe_limit = table_.cap < kMaxProbe ? table_.cap : kMaxProbe;
+  const u64 seg = 1ull << table_.seg_log2;
+  table_.probe_limit = seg < kMaxProbe ? seg : kMaxProbe;
+  max_segs_ = cfg_.table_grow ? (1ull << max_log2_cap_) >> table_.seg_log2 : table_.cap >> table_.seg_log2;
   table_bytes_ = (size_t)table_.cap * table_.L.stride * sizeof(u32);
-  table_.words = static_cast<u32*>(be.alloc(table_bytes_));
+  {
+    void* base = be.table_reserve((size_t)(max_segs_ << table_.seg_log2) * table_.L.stride * sizeof(u32),
+                                  max_segs_ > (table_.cap >> table_.seg_log2));
+    table_.words = static_cast<u32*>(be.table_commit(base, table_bytes_));
+  }
   // one 16-byte block {size, overflow[2]}: a step's snapshot is one copy
   mon_ = balloc<u32>(be, 4);
   table_.size = reinterpret_cast<unsigned long long*>(mon_);
@@ -182,7 +195,8 @@ Engine::~Engine() {
   Backend& be = *be_;
   be.synchronize();
   use_worker_set(cur_wb_);  // (records the current set)
-  void* ptrs[] = {table_.words, mon_, scratch_.keys, scratch_.stamps,
+  be.table_release(table_.words);
+  void* ptrs[] = {mon_, scratch_.keys, scratch_.stamps,
                   scratch_.claims, block_counts_, uniq_keys_, uniq_slot_, wpull_, grad_, tmask_,
                   stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   host_keys_dev_, host_vals_dev_,
@@ -718,6 +732,7 @@ void Engine::push_host(const std::vector<u64>& keys, const std::vector<float>& g
 }
 
 void Engine::prefill(int64_t n, uint64_t seed) {
+  if (n > 0) guard_inserts(n);  // (may grow the table first)
   if (n < 0 || (uint64_t)n > table_.cap - table_.cap / 16)
     throw std::invalid_argument("prefill: at most 15/16 of the table's slots");
   stale_stashes();
@@ -1184,10 +1199,10 @@ void Engine::poll_snapshots(int64_t wait_upto) {
     if (ovf0 || ovf1) {
       char msg[320];
       std::snprintf(msg, sizeof(msg),
-                    "xflow: %s overflow -- keys were dropped (table: %lld keys in 2^%d slots%s); "
+                    "xflow: %s overflow -- keys were dropped (table: %lld keys in %llu slots%s); "
                     "raise the capacity (table_log2_cap / max_log2_cap, max_nnz)",
                     ovf1 ? "parameter table" : "dedup/owner scratch", (long long)size,
-                    log2_cap_, cfg_.table_grow ? "" : ", growth disabled");
+                    (unsigned long long)table_.cap, cfg_.table_grow ? "" : ", growth disabled");
       throw std::runtime_error(msg);
     }
   }
@@ -1213,56 +1228,127 @@ void Engine::end_step() {
   poll_snapshots(snap_seq_ - cfg_.monitor_lag);
 }
 
-// Before an inserting pull of n keys (at most n new): make sure the table can
-// take them below grow_load.  The bound is the last snapshot's size plus
-// every insert bound queued since; only when it passes the watermark does the
-// host read the exact size (one sync), and grow if that is needed too.
+// Before an inserting pull of n keys (at most n new): grow the table so that
+// the growth schedule (EngineConfig::grow_start / grow_load) holds for an
+// upper bound of its size -- the last snapshot's size plus every insert bound
+// queued since.  No host sync: a split is queued device work (split_to).
 void Engine::guard_inserts(int64_t n) {
   if (n <= 0) return;
   // an apply outside a step (e.g. a staleness-k flush) carried a snapshot:
   // close it before these inserts, which it does not include
   if (snap_carried_) close_snapshot();
   poll_snapshots(-1);
-  const double lim = cfg_.grow_load * (double)table_.cap;
-  if (cfg_.table_grow && (double)(known_size_ + (queued_adds_ - known_adds_) + n) > lim) {
-    const int64_t exact = table_size();  // (syncs; re-bases the monitor)
-    ++monitor_waits_;
-    int lg = log2_cap_;
-    while ((double)(exact + n) > cfg_.grow_load * (double)(1ull << lg) && lg < max_log2_cap_) ++lg;
-    if (lg > log2_cap_) grow_table(lg);
+  if (cfg_.table_grow) {
+    const double bound = (double)(known_size_ + (queued_adds_ - known_adds_) + n);
+    const u64 N = table_.cap >> table_.seg_log2;
+    const u64 want = segments_for(bound, cfg_.grow_start, cfg_.grow_load);
+    if (want > N) {
+      // paced: twice what the schedule asks for this call's n keys (and at
+      // least ~64 MB of segments), so a schedule that fell behind catches up
+      // over several calls instead of one burst -- unless the fullest
+      // segments would pass kHardLoad
+      const size_t seg_bytes = ((size_t)1 << table_.seg_log2) * table_.L.stride * sizeof(u32);
+      const u64 before = segments_for(bound - (double)n, cfg_.grow_start, cfg_.grow_load);
+      u64 pace = 2 * (want - (before < want ? before : want)) + 1;
+      const u64 floor_pace = seg_bytes >= (64u << 20) ? 1 : (u64)((64u << 20) / seg_bytes);
+      if (pace < floor_pace) pace = floor_pace;
+      const double hl = cfg_.grow_load > kHardLoad ? cfg_.grow_load : kHardLoad;
+      const u64 hard = segments_for(bound, hl, hl);
+      u64 target = want < N + pace ? want : N + pace;
+      if (hard > target) target = hard;
+      split_to(target);
+    }
   }
   queued_adds_ += n;
 }
 
-void Engine::grow_table(int lg) {
-  if (lg <= log2_cap_) return;
-  if (lg > 31) throw std::invalid_argument("grow_table: at most 2^31 slots (32-bit slot indices)");
-  be_->synchronize();
-  poll_snapshots(snap_seq_);  // (raises on a pending overflow first)
-  TableView nt = table_;
-  nt.cap = 1ull << lg;
-  nt.probe_limit = nt.cap < kMaxProbe ? nt.cap : kMaxProbe;
-  const size_t bytes = (size_t)nt.cap * table_.L.stride * sizeof(u32);
-  const size_t fr = be_->free_memory();
-  if (fr < bytes + (size_t)(256u << 20)) {
-    char msg[256];
-    std::snprintf(msg, sizeof(msg),
-                  "xflow: table growth to 2^%d slots needs %.1f GB, %.1f GB free on the device",
-                  lg, bytes / 1e9, fr / 1e9);
-    throw std::runtime_error(msg);
+// Segments the schedule wants for `keys` keys: at level L with s segments
+// split, a segment not yet split holds keys / 2^L (uniform hashing) at load
+// u = keys / (2^L * G); the schedule splits 2^L * (u - grow_start) /
+// (grow_load - grow_start) of them (all by u = grow_load, when the level is
+// complete and u halves).  u0 == u1: the segments that keep every load <= u1
+// (whole levels).  Capped at 2^max_log2_cap slots.
+u64 Engine::segments_for(double keys, double u0, double u1) const {
+  const int g = table_.seg_log2;
+  const double G = (double)(1ull << g);
+  u64 N = table_.cap >> g;
+  while (N < max_segs_) {
+    int L = 0;
+    while ((2ull << L) <= N) ++L;
+    const u64 P = 1ull << L, s = N - P;
+    const double u = keys / ((double)P * G);
+    if (u <= u0) break;
+    u64 want = u >= u1 ? P : (u64)std::ceil((double)P * (u - u0) / (u1 - u0));  // (u0 < u < u1)
+    if (want > P) want = P;
+    if (want <= s) break;
+    N = P + want;
   }
-  nt.words = static_cast<u32*>(be_->alloc(bytes));
-  be_->table_clear(nt);
-  be_->memset(table_.size, 0, sizeof(unsigned long long));  // counts the re-inserted keys
-  be_->table_rehash(table_, nt);
-  be_->synchronize();
-  be_->free(table_.words);
-  table_ = nt;
-  table_bytes_ = bytes;
-  log2_cap_ = lg;
-  ++growths_;
-  remap_server_slots();
-  (void)table_size();  // (re-bases the monitor)
+  return N < max_segs_ ? N : max_segs_;
+}
+
+// Split segments (level by level, in launches of at most 2^28 slots) until the
+// table has nseg segments: commit the new segments' memory at the end of the
+// range, clear them, split their source segments (Backend::table_split).
+// Slots of the moved keys change: pulled-but-not-applied server buffers are
+// looked up again, queued on the stream.
+void Engine::split_to(u64 nseg) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int g = table_.seg_log2;
+  const u64 G = 1ull << g;
+  const size_t seg_bytes = (size_t)G * table_.L.stride * sizeof(u32);
+  const u64 per_launch = g >= 28 ? 1 : (1ull << (28 - g));
+  if (nseg > max_segs_) nseg = max_segs_;
+  bool grew = false;
+  while ((table_.cap >> g) < nseg) {
+    const u64 N = table_.cap >> g, P = 1ull << table_.level, s0 = table_.split;
+    u64 k = nseg - N;
+    if (k > P - s0) k = P - s0;
+    if (k > per_launch) k = per_launch;
+    const size_t bytes = (size_t)(N + k) * seg_bytes;
+    const size_t have = be_->table_committed();
+    if (bytes > have) {
+      const size_t fr = be_->free_memory();
+      if (fr < bytes - have + (size_t)(256u << 20)) {
+        if (grew) break;  // (what fits was added; the inserts run at a higher load)
+        char msg[256];
+        std::snprintf(msg, sizeof(msg),
+                      "xflow: table growth to %llu slots needs %.2f GB more, %.2f GB free on the device",
+                      (unsigned long long)((N + k) << g), (bytes - have) / 1e9, fr / 1e9);
+        throw std::runtime_error(msg);
+      }
+    }
+    table_.words = static_cast<u32*>(be_->table_commit(table_.words, bytes));
+    TableView fresh = table_;
+    fresh.words = table_.words + (size_t)(N << g) * table_.L.stride;
+    fresh.cap = k << g;
+    be_->table_clear(fresh);
+    table_.cap = (N + k) << g;
+    table_.split = s0 + k;
+    be_->table_split(table_, s0, k);
+    if (table_.split == P) {
+      ++table_.level;
+      table_.split = 0;
+    }
+    table_bytes_ = (size_t)table_.cap * table_.L.stride * sizeof(u32);
+    splits_ += (int64_t)k;
+    grew = true;
+  }
+  if (grew) {
+    ++growths_;
+    remap_server_slots();
+  }
+  grow_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+size_t Engine::table_committed() const { return be_->table_committed(); }
+
+// Explicit growth to at least 2^lg slots (normally automatic).
+void Engine::grow_table(int lg) {
+  if (lg > 31) throw std::invalid_argument("grow_table: at most 2^31 slots (32-bit slot indices)");
+  if (lg < table_.seg_log2 || (1ull << lg) <= table_.cap) return;
+  if (lg > max_log2_cap_) throw std::invalid_argument("grow_table: beyond max_log2_cap");
+  poll_snapshots(-1);
+  split_to((1ull << lg) >> table_.seg_log2);
 }
 
 // Slots of pulled-but-not-yet-applied server buffers point into the old
@@ -1281,7 +1367,6 @@ void Engine::remap_server_slots() {
     pa.pstride = pstride();
     be_->table_pull(pa);
   }
-  be_->synchronize();
 }
 
 // ---------------------------------------------------------------------------

@@ -39,7 +39,8 @@ void launch_table_export(const TableView& t, u64* keys_out, u32* words_out, int6
 void launch_table_import(const TableView& t, const u64* keys, const u32* words, int64_t n,
                          hipStream_t st);
 void launch_table_prefill(const TableView& t, int64_t n, u64 seed, hipStream_t st);
-void launch_table_rehash(const TableView& from, const TableView& to, hipStream_t st);
+// growth: split segments [s0, s0 + k) (marks: (k << seg_log2) / 64 words of scratch)
+void launch_table_split(const TableView& t, u64 s0, u64 k, u64* marks, hipStream_t st);
 void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long long* counter,
                           hipStream_t st);
 

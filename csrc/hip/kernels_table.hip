@@ -590,8 +590,7 @@ void launch_table_clear(const TableView& t, hipStream_t st) {
 // persistent table probe
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, bool& claimed) {
-  const u64 mask = t.cap - 1;
-  u64 s = fmix64(key) & mask;
+  u64 s = table_home(t, fmix64(key));
   const int stride = t.L.stride;
   for (u64 n = 0; n < t.probe_limit; ++n) {
     u64* kp = reinterpret_cast<u64*>(t.words + s * (u64)stride);
@@ -604,7 +603,7 @@ __device__ __forceinline__ u32 probe(const TableView& t, u64 key, bool insert, b
       if (prev == kEmptyKey) { claimed = true; return (u32)s; }
       if (prev == key) return (u32)s;
     }
-    s = (s + 1) & mask;
+    s = table_next(t, s);
   }
   // bounded chain (TableView::probe_limit): a key is never stored further out
   if (insert) *t.overflow = 1u;
@@ -639,7 +638,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
                                                       float* __restrict__ zero_out) {
   const int64_t n = dev_count(n_dev, n_host, n_max);
   if ((int64_t)blockIdx.x * kPullChunk >= n) return;  // (grid sized by capacity)
-  const u64 mask = t.cap - 1;
+  const u64 segm = (1ull << t.seg_log2) - 1;  // (chains wrap inside a segment)
   uint4* slots = reinterpret_cast<uint4*>(t.words);
   const int64_t base = (int64_t)blockIdx.x * kPullChunk + threadIdx.x;
   u64 key[kPullItems], s[kPullItems];
@@ -648,7 +647,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
   for (int j = 0; j < kPullItems; ++j) {
     int64_t i = base + (int64_t)j * kBlock;
     key[j] = i < n ? sanitize_key(keys[i]) : 0ull;
-    s[j] = fmix64(key[j]) & mask;
+    s[j] = table_home(t, fmix64(key[j]));
   }
 #pragma unroll
   for (int j = 0; j < kPullItems; ++j) {
@@ -715,7 +714,7 @@ __global__ void __launch_bounds__(kBlock) k_pull_lr16(TableView t, FtrlParams fp
       if (q1 < kLineSlots) {
         q0 = q1;
       } else {
-        sj = ((sj | (u64)(kLineSlots - 1)) + 1) & mask;
+        sj = (sj & ~segm) | (((sj | (u64)(kLineSlots - 1)) + 1) & segm);
         q0 = 0;
       }
       q1 = kLineSlots;
@@ -1646,29 +1645,105 @@ __global__ void __launch_bounds__(kBlock) k_table_import(TableView t, const u64*
   block_count_add<kBlock>(t.size, claims);
 }
 
-// Growth: every live slot of `from` is re-inserted into the empty, larger
-// table `to` with its state words (one lane per old slot, grid-stride).
-__global__ void __launch_bounds__(kBlock) k_table_rehash(TableView from, TableView to) {
+// Growth by segment splits (TableView geometry, Backend::table_split).  t is
+// the geometry after the split: segments [s0, s0 + k) of t.level split into
+// their buddies s + 2^level, which are mapped and cleared.  A key moves when
+// bit (seg_log2 + level) of its hash is set.
+//
+// Phase 1 marks the cluster starts of the source segments (an occupied slot
+// whose predecessor in the segment is free) in a bitmap, before any slot
+// changes: phase 2 rewrites clusters, and a start test racing with those
+// writes could see a half-rewritten cluster.  Phase 2: one lane per cluster
+// walks it in order (linear probing's backward-shift deletion, for every
+// moving key at once).  At walk position d every slot before d is final:
+// a moving key is CAS-inserted into the buddy segment (an empty table that
+// only other moving keys compete for) with its state words, and slot d is
+// freed; a staying key goes to the first free slot from its home on -- a
+// slot freed earlier in the walk, or d itself -- and slot d is freed if it
+// left.  Slots before d are never freed again, so every chain from a home to
+// its key stays occupied.  Clusters are separated by free slots, so lanes
+// never touch each other's slots.
+__global__ void __launch_bounds__(kBlock) k_table_split_marks(TableView t, u64 s0, u64 k,
+                                                              u64* __restrict__ marks) {
+  const int g = t.seg_log2;
+  const u64 m = (1ull << g) - 1;
+  const u64 n = k << g;
+  const int W = t.L.stride;
   const u64 stride = (u64)gridDim.x * blockDim.x;
-  const int W = from.L.stride;
-  unsigned int claims = 0;
-  for (u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x; s < from.cap; s += stride) {
-    const u32* sp = from.words + s * (u64)W;
-    const u64 key = *reinterpret_cast<const u64*>(sp);
-    if (key == kEmptyKey) continue;
-    bool claimed = false;
-    const u32 slot = probe(to, key, true, claimed);
-    claims += claimed;
-    if (slot == kNoSlot) continue;
-    u32* dp = to.words + (u64)slot * W;
-    for (int w = 2; w < W; ++w) dp[w] = sp[w];
+  // (n is a multiple of 64 when g >= 6; the ballot of a partial wave is padded)
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < ((n + 63) & ~63ull); i += stride) {
+    bool start = false;
+    if (i < n) {
+      const u64 base = (s0 << g) + (i & ~m), c = i & m;
+      const u64 kc = *reinterpret_cast<const u64*>(t.words + (base + c) * (u64)W);
+      const u64 kp = *reinterpret_cast<const u64*>(t.words + (base + ((c - 1) & m)) * (u64)W);
+      start = kc != kEmptyKey && kp == kEmptyKey;
+    }
+    const unsigned long long b = __ballot(start);
+    if ((threadIdx.x & 63) == 0) marks[i >> 6] = b;
   }
-  block_count_add<kBlock>(to.size, claims);
 }
 
-void launch_table_rehash(const TableView& from, const TableView& to, hipStream_t st) {
-  hipLaunchKernelGGL(k_table_rehash, dim3(grid_for((int64_t)from.cap, kBlock, 16384)), dim3(kBlock),
-                     0, st, from, to);
+__global__ void __launch_bounds__(kBlock) k_table_split(TableView t, u64 s0, u64 k,
+                                                        const u64* __restrict__ marks) {
+  const int g = t.seg_log2;
+  const u64 G = 1ull << g, m = G - 1;
+  const u64 n = k << g;
+  const int W = t.L.stride;
+  const u64 move_bit = 1ull << (g + t.level);
+  const u64 buddy = (1ull << t.level) << g;  // slot offset of a segment's buddy
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (!((marks[i >> 6] >> (i & 63)) & 1ull)) continue;
+    const u64 base = (s0 << g) + (i & ~m), c = i & m;
+    auto slot_at = [&](u64 off) { return t.words + (base + ((c + off) & m)) * (u64)W; };
+    auto free_slot = [&](u32* sp) {
+      sp[0] = 0xFFFFFFFFu;
+      sp[1] = 0xFFFFFFFFu;
+      for (int w = 2; w < W; ++w) sp[w] = 0u;
+    };
+    for (u64 d = 0; d < G; ++d) {  // d: walk offset from the cluster start c
+      u32* sp = slot_at(d);
+      const u64 key = *reinterpret_cast<const u64*>(sp);
+      if (key == kEmptyKey) break;
+      const u64 h = fmix64(key);
+      if (h & move_bit) {
+        u64 q = base + buddy + (h & m);
+        bool placed = false;
+        for (u64 r = 0; r < t.probe_limit; ++r) {
+          u32* qp = t.words + q * (u64)W;
+          const u64 prev = atomicCAS(reinterpret_cast<unsigned long long*>(qp),
+                                     (unsigned long long)kEmptyKey, (unsigned long long)key);
+          if (prev == kEmptyKey) {
+            for (int w = 2; w < W; ++w) qp[w] = sp[w];
+            placed = true;
+            break;
+          }
+          q = table_next(t, q);
+        }
+        if (!placed) *t.overflow = 1u;
+        free_slot(sp);
+      } else {
+        u64 off = ((h & m) - c) & m;  // home, in [0, d]: the chain from it is unbroken
+        while (off < d && *reinterpret_cast<const u64*>(slot_at(off)) != kEmptyKey) ++off;
+        if (off != d) {
+          u32* dp = slot_at(off);
+          for (int w = 0; w < W; ++w) dp[w] = sp[w];
+          free_slot(sp);
+        }
+      }
+    }
+  }
+}
+
+void launch_table_split(const TableView& t, u64 s0, u64 k, u64* marks, hipStream_t st) {
+  const int64_t n = (int64_t)(k << t.seg_log2);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_table_split_marks, dim3(grid_for(n, kBlock, 16384)), dim3(kBlock), 0, st,
+                     t, s0, k, marks);
+  XF_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_table_split, dim3(grid_for(n, kBlock, 16384)), dim3(kBlock), 0, st, t, s0,
+                     k, (const u64*)marks);
   XF_HIP_CHECK(hipGetLastError());
 }
 

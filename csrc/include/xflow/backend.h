@@ -28,19 +28,48 @@ namespace xflow {
 // probe_limit slots of its home flags the table overflow instead of walking a
 // (nearly) full table, and a lookup stops at the same distance -- no key is
 // ever stored further from its home than an insert may probe.  The engine
-// keeps the load below EngineConfig::grow_load by growing the table (2x,
-// Backend::table_rehash), so chains stay short and the bound is never hit in
-// normal operation.
+// keeps the load below EngineConfig::grow_load by growing the table
+// (segment splits, Backend::table_split), so chains stay short and the bound
+// is never hit in normal operation.
 constexpr u64 kMaxProbe = 1ull << 16;
+constexpr int kMaxSegLog2 = 20;  // segment slots (TableView), at most
 
+// Table geometry: linear hashing over equal segments (docs/DESIGN.md §2).
+// The slot array is nseg = 2^level + split segments of 2^seg_log2 slots,
+// contiguous in one reserved address range.  With h = fmix64(key) and
+// b = (h >> seg_log2) mod 2^level -- or mod 2^(level+1) when b < split (that
+// segment was split into b and b + 2^level) -- the key's home is slot
+// b * 2^seg_log2 + (h mod 2^seg_log2), and its chain wraps inside the
+// segment.  A power-of-two table (split = 0) has the home h mod cap, as a
+// plain linear-probing table.  Growing adds one segment and splits one: only
+// the split segment's keys move (Backend::table_split), the new memory is one
+// segment, and the rest of the table is untouched -- growth costs no 2x peak
+// and no stop of the world.  The segment index bits (seg_log2 .. 30) stay
+// below the owner bits (fmix64 >> 32, parallel/sparse_a2a.py), so a rank's
+// shard spreads over all of its segments.
 struct TableView {
   u32* words = nullptr;      // slot array
-  u64 cap = 0;               // power of two
+  u64 cap = 0;               // slots in use = nseg << seg_log2
   TableLayout L;
   unsigned long long* size = nullptr;   // device counter: occupied slots
   u32* overflow = nullptr;   // set when an insert finds no slot within probe_limit
-  u64 probe_limit = 0;       // min(cap, kMaxProbe)
+  u64 probe_limit = 0;       // min(segment slots, kMaxProbe)
+  int seg_log2 = 0;          // slots per segment = 2^seg_log2
+  int level = 0;             // 2^level <= nseg < 2^(level+1)
+  u64 split = 0;             // segments [0, split) of this level are split
 };
+
+XF_HD u64 table_home(const TableView& t, u64 h) {
+  const u64 hi = h >> t.seg_log2;
+  u64 b = hi & ((1ull << t.level) - 1);
+  if (b < t.split) b = hi & ((2ull << t.level) - 1);
+  return (b << t.seg_log2) | (h & ((1ull << t.seg_log2) - 1));
+}
+// the slot after s in its chain (wraps inside the segment)
+XF_HD u64 table_next(const TableView& t, u64 s) {
+  const u64 m = (1ull << t.seg_log2) - 1;
+  return (s & ~m) | ((s + 1) & m);
+}
 
 // Worker dedup table.  Persistent across steps: a key keeps its slot, so hot
 // keys are never re-inserted (no CAS storms on the skewed head of the key
@@ -535,9 +564,23 @@ class Backend {
   // keys a long run has accumulated but the current batches do not touch
   // (occupancy-realistic benchmarks).
   virtual void table_prefill(const TableView& t, int64_t n, u64 seed) = 0;
-  // Re-insert every live slot of `from` (key + state words) into the empty
-  // table `to` (a larger capacity); to.size counts the inserted keys.
-  virtual void table_rehash(const TableView& from, const TableView& to) = 0;
+  // Split segments [s0, s0 + k) of level t.level (t.split == s0 + k, i.e. t
+  // is the geometry AFTER the split; segments s0 + 2^level .. are mapped and
+  // cleared): a key whose home moved to the buddy segment goes there, the keys
+  // that stay are re-packed inside their cluster (no tombstones).  Table size
+  // is unchanged; slots of the split segments' keys change.
+  virtual void table_split(const TableView& t, u64 s0, u64 k) = 0;
+  // The slot array's address range: reserve the address space of max_bytes
+  // once, commit memory as the table grows.  table_commit(base, bytes) makes
+  // [base, base + bytes) usable and returns the (possibly moved) base: with
+  // virtual memory management the range stays in place and only the new tail
+  // gets memory; without it the backend re-allocates and copies (2x peak).
+  // (growable = false: the table never grows -- one plain allocation)
+  virtual void* table_reserve(size_t max_bytes, bool growable) = 0;
+  virtual void* table_commit(void* base, size_t bytes) = 0;
+  virtual void table_release(void* base) = 0;
+  // bytes of device memory committed to the table range (>= the bytes asked)
+  virtual size_t table_committed() const = 0;
   // AUC / logloss sums of n predictions (backend memory; labels 0/1 floats)
   virtual EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) = 0;
 };

@@ -34,14 +34,19 @@ struct EngineConfig {
   // Table capacity management (the reference's store is an unbounded
   // unordered_map, ftrl.h:54-56,84).  Before every inserting pull the engine
   // bounds the table's size from below-lagging device snapshots plus the
-  // inserts queued since (each at most the pull's key count); when the bound
-  // would pass grow_load * capacity the table is rehashed into 2x the slots
-  // (stream-ordered, the host is involved only then), up to 2^max_log2_cap.
+  // inserts queued since (each at most the pull's key count), and grows the
+  // table by segment splits (TableView, backend.h) on a schedule that keeps
+  // the fullest segments' load <= grow_load: with u = the load of a segment
+  // not yet split at this level, the first 2^level * (u - grow_start) /
+  // (grow_load - grow_start) segments are split.  A split is stream-ordered
+  // device work on one segment plus one new segment of memory -- no host
+  // sync, no copy of the table -- up to 2^max_log2_cap slots.
   // table_grow = false keeps the capacity fixed: an insert that finds no slot
   // flags the overflow, and the next step start raises within monitor_lag
   // steps of it.
   bool table_grow = true;
   double grow_load = 0.8;
+  double grow_start = 0.6;     // (< grow_load; else 3/4 of it)
   int max_log2_cap = 0;        // 0 => 31, and what the device's free memory allows
   // steps the host may run ahead of the device before it waits for a
   // snapshot (bounds both the growth bound's slack and fail-fast latency)
@@ -143,9 +148,20 @@ class Engine {
   uint64_t table_capacity() const { return table_.cap; }
   size_t table_bytes() const { return table_bytes_; }
   bool overflowed();
-  // capacity management (EngineConfig::table_grow): growths so far, host
-  // waits the monitor needed, and an explicit growth to 2^log2_cap slots
+  // capacity management (EngineConfig::table_grow): growths (split launches)
+  // and segments split so far, host waits the monitor needed, and an explicit
+  // growth to at least 2^log2_cap slots
   int64_t table_growths() const { return growths_; }
+  int64_t table_splits() const { return splits_; }
+  // geometry: {segment slots log2, level, split, segments}
+  std::vector<int64_t> table_geometry() const {
+    return {table_.seg_log2, table_.level, (int64_t)table_.split,
+            (int64_t)(table_.cap >> table_.seg_log2)};
+  }
+  // device bytes committed to the table's range (>= table_bytes())
+  size_t table_committed() const;
+  // seconds of host time the growth calls took (mapping + launches)
+  double grow_seconds() const { return grow_s_; }
   int64_t monitor_waits() const { return monitor_waits_; }
   // host seconds spent blocked on the monitor's run-ahead bound (the device
   // was monitor_lag steps behind): subtracted from the host's issue time
@@ -390,7 +406,9 @@ class Engine {
   int64_t known_size_ = 0;          // table size at the last consumed snapshot (or sync)
   int64_t known_adds_ = 0;          // cumulative insert bound queued before it
   int64_t queued_adds_ = 0;         // cumulative insert bound queued so far
-  int64_t growths_ = 0, monitor_waits_ = 0;
+  int64_t growths_ = 0, splits_ = 0, monitor_waits_ = 0;
+  double grow_s_ = 0.0;
+  u64 max_segs_ = 0;                // segments of 2^max_log2_cap slots
   double monitor_wait_s_ = 0.0;
   unsigned long long* rec_count_ = nullptr;  // (count_records) device counter
   u32* red_vmax_ = nullptr;                   // MVM: per-step fixed-point scale words [2]
@@ -403,6 +421,11 @@ class Engine {
   void poll_snapshots(int64_t wait_upto);
   void guard_inserts(int64_t n);   // before an inserting pull of <= n new keys
   void remap_server_slots();
+  // segment count the growth schedule (u0 = grow_start, u1 = grow_load) wants
+  u64 segments_for(double keys, double u0, double u1) const;
+  // load of the fullest segments at which growth stops pacing itself
+  static constexpr double kHardLoad = 0.9;
+  void split_to(u64 nseg);              // split segments until there are nseg
 
   u64* host_keys_dev_ = nullptr;   // push_host / pull_host staging
   float* host_vals_dev_ = nullptr;

@@ -1,8 +1,15 @@
 """Parameter-table capacity management (the reference's store is an unbounded
 unordered_map, /root/reference/src/optimizer/ftrl.h:54-56,84).
 
-* A table that starts small grows (2x rehash) before its load passes
-  grow_load, and the trained model is bitwise the one of a pre-sized table.
+* A table that starts small grows (segment splits, linear hashing over the
+  table's segments: TableView in csrc/include/xflow/backend.h) before its
+  load passes grow_load, and the trained model is bitwise the one of a
+  pre-sized table.
+* Splits of a populated table -- partial levels, wrapped clusters -- keep
+  every key and its state words, and lookups find them.
+* Growth queues device work only: a rank that grows in the middle of a
+  lock-step multi-rank run makes no host sync (its peers wait for nothing
+  but the split kernels).
 * A fixed table that fills up fails within monitor_lag steps, not at epoch
   end.
 * Growth in the middle of a staleness-k step re-probes the slots of the
@@ -147,3 +154,85 @@ def test_diverged_model_is_flagged(devname):
         for _ in range(4):
             e.train_step(to_batch(k, rp, fg, lab, dev))
     assert e.overflowed()
+
+
+def _rand_state(rng, n, words):
+    keys = np.unique(rng.integers(1, 1 << 62, size=n + n // 8, dtype=np.int64))[:n]
+    rng.shuffle(keys)
+    w = rng.integers(0, 1 << 20, size=(len(keys), words), dtype=np.int64).astype(np.uint32)
+    # state words as small positive floats (valid n / z accumulators)
+    w = (w.astype(np.float32) / (1 << 16)).view(np.uint32)
+    return keys.astype(np.uint64), w
+
+
+@pytest.mark.parametrize("devname", DEVICES)
+@pytest.mark.parametrize("kind", ["lr", "fm"])
+def test_segment_splits_keep_every_key(devname, kind):
+    """Chunks of imported (key, state) rows into a 2^12-slot table (one
+    segment): each chunk's guard splits segments of a populated table, level
+    after level and part-way through levels; after every chunk the export is
+    exactly the imported rows and every key's pulled weights equal those of
+    a pre-sized table holding the same rows."""
+    dev = _dev(devname)
+    mk = lambda cap: Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
+                            EngineConfig(table_log2_cap=cap, max_rows=256, max_nnz=4096), device=dev)
+    e, big = mk(12), mk(18)
+    rng = np.random.default_rng(11)
+    keys, words = _rand_state(rng, 40000, e.state_words)
+    done = 0
+    geoms = set()
+    for chunk in [2000, 1000, 500, 500, 1500, 3000, 3500, 8000, 20000]:
+        e.import_table(keys[done:done + chunk], words[done:done + chunk])
+        big.import_table(keys[done:done + chunk], words[done:done + chunk])
+        done += chunk
+        g = e.table_geometry
+        geoms.add((g["level"], g["split"]))
+        assert e.table_capacity == g["segments"] << g["seg_log2"]
+        assert e.table_size() == done and not e.overflowed()
+        ek, ew = e.export_table()
+        ew = ew.reshape(len(ek), -1)
+        o = np.argsort(ek)
+        ref = np.argsort(keys[:done])
+        np.testing.assert_array_equal(ek[o], keys[:done][ref])
+        np.testing.assert_array_equal(ew[o], words[:done][ref])
+        q = keys[:done]
+        np.testing.assert_array_equal(e.pull(q).view(np.uint32), big.pull(q).view(np.uint32))
+    assert e.table_splits >= 8 and e.table_growths >= 4
+    # some chunk ended part-way through a level (split != 0)
+    assert any(sp for _, sp in geoms)
+    assert done <= 0.8 * e.table_capacity
+
+
+def _sync_growth_worker(rank, world, out_dir, caps):
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    cap = caps[rank]
+    eng = Engine(ModelConfig(kind="fm", v_dim=4), OptimConfig(),
+                 EngineConfig(table_log2_cap=cap, max_rows=256, max_nnz=256 * 12))
+    sh = ShardedEngine(eng)
+    for step in range(10):
+        k, rp, fg, lab = _fresh_csr(256, 8, seed=300 * step + rank)
+        sh.train_step(to_batch(k, rp, fg, lab, torch.device("cpu")), S=1)
+    keys, _ = eng.export_table()
+    tag = "-".join(map(str, caps))
+    np.save(os.path.join(out_dir, f"k{rank}_{tag}.npy"), keys)
+    np.save(os.path.join(out_dir, f"v{rank}_{tag}.npy"), eng.pull(keys))
+    np.save(os.path.join(out_dir, f"g{rank}_{tag}.npy"),
+            np.array([eng.table_growths, eng.monitor_waits, eng.table_splits]))
+
+
+def test_one_rank_grows_mid_run_without_host_sync(tmp_path):
+    """gloo, 2 lock-step ranks: rank 0's shard starts at 2^10 slots and grows
+    several times mid-run, rank 1's is pre-sized.  The growing rank makes no
+    host wait for it (monitor_waits == 0: the split is queued device work),
+    and both shards equal a run where both are pre-sized, bit for bit."""
+    run_world(_sync_growth_worker, 2, str(tmp_path), (10, 16))
+    run_world(_sync_growth_worker, 2, str(tmp_path), (16, 16))
+    g0 = np.load(tmp_path / "g0_10-16.npy")
+    assert g0[0] >= 2 and g0[2] >= 2 and g0[1] == 0
+    for r in range(2):
+        ka, kb = np.load(tmp_path / f"k{r}_10-16.npy"), np.load(tmp_path / f"k{r}_16-16.npy")
+        oa, ob = np.argsort(ka), np.argsort(kb)
+        np.testing.assert_array_equal(ka[oa], kb[ob])
+        va, vb = np.load(tmp_path / f"v{r}_10-16.npy"), np.load(tmp_path / f"v{r}_16-16.npy")
+        np.testing.assert_array_equal(va[oa].view(np.uint32), vb[ob].view(np.uint32))

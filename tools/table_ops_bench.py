@@ -9,9 +9,10 @@ store's maintenance takes at the bench's occupancy.
             checkpoint writer's source, csrc/engine/engine.cpp)
 * save      the native shard file of a checkpoint (--save-dir; skipped when
             empty: a 1e9-key LR shard is 16 GB)
-* grow      a 2x rehash of a table prefilled to --grow-load (k_table_rehash;
-            the pause a run takes when the store outgrows its capacity,
-            EngineConfig.table_grow), at 2^--grow-log2 slots
+* grow      every segment of a table prefilled to --grow-load split once
+            (k_table_split_marks + k_table_split: the device work a run's
+            growth adds, spread over the steps by EngineConfig.grow_start),
+            at 2^--grow-log2 slots, for LR and FM-8 (--grow-kinds)
 
 Prints one JSON line of seconds and rates.  The reference keeps its weights
 in server RAM and never checkpoints or rehashes (ftrl.h:84,151).
@@ -45,12 +46,50 @@ def main():
     ap.add_argument("--grow-log2", type=int, default=28)
     ap.add_argument("--grow-load", type=float, default=0.75)
     ap.add_argument("--save-dir", default="")
+    ap.add_argument("--grow-kinds", default="lr,fm")
+    ap.add_argument("--grow-only", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cpu":
         a.log2_cap, a.keys, a.grow_log2 = min(a.log2_cap, 20), min(a.keys, 400_000), 18
     out = {"tool": "table_ops_bench", "device": str(dev)}
+    if not a.grow_only:
+        ops(a, dev, out)
+    for kind in a.grow_kinds.split(","):
+        out[f"grow_{kind}"] = grow(a, dev, kind)
+    print(json.dumps(out), flush=True)
 
+
+def grow(a, dev, kind):
+    """Split every segment of a 2^grow_log2-slot table at load grow_load once
+    (explicit grow_table: a whole level at once; a run spreads these splits
+    over its steps).  Device seconds, from synchronised wall clock."""
+    g = Engine(ModelConfig(kind=kind, v_dim=8), OptimConfig(),
+               EngineConfig(table_log2_cap=a.grow_log2, max_rows=1024, max_nnz=1024 * 39,
+                            max_log2_cap=a.grow_log2 + 1, grow_start=0.79, grow_load=0.8),
+               device=dev)
+    n = int(a.grow_load * (1 << a.grow_log2))
+    g.prefill(n)
+    _sync(dev)
+    assert g.table_growths == 0
+    t = time.perf_counter()
+    g.grow_table(a.grow_log2 + 1)
+    _sync(dev)
+    dt = time.perf_counter() - t
+    r = {"slots_from": 1 << a.grow_log2, "slots_to": g.table_capacity, "keys": g.table_size(),
+         "slot_bytes": g.state_words * 4 + 8, "segments_split": g.table_splits, "s": dt,
+         "ms_per_1e8_keys": dt * 1e3 / max(g.table_size(), 1) * 1e8,
+         "table_GB_to": g.table_capacity * (g.state_words * 4 + 8) / 1e9,
+         "committed_GB": g.table_committed / 1e9}
+    assert g.table_size() == n and g.table_capacity == 1 << (a.grow_log2 + 1)
+    assert not g.overflowed()
+    del g
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return r
+
+
+def ops(a, dev, out):
     e = Engine(ModelConfig(kind="lr"), OptimConfig(),
                EngineConfig(table_log2_cap=a.log2_cap, max_rows=1024, max_nnz=1024 * 39,
                             table_grow=False), device=dev)
@@ -105,22 +144,6 @@ def main():
         del g0
     if dev.type == "cuda":
         torch.cuda.empty_cache()
-
-    g = Engine(ModelConfig(kind="lr"), OptimConfig(),
-               EngineConfig(table_log2_cap=a.grow_log2, max_rows=1024, max_nnz=1024 * 39,
-                            max_log2_cap=a.grow_log2 + 1), device=dev)
-    n = int(a.grow_load * (1 << a.grow_log2))
-    g.prefill(n)
-    _sync(dev)
-    t = time.perf_counter()
-    g.grow_table(a.grow_log2 + 1)
-    _sync(dev)
-    out["grow_s"] = time.perf_counter() - t
-    out["grow_keys"] = g.table_size()
-    out["grow_from_slots"] = 1 << a.grow_log2
-    out["grow_Mkeys_per_s"] = g.table_size() / 1e6 / max(out["grow_s"], 1e-9)
-    assert g.table_size() == n and g.table_capacity == 1 << (a.grow_log2 + 1)
-    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

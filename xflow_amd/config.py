@@ -89,11 +89,13 @@ class EngineConfig:
     sum_slices: bool = False      # one push of Σ_s g_s instead of ordered per-slice pushes
     scratch_factor: float = 2.5
     # table capacity management (csrc/include/xflow/engine.h EngineConfig):
-    # grow 2x before the load could pass grow_load, up to 2^max_log2_cap
-    # (0: 2^31 or what free HBM allows); table_grow=False keeps it fixed and
-    # an overflow raises within monitor_lag steps
+    # grow by segment splits (linear hashing) on a schedule that starts when
+    # the fullest segments pass grow_start and keeps them <= grow_load, up to
+    # 2^max_log2_cap slots (0: 2^31 or what free HBM allows); table_grow=False
+    # keeps it fixed and an overflow raises within monitor_lag steps
     table_grow: bool = True
     grow_load: float = 0.8
+    grow_start: float = 0.6
     max_log2_cap: int = 0
     monitor_lag: int = 2
     # owner apply of a multi-source sharded step on the GPU: 0 one launch per

@@ -142,7 +142,8 @@ class Engine:
                            sum_slices=self.cfg.sum_slices, scratch_factor=self.cfg.scratch_factor,
                            device=_device_index(self.device), table_grow=self.cfg.table_grow,
                            grow_load=self.cfg.grow_load, max_log2_cap=self.cfg.max_log2_cap,
-                           monitor_lag=self.cfg.monitor_lag, owner_group=self.cfg.owner_group)
+                           monitor_lag=self.cfg.monitor_lag, owner_group=self.cfg.owner_group,
+                           grow_start=self.cfg.grow_start)
         if self.is_gpu != (self.device.type == "cuda"):
             raise RuntimeError("native engine backend does not match the requested device")
 
@@ -325,8 +326,29 @@ class Engine:
 
     @property
     def table_growths(self) -> int:
-        """Times the table was rehashed into 2x the slots."""
+        """Times the table grew (each: one or more segment splits)."""
         return int(self._e.table_growths)
+
+    @property
+    def table_splits(self) -> int:
+        """Segments split so far (each added one segment of memory)."""
+        return int(self._e.table_splits)
+
+    @property
+    def table_geometry(self) -> dict:
+        """{seg_log2, level, split, segments} (TableView, csrc/include/xflow/backend.h)."""
+        g, lv, sp, ns = self._e.table_geometry
+        return {"seg_log2": int(g), "level": int(lv), "split": int(sp), "segments": int(ns)}
+
+    @property
+    def table_committed(self) -> int:
+        """Device bytes committed to the table's address range."""
+        return int(self._e.table_committed)
+
+    @property
+    def grow_seconds(self) -> float:
+        """Host seconds spent in growth calls (memory mapping + split launches)."""
+        return float(self._e.grow_seconds)
 
     @property
     def monitor_waits(self) -> int:
@@ -362,7 +384,8 @@ class Engine:
         return float(self._e.monitor_wait_seconds)
 
     def grow_table(self, log2_cap: int) -> None:
-        """Rehash the table into 2^log2_cap slots now (normally automatic)."""
+        """Grow the table to >= 2^log2_cap slots now by segment splits (normally
+        automatic)."""
         self._sync_stream()
         self._e.grow_table(int(log2_cap))
 
