@@ -18,6 +18,7 @@
 #include <string>
 
 #include "../comm/rccl_comm.h"
+#include "../comm/sharded_step.h"
 #include "xflow/engine.h"
 #include "xflow/reader.h"
 #include "xflow/trainer.h"
@@ -220,6 +221,39 @@ PYBIND11_MODULE(_xflow_native, m) {
              c.send_recv(peers, sends, send_bytes, recvs, recv_bytes, stream);
            })
       .def("abort", &RcclComm::abort);
+
+  py::class_<ShardedStep>(m, "ShardedStep")
+      .def(py::init([](Engine& e, RcclComm* comm, int world, int rank, bool early_keys) {
+             return new ShardedStep(e, comm, world, rank, early_keys);
+           }),
+           py::arg("engine"), py::arg("comm"), py::arg("world"), py::arg("rank"),
+           py::arg("early_keys") = true, py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("train_step",
+           [](ShardedStep& s, const BatchView& b, int64_t id, int S, py::object next,
+              int64_t next_id) {
+             BatchView nv;
+             const bool has = !next.is_none();
+             if (has) nv = next.cast<BatchView>();
+             py::gil_scoped_release nogil;
+             return s.train_step(b, id, S, has ? &nv : nullptr, next_id);
+           },
+           py::arg("batch"), py::arg("id"), py::arg("S"), py::arg("next") = py::none(),
+           py::arg("next_id") = 0)
+      .def("eval_step",
+           [](ShardedStep& s, const BatchView& b, uintptr_t pctr) {
+             return s.eval_step(b, P<float>(pctr));
+           },
+           py::call_guard<py::gil_scoped_release>())
+      .def_readwrite("host_waits", &ShardedStep::host_waits)
+      .def_readwrite("mid_step_waits", &ShardedStep::mid_step_waits)
+      .def_readwrite("early_key_exchanges", &ShardedStep::early_key_exchanges)
+      .def_readwrite("inline_prepares", &ShardedStep::inline_prepares)
+      .def_readwrite("empty_steps", &ShardedStep::empty_steps)
+      .def_readwrite("bytes_moved", &ShardedStep::bytes_moved)
+      .def_readwrite("drop_exchanges", &ShardedStep::drop_exchanges)
+      .def_readwrite("host_wait_s", &ShardedStep::host_wait_s)
+      .def_readonly("last_send", &ShardedStep::last_send)
+      .def_readonly("last_recv", &ShardedStep::last_recv);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,

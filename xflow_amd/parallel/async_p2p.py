@@ -45,6 +45,8 @@ _SRV_BUFS = 8  # server buffers of the native engine (Engine::kSrvBufs)
 
 
 class AsyncShardedEngine(ShardedEngine):
+    _native_ok = False  # (the staleness-k step stays in Python)
+
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
                  staleness: int = 1, **kw):
         if not 1 <= int(staleness) <= _SRV_BUFS - 1:

@@ -69,6 +69,24 @@ class _Buf:
         return self.t[:n]
 
 
+def _native_counter(name: str):
+    """A step counter kept by the native step when it runs (ShardedStep in
+    csrc/comm/sharded_step.h), else on the Python object."""
+
+    def fget(self):
+        n = self.__dict__.get("_native")
+        return getattr(n, name) if n is not None else self.__dict__.get("_c_" + name, 0)
+
+    def fset(self, v):
+        n = self.__dict__.get("_native")
+        if n is not None:
+            setattr(n, name, v)
+        else:
+            self.__dict__["_c_" + name] = v
+
+    return property(fget, fset)
+
+
 class ShardedEngine:
     """Runs Engine phases with sparse all-to-alls between them.
 
@@ -80,7 +98,27 @@ class ShardedEngine:
     ago (it sits ahead of the current step's forward/backward, gradient
     exchange and apply in the queue): the host never waits on an in-flight
     exchange and stays about one step ahead of the device.  Without
-    next_batch a step prepares its own batch first (one host wait per step)."""
+    next_batch a step prepares its own batch first (one host wait per step).
+
+    Native step: with the native RCCL communicator (or the world-1
+    self-exchange) the whole step -- split decoding, op lists, group calls,
+    applies -- runs in C++ (csrc/comm/sharded_step.cpp, one call per step;
+    XFLOW_NATIVE_STEP=0 keeps it in Python).  The methods below are the same
+    step for the torch.distributed transport, and the specification the
+    native one follows (tests/test_native_sharded.py)."""
+
+    # steps the native implementation may run (the staleness-k subclass: no)
+    _native_ok = True
+    host_waits = _native_counter("host_waits")
+    mid_step_waits = _native_counter("mid_step_waits")
+    host_wait_s = _native_counter("host_wait_s")
+    early_key_exchanges = _native_counter("early_key_exchanges")
+    inline_prepares = _native_counter("inline_prepares")
+    empty_steps = _native_counter("empty_steps")
+    bytes_moved = _native_counter("bytes_moved")
+    drop_exchanges = _native_counter("drop_exchanges")
+    last_send = _native_counter("last_send")
+    last_recv = _native_counter("last_recv")
 
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
                  world: Optional[int] = None, rank: Optional[int] = None,
@@ -143,9 +181,26 @@ class ShardedEngine:
         self._prep_seq = [0, 0]    # sequence number of each worker set's batch
         self._next_wb = 0
         self._comm = None
+        self.__dict__["_native"] = None
         self.transport = "custom"
         if not custom:
             self._init_transport(transport)
+            self._init_native()
+
+    def _init_native(self) -> None:
+        if not self._native_ok or os.environ.get("XFLOW_NATIVE_STEP", "1") == "0":
+            return
+        if self._comm is None and not (self.world == 1 and self.self_exchange == "alias"):
+            return
+        from xflow_amd import native
+
+        self.__dict__["_native"] = native.load().ShardedStep(
+            self.engine._e, self._comm, self.world, self.rank, self.early_keys)
+
+    @property
+    def native_step(self) -> bool:
+        """True when train_step / eval_step run in C++ (ShardedStep)."""
+        return self._native is not None
 
     # ---- transport ----------------------------------------------------------
     def _init_transport(self, transport: str) -> None:
@@ -372,6 +427,16 @@ class ShardedEngine:
         same counts, so all of them stop at the same step."""
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
+        if self._native is not None:
+            batch.check(e.device)
+            if next_batch is not None:
+                next_batch.check(e.device)
+            e._sync_stream()
+            if prefetch is not None:  # (produces next_batch: before its prepare)
+                prefetch()
+            return bool(self._native.train_step(
+                batch.view(), id(batch), S, next_batch.view() if next_batch is not None else None,
+                id(next_batch) if next_batch is not None else 0))
         ps = e.value_width  # floats per pulled value row
         ordered_masks = S > 1 and not e.cfg.sum_slices
         ahead = self._ahead
@@ -487,6 +552,13 @@ class ShardedEngine:
         returns None on every rank when no rank had rows (the counts exchange
         says so: the evaluation loop's end, without another collective)."""
         e = self.engine
+        if self._native is not None:
+            batch.check(e.device)
+            if pctr is None:
+                pctr = torch.empty(batch.rows, dtype=torch.float32, device=e.device)
+            e._sync_stream()
+            ok = self._native.eval_step(batch.view(), pctr.data_ptr() if batch.rows else 0)
+            return pctr if ok else None
         # (keys exchanged ahead for a training batch no step will take now:
         # every rank drops them at the same point)
         self._ahead = None
@@ -505,7 +577,10 @@ class ShardedEngine:
         return pctr
 
     def close(self) -> None:
-        """Release the native communicator (before the process group goes)."""
-        if self._comm is not None:
-            torch.cuda.synchronize(self.engine.device)
+        """Release the native step and communicator (before the process group
+        goes)."""
+        if self._native is not None or self._comm is not None:
+            if self.engine.is_gpu:
+                torch.cuda.synchronize(self.engine.device)
+            self.__dict__["_native"] = None
             self._comm = None
