@@ -122,10 +122,15 @@ void ShardedStep::prepare(const BatchView& b, int64_t id, bool exchange) {
   }
 }
 
-ShardedStep::Split ShardedStep::take(const BatchView& b, int64_t id, bool mid_step) {
+ShardedStep::Split ShardedStep::take(const BatchView& b, int64_t id, bool mid_step,
+                                     const std::function<void()>* prefetch) {
   if (!prep_valid_ || prep_id_ != id) {
     ++inline_prepares;
     prepare(b, id, true);
+    if (prefetch && *prefetch) {  // device work to overlap the split-size round trip
+      (*prefetch)();
+      prefetch = nullptr;
+    }
   }
   prep_valid_ = false;
   Split sp;
@@ -192,7 +197,8 @@ void ShardedStep::apply_groups(const u64* recv_keys, const std::vector<const flo
 }
 
 bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchView* next,
-                             int64_t next_id) {
+                             int64_t next_id, const std::function<void()>& prefetch) {
+  bool prefetched = false;
   const int ps = e_.value_width();
   const bool ordered_masks = S > 1 && !e_.config().sum_slices;
   const Ahead ah = ahead_;
@@ -204,7 +210,9 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
     last_send = ah.n_send;
     last_recv = ah.n_recv;
   } else {
-    sp = take(b, id, false);
+    const bool inline_prep = !prep_valid_ || prep_id_ != id;
+    sp = take(b, id, false, &prefetch);
+    prefetched = inline_prep && prefetch;
   }
   if (!sp.any) {
     ++empty_steps;
@@ -227,6 +235,7 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
   const int ngroups = Engine::slice_groups(S);
   float* vals = static_cast<float*>(get(vals_, sizeof(float) * (size_t)(n_recv * ps)));
   e_.s_pull(recv_keys, n_recv, vals, true, 0, offsets, ngroups > 1);
+  if (prefetch && !prefetched) prefetch();
   const bool alias = self_only();
   float* pulled = alias ? vals : static_cast<float*>(get(pulled_, sizeof(float) * (size_t)(n_send * ps)));
   std::vector<RcclComm::A2AOp> ops;

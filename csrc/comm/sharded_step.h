@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "rccl_comm.h"
@@ -38,7 +39,10 @@ class ShardedStep {
   // train (prepared and, with early keys, its keys exchanged here), or null.
   // S: slices per step (identical on every rank).  Returns false, having
   // done nothing, when no rank had data for b.
-  bool train_step(const BatchView& b, int64_t id, int S, const BatchView* next, int64_t next_id);
+  // prefetch (optional): called once the step's pull is queued -- device work
+  // producing `next` (e.g. the synthetic generator), which its prepare follows
+  bool train_step(const BatchView& b, int64_t id, int S, const BatchView* next, int64_t next_id,
+                  const std::function<void()>& prefetch = nullptr);
   // Forward-only step (keys looked up, never inserted) writing pctr (may be
   // null when b has no rows); false when no rank had rows.
   bool eval_step(const BatchView& b, float* pctr);
@@ -47,7 +51,7 @@ class ShardedStep {
   // was still in flight at a step start / in the middle of a step, the host
   // seconds those waits took, steps whose next keys rode with the gradients,
   // steps that prepared their own batch, steps no rank had data for, bytes
-  // sent + received, host seconds inside train_step net of the waits
+  // sent + received
   int64_t host_waits = 0, mid_step_waits = 0, early_key_exchanges = 0, inline_prepares = 0,
           empty_steps = 0, bytes_moved = 0, drop_exchanges = 0;
   double host_wait_s = 0.0;
@@ -76,7 +80,8 @@ class ShardedStep {
   void prepare(const BatchView& b, int64_t id, bool exchange);
   RcclComm::A2AOp counts_op(int wb);
   void counts_sent(int wb);
-  Split take(const BatchView& b, int64_t id, bool mid_step);
+  Split take(const BatchView& b, int64_t id, bool mid_step,
+             const std::function<void()>* prefetch = nullptr);
   void a2a_group(std::vector<RcclComm::A2AOp>& ops);
   void apply_groups(const u64* recv_keys, const std::vector<const float*>& grads,
                     const std::vector<const u32*>& masks, const std::vector<int>& group_S,

@@ -230,15 +230,26 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("early_keys") = true, py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
       .def("train_step",
            [](ShardedStep& s, const BatchView& b, int64_t id, int S, py::object next,
-              int64_t next_id) {
+              int64_t next_id, py::object prefetch) {
              BatchView nv;
              const bool has = !next.is_none();
              if (has) nv = next.cast<BatchView>();
-             py::gil_scoped_release nogil;
-             return s.train_step(b, id, S, has ? &nv : nullptr, next_id);
+             std::function<void()> pf;
+             if (!prefetch.is_none()) {
+               pf = [prefetch]() {
+                 py::gil_scoped_acquire gil;
+                 prefetch();
+               };
+             }
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = s.train_step(b, id, S, has ? &nv : nullptr, next_id, pf);
+             }
+             return ok;
            },
            py::arg("batch"), py::arg("id"), py::arg("S"), py::arg("next") = py::none(),
-           py::arg("next_id") = 0)
+           py::arg("next_id") = 0, py::arg("prefetch") = py::none())
       .def("eval_step",
            [](ShardedStep& s, const BatchView& b, uintptr_t pctr) {
              return s.eval_step(b, P<float>(pctr));

@@ -37,9 +37,14 @@ def _worker(rank, world, out_dir, kind, slices, pipelined, native):
                for step in range(STEPS)]
     test = to_batch(*random_csr(ROWS, FIELDS, VOCAB, seed=999), dev)
     preds = []
+    calls = [0]
+
+    def prefetch():  # (the caller's device work producing the next batch)
+        calls[0] += 1
+
     for step in range(STEPS):
         nxt = batches[step + 1] if pipelined and step + 1 < STEPS else None
-        assert sh.train_step(batches[step], S=slices, next_batch=nxt)
+        assert sh.train_step(batches[step], S=slices, next_batch=nxt, prefetch=prefetch)
         if step == 1:  # an evaluation between training steps
             preds.append(sh.eval_step(test).numpy().copy())
     preds.append(sh.eval_step(test).numpy().copy())
@@ -56,7 +61,7 @@ def _worker(rank, world, out_dir, kind, slices, pipelined, native):
     np.save(os.path.join(out_dir, f"stats_{tag}.npy"), np.array([st["rows"], st["ln_loss"]]))
     np.save(os.path.join(out_dir, f"preds_{tag}.npy"), np.stack(preds))
     np.save(os.path.join(out_dir, f"counters_{tag}.npy"),
-            np.array([sh.inline_prepares, sh.empty_steps, sh.bytes_moved]))
+            np.array([sh.inline_prepares, sh.empty_steps, sh.bytes_moved, calls[0]]))
 
 
 @pytest.mark.parametrize("kind,slices,pipelined",

@@ -190,12 +190,15 @@ class ShardedEngine:
     def _init_native(self) -> None:
         if not self._native_ok or os.environ.get("XFLOW_NATIVE_STEP", "1") == "0":
             return
-        if self._comm is None and not (self.world == 1 and self.self_exchange == "alias"):
+        alias = self.world == 1 and self.self_exchange == "alias"
+        if self._comm is None and not alias:
             return
         from xflow_amd import native
 
+        # (world 1, aliased: no communicator -- the owner reads the send
+        # buffers in place, as _self_only)
         self.__dict__["_native"] = native.load().ShardedStep(
-            self.engine._e, self._comm, self.world, self.rank, self.early_keys)
+            self.engine._e, None if alias else self._comm, self.world, self.rank, self.early_keys)
 
     @property
     def native_step(self) -> bool:
@@ -432,11 +435,10 @@ class ShardedEngine:
             if next_batch is not None:
                 next_batch.check(e.device)
             e._sync_stream()
-            if prefetch is not None:  # (produces next_batch: before its prepare)
-                prefetch()
+            # (prefetch: called back once the pull is queued, as below)
             return bool(self._native.train_step(
                 batch.view(), id(batch), S, next_batch.view() if next_batch is not None else None,
-                id(next_batch) if next_batch is not None else 0))
+                id(next_batch) if next_batch is not None else 0, prefetch))
         ps = e.value_width  # floats per pulled value row
         ordered_masks = S > 1 and not e.cfg.sum_slices
         ahead = self._ahead
