@@ -8,8 +8,20 @@
 
 namespace xflow {
 
-ShardedStep::ShardedStep(Engine& e, RcclComm* comm, int world, int rank, bool early_keys)
-    : e_(e), comm_(comm), world_(world), rank_(rank), early_keys_(early_keys) {
+ShardedStep::ShardedStep(Engine& e, RcclComm* comm, int world, int rank, bool early_keys,
+                         int staleness)
+    : e_(e), comm_(comm), world_(world), rank_(rank), early_keys_(early_keys),
+      staleness_(staleness) {
+  if (staleness < 0 || staleness > 3) throw std::invalid_argument("ShardedStep: staleness in [0, 3]");
+  if (staleness > 0) {
+    const int nbuf = staleness + 1;  // step t's buffers live until its apply at step t+k
+    rk_.resize(nbuf);
+    vals_k_.resize(nbuf);
+    gin_k_.assign(nbuf, std::vector<Buf>(1));
+    gout_k_.assign(nbuf, std::vector<Buf>(1));
+    min_k_.assign(nbuf, std::vector<Buf>(1));
+    mout_k_.assign(nbuf, std::vector<Buf>(1));
+  }
   if (world < 1 || rank < 0 || rank >= world) throw std::invalid_argument("ShardedStep: bad world/rank");
   if (!comm && world != 1)
     throw std::invalid_argument("ShardedStep: world > 1 needs a communicator");
@@ -40,8 +52,11 @@ ShardedStep::~ShardedStep() {
     be.event_destroy(counts_ready_[i]);
   }
   std::vector<Buf*> all = {&recv_keys_, &vals_, &pulled_, &ahead_keys_[0], &ahead_keys_[1]};
-  for (auto* v : {&grads_out_, &grads_in_, &masks_out_, &masks_in_})
+  for (auto* v : {&grads_out_, &grads_in_, &masks_out_, &masks_in_, &rk_, &vals_k_})
     for (Buf& b : *v) all.push_back(&b);
+  for (auto* vv : {&gin_k_, &gout_k_, &min_k_, &mout_k_})
+    for (auto& v : *vv)
+      for (Buf& b : v) all.push_back(&b);
   for (Buf* b : all)
     if (b->p) be.free(b->p);
 }
@@ -180,9 +195,9 @@ ShardedStep::Split ShardedStep::take(const BatchView& b, int64_t id, bool mid_st
 
 void ShardedStep::apply_groups(const u64* recv_keys, const std::vector<const float*>& grads,
                                const std::vector<const u32*>& masks, const std::vector<int>& group_S,
-                               const std::vector<int64_t>& offsets) {
+                               const std::vector<int64_t>& offsets, int buf) {
   if (grads.size() == 1) {
-    e_.s_apply(recv_keys, grads[0], masks[0], offsets, group_S[0], 0);
+    e_.s_apply(recv_keys, grads[0], masks[0], offsets, group_S[0], buf);
     return;
   }
   // several slice groups: the pushes go in (source, slice) order -- source by
@@ -192,12 +207,14 @@ void ShardedStep::apply_groups(const u64* recv_keys, const std::vector<const flo
     if (offsets[src + 1] <= offsets[src]) continue;
     std::vector<int64_t> offs(W + 1);
     for (int i = 0; i <= W; ++i) offs[i] = i <= src ? offsets[src] : offsets[src + 1];
-    for (size_t g = 0; g < grads.size(); ++g) e_.s_apply(recv_keys, grads[g], masks[g], offs, group_S[g], 0);
+    for (size_t g = 0; g < grads.size(); ++g)
+      e_.s_apply(recv_keys, grads[g], masks[g], offs, group_S[g], buf);
   }
 }
 
 bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchView* next,
                              int64_t next_id, const std::function<void()>& prefetch) {
+  if (staleness_ > 0) return train_step_async(b, id, S, next, next_id, prefetch);
   bool prefetched = false;
   const int ps = e_.value_width();
   const bool ordered_masks = S > 1 && !e_.config().sum_slices;
@@ -305,7 +322,117 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
   return true;
 }
 
+void ShardedStep::push_ops(const Pending& p, std::vector<RcclComm::A2AOp>& ops) {
+  // gradients (+ slice masks) to their owners: the reverse of the step's key
+  // exchange, one pair per slice group
+  const int gw = e_.grad_width();
+  for (const PendGroup& g : p.groups) {
+    ops.push_back({g.gout, p.send, g.gin, p.recv, (int)sizeof(float) * g.S * gw});
+    if (g.min) ops.push_back({g.mout, p.send, g.min, p.recv, (int)sizeof(u32)});
+  }
+}
+
+void ShardedStep::apply_pending(const Pending& p) {
+  std::vector<const float*> g;
+  std::vector<const u32*> m;
+  std::vector<int> gs;
+  for (const PendGroup& x : p.groups) {
+    g.push_back(x.gin);
+    m.push_back(x.min);
+    gs.push_back(x.S);
+  }
+  apply_groups(p.rk, g, m, gs, p.offsets, p.buf);
+}
+
+// The staleness-k step (AsyncShardedEngine.train_step): step t-k's pushes
+// ride in the group call of step t's keys and land after step t's pull.
+bool ShardedStep::train_step_async(const BatchView& b, int64_t id, int S, const BatchView* next,
+                                   int64_t next_id, const std::function<void()>& prefetch) {
+  const int ps = e_.value_width(), gw = e_.grad_width();
+  const bool ordered_masks = S > 1 && !e_.config().sum_slices;
+  const bool inline_prep = !prep_valid_ || prep_id_ != id;
+  Split sp = take(b, id, false, &prefetch);
+  const bool prefetched = inline_prep && prefetch;
+  if (!sp.any) {
+    ++empty_steps;
+    return false;
+  }
+  const int buf = (int)(step_no_ % (staleness_ + 1));
+  const int64_t n_send = last_send, n_recv = last_recv;
+  const bool alias = self_only();
+  // this step's received keys stay alive until its pushes are applied
+  u64* rk = static_cast<u64*>(get(rk_[buf], sizeof(u64) * (size_t)n_recv));
+  std::vector<RcclComm::A2AOp> ops;
+  ops.push_back({send_keys_[sp.wb], sp.send, rk, sp.recv, (int)sizeof(u64)});
+  const bool due = (int)pending_.size() == staleness_;
+  if (due && !alias) push_ops(pending_.front(), ops);  // step t-k's pushes ride with step t's keys
+  a2a_group(ops);
+  if (due) ++p2p_ops;
+  const std::vector<int64_t> offsets = offsets_of(sp.recv);
+  float* vals = static_cast<float*>(get(vals_k_[buf], sizeof(float) * (size_t)(n_recv * ps)));
+  // (applied after the next k pulls: keep the pulled weights)
+  e_.s_pull(rk, n_recv, vals, true, buf, offsets, true);
+  if (prefetch && !prefetched) prefetch();
+  float* pulled = alias ? vals : static_cast<float*>(get(pulled_, sizeof(float) * (size_t)(n_send * ps)));
+  ops.clear();
+  if (!alias) ops.push_back({vals, sp.recv, pulled, sp.send, (int)sizeof(float) * ps});
+  if (next) {
+    prepare(*next, next_id, false);
+    if (!alias) ops.push_back(counts_op(prep_wb_));
+  }
+  a2a_group(ops);
+  if (next && !alias) counts_sent(prep_wb_);
+  // staleness k: step t-k's pushes land after this step's pull
+  if (due) {
+    apply_pending(pending_.front());
+    pending_.pop_front();
+  }
+  const int ngroups = Engine::slice_groups(S);
+  for (auto* vv : {&gin_k_, &gout_k_, &min_k_, &mout_k_})
+    if ((int)(*vv)[buf].size() < ngroups) (*vv)[buf].resize(ngroups);
+  Pending p;
+  for (int k = 0; k < ngroups; ++k) {
+    const int Sg = Engine::group_slices(S, k);
+    const int Wd = Sg * gw;
+    const bool om = ordered_masks && Sg > 1;
+    float* go = static_cast<float*>(get(gout_k_[buf][k], sizeof(float) * (size_t)(n_send * Wd)));
+    u32* mo = om ? static_cast<u32*>(get(mout_k_[buf][k], sizeof(u32) * (size_t)n_send)) : nullptr;
+    e_.w_forward_backward(b, pulled, n_send, go, mo, S, sp.wb, k);
+    float* gi = go;
+    u32* mi = mo;
+    if (!alias) {  // (world 1: the owner reads the pushes in place)
+      gi = static_cast<float*>(get(gin_k_[buf][k], sizeof(float) * (size_t)(n_recv * Wd)));
+      mi = om ? static_cast<u32*>(get(min_k_[buf][k], sizeof(u32) * (size_t)n_recv)) : nullptr;
+    }
+    p.groups.push_back({gi, go, mi, mo, Sg});
+  }
+  p.rk = rk;
+  p.send = sp.send;
+  p.recv = sp.recv;
+  p.offsets = offsets;
+  p.buf = buf;
+  pending_.push_back(std::move(p));
+  ++step_no_;
+  e_.w_finish();
+  bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * (int64_t)S * gw);
+  return true;
+}
+
+void ShardedStep::flush() {
+  while (!pending_.empty()) {
+    if (!self_only()) {
+      std::vector<RcclComm::A2AOp> ops;
+      push_ops(pending_.front(), ops);
+      a2a_group(ops);
+    }
+    ++p2p_ops;
+    apply_pending(pending_.front());
+    pending_.pop_front();
+  }
+}
+
 bool ShardedStep::eval_step(const BatchView& b, float* pctr) {
+  flush();
   // (keys exchanged ahead for a training batch no step will take now: every
   // rank drops them at the same point)
   ahead_.valid = false;

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <vector>
 
@@ -29,7 +30,11 @@ class ShardedStep {
  public:
   // comm: null for world 1 (self-exchange aliased: the owner reads the send
   // buffers in place); otherwise the job's verified communicator.
-  ShardedStep(Engine& e, RcclComm* comm, int world, int rank, bool early_keys);
+  // staleness k > 0: the bounded-staleness step (xflow_amd/parallel/
+  // async_p2p.py AsyncShardedEngine): a step's pushes are exchanged with the
+  // keys of step t+k and applied after that step's pull.
+  ShardedStep(Engine& e, RcclComm* comm, int world, int rank, bool early_keys,
+              int staleness = 0);
   ~ShardedStep();
   ShardedStep(const ShardedStep&) = delete;
   ShardedStep& operator=(const ShardedStep&) = delete;
@@ -46,6 +51,9 @@ class ShardedStep {
   // Forward-only step (keys looked up, never inserted) writing pctr (may be
   // null when b has no rows); false when no rank had rows.
   bool eval_step(const BatchView& b, float* pctr);
+  // staleness k: exchange and apply every pending push in step order (before
+  // evaluation / checkpoints; every rank calls it)
+  void flush();
 
   // host-side counters (see ShardedEngine): reads of split sizes whose copy
   // was still in flight at a step start / in the middle of a step, the host
@@ -56,6 +64,7 @@ class ShardedStep {
           empty_steps = 0, bytes_moved = 0, drop_exchanges = 0;
   double host_wait_s = 0.0;
   int64_t last_send = 0, last_recv = 0;
+  int64_t p2p_ops = 0;  // staleness k: push exchanges so far
 
  private:
   struct Buf {  // grow-only device buffer
@@ -66,6 +75,19 @@ class ShardedStep {
     int wb = 0;
     std::vector<int64_t> send, recv;
     bool any = false;
+  };
+  struct PendGroup {  // one slice group's pushes of a pending step
+    float* gin;
+    float* gout;
+    u32* min;
+    u32* mout;
+    int S;
+  };
+  struct Pending {  // a staleness-k step whose pushes are not applied yet
+    u64* rk = nullptr;
+    std::vector<PendGroup> groups;
+    std::vector<int64_t> send, recv, offsets;
+    int buf = 0;
   };
   struct Ahead {  // a prepared batch whose keys were already received
     bool valid = false;
@@ -85,7 +107,11 @@ class ShardedStep {
   void a2a_group(std::vector<RcclComm::A2AOp>& ops);
   void apply_groups(const u64* recv_keys, const std::vector<const float*>& grads,
                     const std::vector<const u32*>& masks, const std::vector<int>& group_S,
-                    const std::vector<int64_t>& offsets);
+                    const std::vector<int64_t>& offsets, int buf = 0);
+  bool train_step_async(const BatchView& b, int64_t id, int S, const BatchView* next,
+                        int64_t next_id, const std::function<void()>& prefetch);
+  void push_ops(const Pending& p, std::vector<RcclComm::A2AOp>& ops);
+  void apply_pending(const Pending& p);
   static std::vector<int64_t> offsets_of(const std::vector<int64_t>& splits);
   uintptr_t stream() const;
 
@@ -105,6 +131,14 @@ class ShardedStep {
   int64_t prep_id_ = 0;
   int prep_wb_ = 0;
   Ahead ahead_;
+  // staleness k (> 0): per step buffer (k + 1 of them) the received keys,
+  // pulled values and per-group gradient / mask buffers, and the queue of
+  // steps whose pushes are pending
+  int staleness_ = 0;
+  int64_t step_no_ = 0;
+  std::vector<Buf> rk_, vals_k_;
+  std::vector<std::vector<Buf>> gin_k_, gout_k_, min_k_, mout_k_;
+  std::deque<Pending> pending_;
 };
 
 }  // namespace xflow

@@ -223,11 +223,15 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def("abort", &RcclComm::abort);
 
   py::class_<ShardedStep>(m, "ShardedStep")
-      .def(py::init([](Engine& e, RcclComm* comm, int world, int rank, bool early_keys) {
-             return new ShardedStep(e, comm, world, rank, early_keys);
+      .def(py::init([](Engine& e, RcclComm* comm, int world, int rank, bool early_keys,
+                       int staleness) {
+             return new ShardedStep(e, comm, world, rank, early_keys, staleness);
            }),
            py::arg("engine"), py::arg("comm"), py::arg("world"), py::arg("rank"),
-           py::arg("early_keys") = true, py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+           py::arg("early_keys") = true, py::arg("staleness") = 0, py::keep_alive<1, 2>(),
+           py::keep_alive<1, 3>())
+      .def("flush", &ShardedStep::flush, py::call_guard<py::gil_scoped_release>())
+      .def_readwrite("p2p_ops", &ShardedStep::p2p_ops)
       .def("train_step",
            [](ShardedStep& s, const BatchView& b, int64_t id, int S, py::object next,
               int64_t next_id, py::object prefetch) {

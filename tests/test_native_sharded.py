@@ -22,15 +22,16 @@ from xflow_amd.engine import Batch, Engine
 ROWS, FIELDS, VOCAB, STEPS = 120, 6, 90, 4
 
 
-def _worker(rank, world, out_dir, kind, slices, pipelined, native):
+def _worker(rank, world, out_dir, kind, slices, pipelined, native, staleness=0):
     os.environ["XFLOW_NATIVE_STEP"] = "1" if native else "0"
+    from xflow_amd.parallel.async_p2p import AsyncShardedEngine
     from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
     dev = torch.device("cpu")
     eng = Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
                  EngineConfig(table_log2_cap=14, max_rows=ROWS, max_nnz=ROWS * 16,
                               max_slices=slices))
-    sh = ShardedEngine(eng)
+    sh = AsyncShardedEngine(eng, staleness=staleness) if staleness else ShardedEngine(eng)
     assert sh.native_step == native
     sr = max(1, ROWS // slices)
     batches = [to_batch(*random_csr(ROWS, FIELDS, VOCAB, seed=7 * step + 1), dev, slice_rows=sr)
@@ -52,6 +53,8 @@ def _worker(rank, world, out_dir, kind, slices, pipelined, native):
                   row_ptr=torch.zeros(1, dtype=torch.int32), slice_rows=sr)
     assert not sh.train_step(empty, S=slices)
     assert sh.eval_step(empty) is None
+    if staleness:
+        sh.flush()
     keys, words = eng.export_table()
     o = np.argsort(keys)
     st = eng.read_stats()
@@ -61,15 +64,18 @@ def _worker(rank, world, out_dir, kind, slices, pipelined, native):
     np.save(os.path.join(out_dir, f"stats_{tag}.npy"), np.array([st["rows"], st["ln_loss"]]))
     np.save(os.path.join(out_dir, f"preds_{tag}.npy"), np.stack(preds))
     np.save(os.path.join(out_dir, f"counters_{tag}.npy"),
-            np.array([sh.inline_prepares, sh.empty_steps, sh.bytes_moved, calls[0]]))
+            np.array([sh.inline_prepares, sh.empty_steps, sh.bytes_moved, calls[0],
+                      getattr(sh, "p2p_ops", 0)]))
 
 
-@pytest.mark.parametrize("kind,slices,pipelined",
-                         [("lr", 1, True), ("lr", 4, False), ("fm", 1, True), ("fm", 40, True),
-                          ("mvm", 1, False), ("lr", 40, True)])
-def test_native_step_equals_python_step(tmp_path, kind, slices, pipelined):
+@pytest.mark.parametrize("kind,slices,pipelined,staleness",
+                         [("lr", 1, True, 0), ("lr", 4, False, 0), ("fm", 1, True, 0),
+                          ("fm", 40, True, 0), ("mvm", 1, False, 0), ("lr", 40, True, 0),
+                          # the staleness-k step (async_p2p.AsyncShardedEngine)
+                          ("lr", 1, True, 1), ("fm", 4, False, 2), ("mvm", 40, True, 1)])
+def test_native_step_equals_python_step(tmp_path, kind, slices, pipelined, staleness):
     for native in (False, True):
-        run_world(_worker, 1, str(tmp_path), kind, slices, pipelined, native)
+        run_world(_worker, 1, str(tmp_path), kind, slices, pipelined, native, staleness)
     for name in ("keys", "words", "stats", "preds", "counters"):
         a = np.load(tmp_path / f"{name}_p.npy")
         b = np.load(tmp_path / f"{name}_n.npy")

@@ -39,21 +39,23 @@ import torch
 import torch.distributed as dist
 
 from xflow_amd.engine import Batch, Engine
-from xflow_amd.parallel.sparse_a2a import ShardedEngine, _Buf
+from xflow_amd.parallel.sparse_a2a import _native_counter, ShardedEngine, _Buf
 
 _SRV_BUFS = 8  # server buffers of the native engine (Engine::kSrvBufs)
 
 
 class AsyncShardedEngine(ShardedEngine):
-    _native_ok = False  # (the staleness-k step stays in Python)
+    # (the native step -- csrc/comm/sharded_step.cpp train_step_async -- runs
+    # the same staleness-k step when ShardedEngine selects it)
+    p2p_ops = _native_counter("p2p_ops")  # gradient pushes exchanged (one per step)
 
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
                  staleness: int = 1, **kw):
         if not 1 <= int(staleness) <= _SRV_BUFS - 1:
             raise ValueError("staleness must be in [1, %d]" % (_SRV_BUFS - 1))
+        self.staleness = int(staleness)  # (read by the native step's setup)
         super().__init__(engine, group, **kw)
         dev = engine.device
-        self.staleness = int(staleness)
         nbuf = self.staleness + 1  # step t's buffers live until its apply at step t+k
         self._nbuf = nbuf
         self._rk = [_Buf(torch.int64, dev) for _ in range(nbuf)]
@@ -67,7 +69,6 @@ class AsyncShardedEngine(ShardedEngine):
         self._vals_out = [_Buf(torch.float32, dev) for _ in range(nbuf)]
         self._step_no = 0
         self._pending: deque = deque()
-        self.p2p_ops = 0           # gradient pushes exchanged (one per step)
         self.p2p_transport = self.transport
 
     # ---- pushes ---------------------------------------------------------------
@@ -89,6 +90,8 @@ class AsyncShardedEngine(ShardedEngine):
 
     def train_step(self, batch: Batch, S: Optional[int] = None, prefetch=None,
                    next_batch: Optional[Batch] = None) -> bool:
+        if self._native is not None:
+            return super().train_step(batch, S, prefetch, next_batch)
         e = self.engine
         S = int(S) if S else e.slices_of(batch)
         ps = e.value_width  # floats per pulled value row
@@ -156,6 +159,10 @@ class AsyncShardedEngine(ShardedEngine):
     def flush(self) -> None:
         """Exchange and apply every pending push in step order (call before
         evaluation/checkpoint; every rank must call it)."""
+        if self._native is not None:
+            self.engine._sync_stream()
+            self._native.flush()
+            return
         while self._pending:
             p = self._pending.popleft()
             if not self._self_only():

@@ -103,11 +103,11 @@ class ShardedEngine:
     Native step: with the native RCCL communicator (or the world-1
     self-exchange) the whole step -- split decoding, op lists, group calls,
     applies -- runs in C++ (csrc/comm/sharded_step.cpp, one call per step;
-    XFLOW_NATIVE_STEP=0 keeps it in Python).  The methods below are the same
+    XFLOW_NATIVE_STEP=0 keeps it in Python; the staleness-k subclass too).  The methods below are the same
     step for the torch.distributed transport, and the specification the
     native one follows (tests/test_native_sharded.py)."""
 
-    # steps the native implementation may run (the staleness-k subclass: no)
+    # steps the native implementation may run
     _native_ok = True
     host_waits = _native_counter("host_waits")
     mid_step_waits = _native_counter("mid_step_waits")
@@ -198,7 +198,8 @@ class ShardedEngine:
         # (world 1, aliased: no communicator -- the owner reads the send
         # buffers in place, as _self_only)
         self.__dict__["_native"] = native.load().ShardedStep(
-            self.engine._e, None if alias else self._comm, self.world, self.rank, self.early_keys)
+            self.engine._e, None if alias else self._comm, self.world, self.rank, self.early_keys,
+            int(getattr(self, "staleness", 0)))
 
     @property
     def native_step(self) -> bool:
