@@ -201,7 +201,8 @@ Engine::~Engine() {
                   stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
                   host_keys_dev_, host_vals_dev_,
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
-                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, own_keys_, fm_grad_, row_grad_,
+                  red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, grp_nz_, own_keys_, fm_grad_,
+                  row_grad_,
                   lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
@@ -502,6 +503,11 @@ void Engine::train_step(const BatchView& b) {
     const int rs = fsu ? slice_cap_ : 1;
     if (!row_grad_) row_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps * rs);
   }
+  // FTRL with several params per key (FM / MVM) on the packed apply: the pull
+  // stashes every key's (n, z) in unique order, so the first group's apply
+  // reads them coalesced instead of re-reading the slot's row at random
+  const bool grpst = be_->is_gpu() && L.opt == kFTRL && L.P > 1;
+  if (grpst && !grp_nz_) grp_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * L.P);
   // the unique-order outputs of a multi-slice step and their slice bits
   const bool uq = Sf > 1 && (lr16 || fmu || fsu);
   if (uq && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
@@ -540,6 +546,7 @@ void Engine::train_step(const BatchView& b) {
     pa.zero_out = lr_grad_;
   }
   if (lr16s) pa.out_nz = lr_nz_;
+  if (grpst) pa.out_nz = grp_nz_;
   if (fmu) {
     pa.zero_out = fm_grad_;
     pa.zero_width = 2;
@@ -632,6 +639,7 @@ void Engine::train_step(const BatchView& b) {
       aa.nz_stash = stash ? lr_nz_ : nullptr;
     }
     if (lr16s) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
+    if (grpst && stash) aa.nz_stash = grp_nz_;
     if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
       aa.grads = fm_grad_;
       aa.grad_map = nullptr;

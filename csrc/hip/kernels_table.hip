@@ -841,17 +841,39 @@ __device__ __forceinline__ RowPre row_pre(const u32* __restrict__ words, u32 slo
   return r;
 }
 
+// The same words from the pull's stash (PullArgs::out_nz, FTRL): entry i's
+// (n, z) of param p at [i * P + p], n < 0 marking a key never pushed; the
+// key from the unique list.  Coalesced, unlike the slot's row.
+__device__ __forceinline__ RowPre row_stash(const float2* __restrict__ stash,
+                                            const u64* __restrict__ keys, int64_t i, int p,
+                                            int P) {
+  RowPre r;
+  const float2 nz = stash[(size_t)i * P + p];
+  r.key = keys[i];
+  r.flag = nz.x >= 0.0f ? 1u : 0u;
+  r.s0 = nz.x >= 0.0f ? nz.x : 0.0f;
+  r.s1 = nz.y;
+  return r;
+}
+
 // Grid-stride pipeline over a packed group's keys: slots two iterations
-// ahead, row words one ahead (RowPre).
+// ahead, row words one ahead (RowPre) -- from the slot's row, or from the
+// pull's stash when the caller sets `stash` (and `keys`).
 struct RowPipe {
   int64_t stride, n;
   u32 s_cur, s_nx;
   RowPre r_nx;
+  const float2* stash = nullptr;
+  const u64* keys = nullptr;
+  __device__ __forceinline__ RowPre row(const u32* words, u32 slot, int64_t i, int p,
+                                        const TableLayout& L) const {
+    return stash ? row_stash(stash, keys, i, p, L.P) : row_pre(words, slot, p, L);
+  }
   __device__ __forceinline__ void start(const u32* __restrict__ slots, const u32* words,
                                         int64_t i, int p, const TableLayout& L) {
     s_cur = i < n ? slots[i] : kNoSlot;
     s_nx = i + stride < n ? slots[i + stride] : kNoSlot;
-    r_nx = row_pre(words, s_cur, p, L);
+    if (i < n) r_nx = row(words, s_cur, i, p, L);
   }
   // at the top of iteration i: returns (slot, row) of i, issues i + stride's
   // row loads and i + 2 * stride's slot load
@@ -860,7 +882,7 @@ struct RowPipe {
     const u32 slot = s_cur;
     r = r_nx;
     s_cur = s_nx;
-    if (i + stride < n) r_nx = row_pre(words, s_cur, p, L);
+    if (i + stride < n) r_nx = row(words, s_cur, i + stride, p, L);
     if (i + 2 * stride < n) s_nx = slots[i + 2 * stride];
     return slot;
   }
@@ -893,6 +915,9 @@ __global__ void __launch_bounds__(kBlock) k_pull_values(PullArgs a) {
     } else {
       v = state_weight(rp.key, rp.flag != 0u, rp.s0, rp.s1, p, L, a.opt);
     }
+    if (a.out_nz)  // the apply's stash (FTRL): (n, z), n = -1 for a key never pushed
+      reinterpret_cast<float2*>(a.out_nz)[(size_t)i * L.P + p] =
+          make_float2(slot != kNoSlot && rp.flag ? rp.s0 : -1.0f, slot != kNoSlot ? rp.s1 : 0.0f);
     if (a.out_w) {
       a.out_w[(size_t)i * a.pstride + p] = v;
       for (int c = L.P + p; c < a.pstride; c += L.P) a.out_w[(size_t)i * a.pstride + c] = 0.0f;
@@ -1189,6 +1214,10 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
   RowPipe pipe;
   pipe.stride = pl.stride;
   pipe.n = n;
+  if (ftrl && a.nz_stash) {  // (the pull's (n, z): the row is only written)
+    pipe.stash = reinterpret_cast<const float2*>(a.nz_stash);
+    pipe.keys = a.keys;
+  }
   pipe.start(a.slots, a.table.words, i, p, L);
   // one source, one slice: the key's gradient row joins the pipeline too
   // (row index two iterations ahead, the lane's value(s) one ahead)
@@ -1229,11 +1258,6 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
       const u64 key = rp.key;
       bool pushed = rp.flag != 0u;
       float n0 = rp.s0, z0 = rp.s1;  // FTRL (n, z); SGD w
-      if (ftrl && a.nz_stash && L.P == 1) {
-        const float2 nz = reinterpret_cast<const float2*>(a.nz_stash)[i];
-        n0 = nz.x;
-        z0 = nz.y;
-      }
       // current weight; w_next caches it between pushes and is recomputed
       // only when another push follows (the closed form is the bulk of this
       // kernel's instructions: one push per key -- S = 1 -- evaluates it once)
@@ -1310,6 +1334,8 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   const bool lr16_slices = lr16_slot && a.S > 1 && a.masks && !a.masks_rw && !a.grad_map &&
                            !a.zero_after && !a.reset_pos && a.nz_stash && !a.sum_slices &&
                            !a.slice_rows && !a.grp.oidx;
+  if (a.nz_stash && !a.keys && !a.grp.oidx && L.P > 1)
+    throw std::runtime_error("table_apply: a stash needs the entries' keys");
   if (a.grp.oidx) {
     if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");
     if (lr16) hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);

@@ -246,7 +246,7 @@ struct PullArgs {
   // LR-FTRL 16-byte slots, fused step: the (n, z) each key was pulled with,
   // in unique order (read back by the apply instead of the table), and a
   // unique-order gradient buffer to zero for the reduction's direct writes.
-  float* out_nz = nullptr;         // [n][2]
+  float* out_nz = nullptr;         // [n][2] (LR), [n][P][2] (packed pull, FTRL: n = -1 never pushed)
   float* zero_out = nullptr;       // [n][zero_width]
   int zero_width = 1;
   // reference-math FM: out_vals rows are (w, Σ v, Σ v^2, 0) (FwdArgs::fm_vals)

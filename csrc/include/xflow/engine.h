@@ -410,6 +410,7 @@ class Engine {
   double grow_s_ = 0.0;
   u64 max_segs_ = 0;                // segments of 2^max_log2_cap slots
   double monitor_wait_s_ = 0.0;
+  float* grp_nz_ = nullptr;                   // FM / MVM FTRL: the pull's (n, z) stash [unique][P]
   unsigned long long* rec_count_ = nullptr;  // (count_records) device counter
   u32* red_vmax_ = nullptr;                   // MVM: per-step fixed-point scale words [2]
   u32* text_ws_ = nullptr;                    // parse_text workspace
