@@ -245,3 +245,37 @@ def test_trainer_async_p2p_two_workers(tmp_path):
 
     run_world(_async_trainer_worker, 2, DATA, str(tmp_path))
     assert np.loadtxt(tmp_path / "pred_0_0.txt").shape == (200, 3)
+
+
+def _mismatch_worker(rank, world, out_dir, pipelined):
+    """train_step(A, next_batch=B) then train_step(C): the step must drop the
+    keys exchanged ahead for B and train C on its own keys."""
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    eng = _make_engine("fm", 1)
+    sh = ShardedEngine(eng)
+    dev = torch.device("cpu")
+    A, B, C = (to_batch(*_batches(rank, s), dev, slice_rows=ROWS) for s in (0, 1, 2))
+    if pipelined:
+        sh.train_step(A, S=1, next_batch=B)  # (B's keys ride in A's gradient exchange)
+        sh.train_step(C, S=1)                # not the announced batch
+        sh.train_step(B, S=1)
+    else:
+        for b in (A, C, B):
+            sh.train_step(b, S=1)
+    keys, _ = eng.export_table()
+    o = np.argsort(keys)
+    np.save(os.path.join(out_dir, f"k{rank}_{int(pipelined)}.npy"), keys[o])
+    np.save(os.path.join(out_dir, f"v{rank}_{int(pipelined)}.npy"), eng.pull(keys[o]))
+
+
+def test_unannounced_batch_drops_early_keys(tmp_path):
+    """gloo, 2 ranks: a step on a batch other than the announced next one
+    equals the unpipelined sequence bit for bit."""
+    for pipelined in (False, True):
+        run_world(_mismatch_worker, 2, str(tmp_path), pipelined)
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"k{r}_0.npy"),
+                                      np.load(tmp_path / f"k{r}_1.npy"))
+        np.testing.assert_array_equal(np.load(tmp_path / f"v{r}_0.npy").view(np.uint32),
+                                      np.load(tmp_path / f"v{r}_1.npy").view(np.uint32))

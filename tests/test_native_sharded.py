@@ -81,3 +81,34 @@ def test_native_step_equals_python_step(tmp_path, kind, slices, pipelined, stale
         b = np.load(tmp_path / f"{name}_n.npy")
         assert a.shape == b.shape, name
         np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8), err_msg=name)
+
+
+def _mismatch_worker(rank, world, out_dir, native):
+    os.environ["XFLOW_NATIVE_STEP"] = "1" if native else "0"
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    dev = torch.device("cpu")
+    eng = Engine(ModelConfig(kind="fm", v_dim=4), OptimConfig(),
+                 EngineConfig(table_log2_cap=14, max_rows=ROWS, max_nnz=ROWS * 16))
+    sh = ShardedEngine(eng)
+    A, B, C = (to_batch(*random_csr(ROWS, FIELDS, VOCAB, seed=s), dev) for s in (3, 4, 5))
+    sh.train_step(A, S=1, next_batch=B)  # B prepared ahead ...
+    sh.train_step(C, S=1)                # ... but C comes first
+    sh.train_step(B, S=1, next_batch=C)
+    sh.train_step(C, S=1)
+    keys, _ = eng.export_table()
+    o = np.argsort(keys)
+    tag = "n" if native else "p"
+    np.save(os.path.join(out_dir, f"mk_{tag}.npy"), keys[o])
+    np.save(os.path.join(out_dir, f"mv_{tag}.npy"), eng.pull(keys[o]))
+    np.save(os.path.join(out_dir, f"mc_{tag}.npy"), np.array([sh.inline_prepares]))
+
+
+def test_native_step_unannounced_batch(tmp_path):
+    """A step on a batch other than the prepared one prepares its own (both
+    implementations alike, bit for bit)."""
+    for native in (False, True):
+        run_world(_mismatch_worker, 1, str(tmp_path), native)
+    for name in ("mk", "mv", "mc"):
+        a, b = np.load(tmp_path / f"{name}_p.npy"), np.load(tmp_path / f"{name}_n.npy")
+        np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8), err_msg=name)
