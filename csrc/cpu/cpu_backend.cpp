@@ -187,6 +187,7 @@ class CpuBackend final : public Backend {
       u32 row = a.grad_map ? a.grad_map[i] : (u32)i;
       float* g = a.grads + (size_t)row * S * ps;
       u32 m = a.masks ? a.masks[row] : all;
+      if (a.masks && a.masks_clear) const_cast<u32*>(a.masks)[row] = 0u;
       if (slot != kNoSlot) {
         u32* sp = t.words + (u64)slot * L.stride;
         u64 key = *reinterpret_cast<u64*>(sp);

@@ -257,8 +257,11 @@ void Engine::use_worker_set(int wb) {
 // The GPU reduction path sees every (key, slice) that occurs (a record per
 // column-table entry, or per occurrence), so it can write the slice bits:
 // every model on its bucket-reduction path.
-bool Engine::reduction_masks() const {
-  if (!red_pairs_ || (double)scratch_.cap * slice_cap_ * pstride() >= 4294967295.0) return false;
+bool Engine::reduction_masks(bool unique_positions) const {
+  // (dest * pstride in 32 bits: dests = unique index x slices with unique-
+  // index positions, at most max_nnz keys -- else scratch slot x slices)
+  const double keys = unique_positions ? (double)cfg_.max_nnz : (double)scratch_.cap;
+  if (!red_pairs_ || keys * slice_cap_ * pstride() >= 4294967295.0) return false;
   return cfg_.model.kind == kLR || cfg_.model.kind == kFM ||
          (cfg_.model.kind == kMVM && red_rowv_ != nullptr);
 }
@@ -465,14 +468,19 @@ void Engine::train_step(const BatchView& b) {
   const bool lr16_layout_ok = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 &&
                               L.P == 1 && L.opt == kFTRL && !L.has_flag && red_pairs_ &&
                               (double)scratch_.cap < 4294967295.0;
-  const bool lr16 = lr16_layout_ok && (Sf == 1 || (masks && reduction_masks()));
+  // unique-index positions (see below): decided first, the 32-bit index
+  // bounds of the reductions depend on them
+  const bool upos_path = be_->remaps_positions() && red_pairs_ &&
+                         (Sf > 1 || cfg_.model.kind == kMVM ||
+                          (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard));
+  const bool lr16 = lr16_layout_ok && (Sf == 1 || (masks && reduction_masks(upos_path)));
   // summed slices: slot-indexed sums (packed apply), still the (n, z) stash
   const bool lr16s = lr16_layout_ok && Sf > 1 && !lr16;
   if (lr16s && !lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   // several slices on the reduction path: unique-order [unique][slice]
   // gradients plus the slice bits the reduction writes (uq_mask_); the pull
   // clears the bits, the apply reads only the present slices
-  const bool uqm = masks && reduction_masks();
+  const bool uqm = masks && reduction_masks(upos_path);
   if (lr16) {
     ensure_inv();
     if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * slice_cap_);
@@ -492,8 +500,11 @@ void Engine::train_step(const BatchView& b) {
   // MVM (one slice) and standard-math FM (any slices) on their reduction
   // paths: the per-key gradient rows land in unique order too (a dense apply
   // read instead of slot-indexed rows the apply had to zero after reading)
-  const bool rows_ok = be_->is_gpu() && red_pairs_ &&
-                       (double)scratch_.cap * ps * slice_cap_ < 4294967295.0;
+  // (row indices dest * ps in 32 bits: dests are unique indices x slices
+  // with unique-index positions -- at most max_nnz unique keys -- else
+  // scratch slots x slices)
+  const double key_bound = upos_path ? (double)cfg_.max_nnz : (double)scratch_.cap;
+  const bool rows_ok = be_->is_gpu() && red_pairs_ && key_bound * ps * slice_cap_ < 4294967295.0;
   const bool mvmu = rows_ok && Sf == 1 && cfg_.model.kind == kMVM && red_rowv_;
   const bool fsu = rows_ok && (Sf == 1 || uqm) && cfg_.model.kind == kFM &&
                    cfg_.model.fm_math == kFmStandard;
@@ -519,9 +530,7 @@ void Engine::train_step(const BatchView& b) {
   // a win with several slices (FM-8 std S = 8 143 -> 222 M samples/s, FM-8
   // S = 8 +1.9 %, LR S = 8 +0.8 %) and for standard FM (+10.5 %), a loss for
   // one-slice LR (-5.1 %), MVM (-3.5 %) and reference FM (-1.4 %).
-  const bool upos = be_->remaps_positions() && red_pairs_ &&
-                    (Sf > 1 || cfg_.model.kind == kMVM ||
-                     (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard));
+  const bool upos = upos_path;
   if (upos) ensure_inv();
   dedup_(b, 1, nullptr, upos || lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)
@@ -566,10 +575,10 @@ void Engine::train_step(const BatchView& b) {
     const BatchView bk = group_view(b, S, k, posk);
     const int Sg = group_slices(S, k);
     const int32_t* srk = srows + (int64_t)k * kSliceGroup;
-    // a later group's unique-order slice bits start from zero again (the
-    // pull cleared them for the first); its apply reads the table, which
-    // the earlier groups updated, instead of the pull's (n, z) stash
-    if (k > 0 && uq) be_->memset(lr_mask_, 0, sizeof(u32) * (size_t)b.nnz);
+    // a later group's unique-order slice bits start from zero again: the
+    // pull cleared them for the first group, each group's apply clears the
+    // bits it read (ApplyArgs::masks_clear); a later group's apply reads the
+    // table, which the earlier groups updated, instead of the pull's stash
     const bool stash = k == 0;
 
     FwdArgs fa;
@@ -580,7 +589,7 @@ void Engine::train_step(const BatchView& b) {
     fa.stats = stats_;
     fa.model = cfg_.model;
     fa.S = Sg;
-    fa.agg_ok = (double)scratch_.cap * Sg * ps < 4294967295.0;
+    fa.agg_ok = key_bound * Sg * ps < 4294967295.0;  // (32-bit dest * ps, see rows_ok)
     fa.fx_bad = overflow_;
     set_reduction(fa);
     if (upos) fa.red_nuq = n_uniq_;
@@ -655,6 +664,7 @@ void Engine::train_step(const BatchView& b) {
     if (uq) {  // present slices by the unique-order bits (cleared by the next pull)
       aa.masks = lr_mask_;
       aa.masks_rw = nullptr;
+      aa.masks_clear = k + 1 < ng;  // (for the next group's reduction)
     }
     attach_snapshot(aa);
     be_->table_apply(aa);
@@ -1027,7 +1037,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
   fa.agg_ok = (double)scratch_.cap * S * pstride() < 4294967295.0;
   fa.fx_bad = overflow_;
   set_reduction(fa);
-  if (masks && reduction_masks()) fa.red_masks = tmask_;
+  if (masks && reduction_masks(false)) fa.red_masks = tmask_;
   else if (masks) be_->slice_masks(bk, posk, tmask_);
   fa.fm_compact = sharded_fm_compact() && fa.agg_ok;
   fa.fm_vals = fm_vals_;

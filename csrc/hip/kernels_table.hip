@@ -1005,14 +1005,20 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
   const FtrlParams fp = a.opt.ftrl;
   if constexpr (kSlices) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      u32 slot = a.slots[i];
       // unique-order [key][slice] normalised sums: the present slices' pushes
-      // in slice order (the CPU backend's Hogwild order)
+      // in slice order (the CPU backend's Hogwild order); a key no slice of
+      // this group touched is skipped before any table access
+      const u32 m0 = a.masks[i];
+      if (!m0) continue;
+      if (a.masks_clear) const_cast<u32*>(a.masks)[i] = 0u;
+      u32 slot = a.slots[i];
       if (slot == kNoSlot) continue;
       float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
-      float2 nz = reinterpret_cast<const float2*>(a.nz_stash)[i];
+      // (the pull's stash for the step's first group; later groups read the
+      // state the earlier ones wrote)
+      float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
       const float* g = a.grads + (size_t)i * a.S;
-      for (u32 m = a.masks[i]; m; m &= m - 1) {
+      for (u32 m = m0; m; m &= m - 1) {
         const float w = ftrl_weight(nz.y, nz.x, fp);
         ftrl_push(nz.x, nz.y, w, g[__ffs(m) - 1], fp);
       }
@@ -1291,6 +1297,7 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
         const u32 row = a.grad_map ? a.grad_map[e] : e;
         const float* g = a.grads + (size_t)row * S * gs;
         const u32 m = a.masks ? a.masks[row] : all;
+        if (a.masks_clear && p == 0) const_cast<u32*>(a.masks)[row] = 0u;
         any |= m;
         auto raw_of = [&](int s) -> float {
           if (!a.fm_compact) return g[s * gs + p];
@@ -1332,8 +1339,8 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   const bool lr16 = lr16_slot && a.S == 1 && !a.masks;
   // S > 1 on unique-order sums and slice bits (Engine::train_step's fused LR step)
   const bool lr16_slices = lr16_slot && a.S > 1 && a.masks && !a.masks_rw && !a.grad_map &&
-                           !a.zero_after && !a.reset_pos && a.nz_stash && !a.sum_slices &&
-                           !a.slice_rows && !a.grp.oidx;
+                           !a.zero_after && !a.reset_pos && !a.sum_slices && !a.slice_rows &&
+                           !a.grp.oidx;
   if (a.nz_stash && !a.keys && !a.grp.oidx && L.P > 1)
     throw std::runtime_error("table_apply: a stash needs the entries' keys");
   if (a.grp.oidx) {

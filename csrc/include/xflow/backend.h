@@ -346,6 +346,8 @@ struct ApplyArgs {
   float* grads = nullptr;          // rows of S*pstride floats
   const u32* grad_map = nullptr;   // row index for entry i (null => i)
   const u32* masks = nullptr;      // per-row slice bits (null => all S slices)
+  bool masks_clear = false;        // zero each entry's bits once read (unique-order
+                                   // bits of a slice group: the next group starts from zero)
   bool zero_after = false;         // clear consumed gradient rows (and masks)
   u32* masks_rw = nullptr;         // masks buffer to clear when zero_after
   int S = 1;

@@ -333,7 +333,7 @@ class Engine {
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
   void set_reduction(FwdArgs& fa) const;
-  bool reduction_masks() const;
+  bool reduction_masks(bool unique_positions) const;
   void ensure_inv();
   LossStats* stats_ = nullptr;  // [1]
   u32* send_pos_ = nullptr;     // [max_nnz]
