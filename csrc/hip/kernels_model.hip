@@ -1389,9 +1389,12 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   const Rec* src = static_cast<const Rec*>(sorted);
   const int shift = geom.shift(kShift);
   const u32 act = (u32)geom.active(shift, nb);
-  const u32 units = act << (shift - kShift);
-  for (u32 id = blockIdx.x; id < units; id += gridDim.x) {
-    const u32 bk = id % act, sub = id / act;
+  // A workgroup takes whole buckets: a bucket wider than a unit (several
+  // slices' dests) is summed unit after unit by the same workgroup, so its
+  // segment table is staged once (per unit, the staging -- two loads per
+  // producer workgroup -- cost more than the records at 32 slices)
+  const u32 nsubs = 1u << (shift - kShift);
+  for (u32 bk = blockIdx.x; bk < act; bk += gridDim.x) {
     u32 beg, end;
     if constexpr (kSeg) {
       beg = 0;
@@ -1401,9 +1404,6 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
       end = start[bk + 1];
     }
     if (beg == end) continue;  // (block-uniform)
-    const u64 lo = ((u64)bk << shift) + ((u64)sub << kShift);
-    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
-    for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) seen[i] = 0u;
     if constexpr (kSeg) {
       // segment g: records [s_pre[g], s_pre[g+1]) of the bucket, at s_seg[g] + i
       const size_t row0 = (size_t)bk * sg.groups;
@@ -1415,6 +1415,10 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
         s_seg[g] = base + sg.subs[row0 + g] - p;
       }
     }
+  for (u32 sub = 0; sub < nsubs; ++sub) {
+    const u64 lo = ((u64)bk << shift) + ((u64)sub << kShift);
+    for (u32 i = threadIdx.x; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
+    for (u32 i = threadIdx.x; i < kR / 32; i += kRedBlock) seen[i] = 0u;
     lds_barrier();
     for (u32 i = beg + threadIdx.x; i < end; i += kRedBlock) {
       u32 ri = i;
@@ -1497,6 +1501,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
     // even with a zero gradient -- it still pushes, like the reference's slice)
     if (masks) unit_masks<kR>(seen, lo, (u64)S, masks, out ? inv : nullptr);
     lds_barrier();  // (the next unit reinitialises what this one read)
+  }
   }
 }
 
