@@ -528,8 +528,9 @@ void Engine::train_step(const BatchView& b) {
   // not the 4x-headroom scratch slots.  The remap pass costs ~40 us per
   // 10.2 M occurrences; same-box A/B (profiles/r4_unique_positions_ab.txt):
   // a win with several slices (FM-8 std S = 8 143 -> 222 M samples/s, FM-8
-  // S = 8 +1.9 %, LR S = 8 +0.8 %) and for standard FM (+10.5 %), a loss for
-  // one-slice LR (-5.1 %), MVM (-3.5 %) and reference FM (-1.4 %).
+  // S = 8 +1.9 %, LR S = 8 +0.8 %), for standard FM (+10.5 %) and -- since
+  // its scaled fixed-point vector sums -- MVM (live +13 %, degenerate +2.3 %),
+  // a loss for one-slice LR (-5.1 %) and reference FM (-1.4 %).
   const bool upos = upos_path;
   if (upos) ensure_inv();
   dedup_(b, 1, nullptr, upos || lr16 || fmu || rowu);
