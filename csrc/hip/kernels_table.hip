@@ -1018,9 +1018,10 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
       // state the earlier ones wrote)
       float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
       const float* g = a.grads + (size_t)i * a.S;
+      float sn = sqrtf(nz.x);
       for (u32 m = m0; m; m &= m - 1) {
-        const float w = ftrl_weight(nz.y, nz.x, fp);
-        ftrl_push(nz.x, nz.y, w, g[__ffs(m) - 1], fp);
+        const float w = ftrl_weight_sn(nz.y, sn, fp);
+        ftrl_push_sn(nz.x, nz.y, sn, w, g[__ffs(m) - 1], fp);
       }
       *st = nz;
     }
@@ -1183,12 +1184,13 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
     if (slot == kNoSlot) continue;
     float2* st = reinterpret_cast<float2*>(a.table.words + (u64)slot * 4 + 2);
     float2 nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i] : *st;
+    float sn = sqrtf(nz.x);
     for (int s = src0; s < g.nsrc; ++s) {
       const u64 v = row[s];
       if ((u32)(v >> 32) != g.epoch) continue;
       const float gr = a.grads[(u32)v];
-      const float w = ftrl_weight(nz.y, nz.x, fp);
-      ftrl_push(nz.x, nz.y, w, gr, fp);
+      const float w = ftrl_weight_sn(nz.y, sn, fp);
+      ftrl_push_sn(nz.x, nz.y, sn, w, gr, fp);
     }
     *st = nz;
   }
@@ -1204,6 +1206,8 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_multi(ApplyArgs a) {
 // order; other entries skip.
 // (7 waves per SIMD: <= 72 VGPRs without spills -- 77 at the default gave 6;
 // 8 waves spills: FM-8 +1.7 % / -1 %, profiles/r2_s3_fm_pull_apply_pipeline.txt)
+// kSl: a step of several slices (S > 1), whose keys take chains of pushes
+template <bool kSl>
 __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
   XF_APPLY_SNAPSHOT(a);
   const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
@@ -1227,7 +1231,7 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
   pipe.start(a.slots, a.table.words, i, p, L);
   // one source, one slice: the key's gradient row joins the pipeline too
   // (row index two iterations ahead, the lane's value(s) one ahead)
-  const bool gpipe = !multi && S == 1 && !a.masks && !a.sum_slices;
+  const bool gpipe = !kSl && !multi && S == 1 && !a.masks && !a.sum_slices;
   auto grad_row = [&](int64_t k) -> u32 { return a.grad_map ? a.grad_map[k] : (u32)k; };
   auto grad_val = [&](u32 r) -> float2 {
     const float* g = a.grads + (size_t)r * gs;
@@ -1269,10 +1273,18 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
       // kernel's instructions: one push per key -- S = 1 -- evaluates it once)
       float w_next = state_weight(key, pushed, n0, z0, p, L, a.opt);
       bool stale = false;
+      // (several slices: sqrtf(n) carried through the key's pushes)
+      float sn = kSl && ftrl ? sqrtf(n0) : 0.0f;
       auto push = [&](float gv) {
-        if (stale) w_next = state_weight(key, true, n0, z0, p, L, a.opt);
-        if (ftrl) ftrl_push(n0, z0, w_next, gv, a.opt.ftrl);
-        else n0 = w_next - a.opt.sgd.lr * gv;
+        if constexpr (kSl) {
+          if (stale) w_next = ftrl ? ftrl_weight_sn(z0, sn, a.opt.ftrl) : n0;
+          if (ftrl) ftrl_push_sn(n0, z0, sn, w_next, gv, a.opt.ftrl);
+          else n0 = w_next - a.opt.sgd.lr * gv;
+        } else {
+          if (stale) w_next = state_weight(key, true, n0, z0, p, L, a.opt);
+          if (ftrl) ftrl_push(n0, z0, w_next, gv, a.opt.ftrl);
+          else n0 = w_next - a.opt.sgd.lr * gv;
+        }
         pushed = true;
         stale = true;
       };
@@ -1346,14 +1358,18 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (a.grp.oidx) {
     if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");
     if (lr16) hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);
-    else hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+    else if (a.S > 1)
+      hipLaunchKernelGGL(k_apply_group<true>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(k_apply_group<false>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else if (lr16) {
     hipLaunchKernelGGL(k_apply_lr16<false>, dim3(grid), dim3(kBlock), 0, st, a);
   } else if (lr16_slices) {
     hipLaunchKernelGGL(k_apply_lr16<true>, dim3(grid), dim3(kBlock), 0, st, a);
   } else if ((a.pstride >= 2 || (L.P == 1 && a.nz_stash)) && L.P <= kWave && !a.reset_pos) {
     // (LR with several slices and the pull's stash: one lane per key, packed)
-    hipLaunchKernelGGL(k_apply_group, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+    if (a.S > 1)
+      hipLaunchKernelGGL(k_apply_group<true>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+    else hipLaunchKernelGGL(k_apply_group<false>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
   } else {
     hipLaunchKernelGGL(k_apply_generic, dim3(grid), dim3(kBlock), 0, st, a);
   }

@@ -76,21 +76,33 @@ struct FtrlParams {
   float lambda2 = 10.0f;  // ftrl.h:20
 };
 
-XF_HD float ftrl_weight(float z, float n, const FtrlParams& p) {
+// (sn = sqrtf(n): a chain of pushes onto one parameter carries it, so each
+// push takes one square root instead of three -- the same floats)
+XF_HD float ftrl_weight_sn(float z, float sn, const FtrlParams& p) {
   if (fabsf(z) <= p.lambda1) return 0.0f;
   float tmpr = 0.0f;
   if (z > 0.0f) tmpr = z - p.lambda1;
   if (z < 0.0f) tmpr = z + p.lambda1;
-  float tmpl = -1.0f * ((p.beta + sqrtf(n)) / p.alpha + p.lambda2);
+  float tmpl = -1.0f * ((p.beta + sn) / p.alpha + p.lambda2);
   return tmpr / tmpl;
 }
 
+XF_HD float ftrl_weight(float z, float n, const FtrlParams& p) {
+  return ftrl_weight_sn(z, sqrtf(n), p);
+}
+
 // One FTRL-Proximal push of gradient g onto (n, z) whose current weight is w.
-XF_HD void ftrl_push(float& n, float& z, float w, float g, const FtrlParams& p) {
-  float old_n = n;
-  float nn = old_n + g * g;
-  z += g - (sqrtf(nn) - sqrtf(old_n)) / p.alpha * w;
+XF_HD void ftrl_push_sn(float& n, float& z, float& sn, float w, float g, const FtrlParams& p) {
+  float nn = n + g * g;
+  float snn = sqrtf(nn);
+  z += g - (snn - sn) / p.alpha * w;
   n = nn;
+  sn = snn;
+}
+
+XF_HD void ftrl_push(float& n, float& z, float w, float g, const FtrlParams& p) {
+  float sn = sqrtf(n);
+  ftrl_push_sn(n, z, sn, w, g, p);
 }
 
 struct SgdParams {
