@@ -151,12 +151,19 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     // scratch has grown that far (bench shape: S = 8 at 2^23 active slots
     // stays at 4096 buckets of 2^14).
     const uint64_t dests = scratch_.cap * (uint64_t)slice_cap_;
+    // vector records: the producer's larger bucket cap where its LDS allows
+    // (vec_red_max_buckets) and the batch fits the scatter-free form
+    const int vd = nv - 1;  // k_fm_std_red<vd>: NV = 1 + vd
+    const int maxb = vec && (cfg_.max_rows + fmstd_block(vd) - 1) / fmstd_block(vd) <= kSegMaxGroups
+                         ? vec_red_max_buckets(vd)
+                         : kRedMaxBuckets;
+    red_maxb_ = vec ? maxb : 0;
     int nb = (int)((dests + (1ull << shift) - 1) >> shift);
     int nsub = 1;
-    while ((uint64_t)nb > (uint64_t)kRedMaxBuckets * nsub) nsub <<= 1;
-    if (nsub > 1) nb = kRedMaxBuckets;
+    while ((uint64_t)nb > (uint64_t)maxb * nsub) nsub <<= 1;
+    if (nsub > 1) nb = maxb;
     red_nsub_ = nsub;
-    if (nb <= kRedMaxBuckets && dests < (1ull << 32)) {
+    if (nb <= maxb && dests < (1ull << 32)) {
       const int64_t groups = (cfg_.max_rows + group_rows - 1) / group_rows;
       red_nb_ = nb;
       red_pairs_ = balloc<u64>(be, (size_t)nnz * recw);
@@ -335,6 +342,7 @@ void Engine::set_reduction(FwdArgs& fa) const {
   fa.red_tot = red_tot_;
   fa.red_count = red_count_;
   fa.red_nb = red_nb_;
+  fa.red_maxb = red_maxb_;
   fa.red_rowv = red_rowv_;
 }
 

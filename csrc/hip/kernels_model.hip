@@ -39,6 +39,7 @@ struct RedGeom {
   // unique-index positions (FwdArgs::red_nuq): dests = unique * S + s lie
   // below the batch's unique count times S
   const int64_t* nuq;
+  int maxb;  // bucket cap (FwdArgs::red_maxb)
   __device__ __forceinline__ u64 rows() const {
     return nuq ? (u64)*nuq : (bcap ? (u64)*bcap : cap);
   }
@@ -46,6 +47,12 @@ struct RedGeom {
     const u64 dests = rows() * (u64)S;
     int sh = base;
     while (((dests + (1ull << sh) - 1) >> sh) > (u64)kRedMaxBuckets) ++sh;
+    // a larger cap (vector records) only where a bucket would otherwise span
+    // four or more LDS units: at two, the extra buckets' per-(bucket,
+    // workgroup) counts and offsets cost more than the records' second read
+    // (FM-8 std --slices 8 -1.2 %, --slices 64 +5.5 %: profiles/r4_negative_ab.txt)
+    if (maxb > kRedMaxBuckets && sh - base >= 2)
+      while (sh > base && ((dests + (1ull << (sh - 1)) - 1) >> (sh - 1)) <= (u64)maxb) --sh;
     return sh;
   }
   // buckets this step's dests reach (of the nb allocated for the full
@@ -58,7 +65,7 @@ struct RedGeom {
 };
 
 __host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
-  return RedGeom{a.red_bcap, a.red_cap, a.S, a.red_nuq};
+  return RedGeom{a.red_bcap, a.red_cap, a.S, a.red_nuq, a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets};
 }
 
 __device__ __forceinline__ int red_active(const FwdArgs& a, int base) {
@@ -1079,7 +1086,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
 // One LDS table (flushed, then a barrier, per column): 2x the rows of a
 // double-buffered table for the same LDS -- larger workgroups aggregate hot
 // keys over more rows (A/B: 128 rows per workgroup -21 %, 256 -> 512 below)
-constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128); }
+// (fmstd_block: backend.h)
 
 // kSeg (the scatter-free form, launch_fmstd_reduction): a pre-pass counts the
 // workgroup's occurrences per bucket -- an upper bound of its records there --
@@ -1107,8 +1114,9 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   __shared__ long long s_acc[1][kSlots * NV];
   const int fxs = kScaled ? fx_scale_bits(a.red_vmax) : kFx;
   __shared__ unsigned short s_list[1][BLOCK];
-  __shared__ u32 s_hist[kRedMaxBuckets];
-  __shared__ u32 s_off[kSeg ? kRedMaxBuckets : 1];
+  constexpr int kMaxB = vec_red_max_buckets(D);
+  __shared__ u32 s_hist[kMaxB];
+  __shared__ u32 s_off[kSeg ? kMaxB : 1];
   __shared__ u32 s_nlist[3];
   __shared__ int s_wmax[BLOCK / kWave];
   const BatchView& b = a.batch;
@@ -1175,7 +1183,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       if (pj != a.trash_pos) atomicAdd(&s_hist[(pj * S + sl) >> shift], 1u);
     }
     __syncthreads();
-    constexpr int kPer = kRedMaxBuckets / BLOCK;
+    constexpr int kPer = kMaxB / BLOCK;
     const int nb = geom.active(shift, a.red_nb);
     u32 c[kPer], sum = 0;
 #pragma unroll
@@ -1346,7 +1354,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 // records (hist: k_red_scan's exclusive prefix over the workgroups, tot[bk]
 // the total) at region(g) + subs[bk][g]; record i of the bucket is found by a
 // binary search of the LDS-staged prefix.
-constexpr int kSegMaxGroups = 2048;
+// (kSegMaxGroups: backend.h)
 struct SegSrc {
   const u32* hist;   // [nb][groups] exclusive prefix (k_red_scan)
   const u32* tot;    // [nb]
@@ -1581,6 +1589,8 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   const bool seg = groups <= kSegMaxGroups &&
                    (int64_t)a.red_nb * groups <= 2 * a.red_sorted_words &&
                    a.red_sorted_words * 8 / (vec_rec_words(NV) * 4) < (1ll << 32);
+  if (a.red_maxb > vec_red_max_buckets(D) || (!seg && a.red_maxb > kRedMaxBuckets))
+    throw std::runtime_error("vector reduction: bucket cap beyond the producer's");
   const bool split = a.red_rowv != nullptr;
   if (split && !kMvm)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
@@ -1832,7 +1842,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   }
   // standard math: per-component records through the LR reduction pipeline
   const bool red_std = agg && a.model.fm_math == kFmStandard && a.red_pairs && a.red_nb > 0 &&
-                       a.red_nb <= kRedMaxBuckets;
+                       a.red_nb <= (a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets);
   if (a.red_masks && a.S > 1 && a.model.fm_math == kFmStandard && !red_std)
     throw std::runtime_error("red_masks need the standard-FM reduction path");
   if (a.red_out && a.model.fm_math == kFmStandard && !red_std)
@@ -2103,7 +2113,7 @@ template <bool kGrad>
 static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.red_pairs && a.red_rowv && a.red_nb > 0 &&
-                   a.red_nb <= kRedMaxBuckets;
+                   a.red_nb <= (a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets);
   if (a.red_masks && a.S > 1 && !(red && a.model.v_dim >= 2))
     throw std::runtime_error("red_masks need the MVM reduction path");
   switch (a.model.v_dim) {

@@ -165,7 +165,10 @@ struct FwdArgs {
   u32* red_hist = nullptr;         // [red_nb][workgroups] pairs per (bucket, workgroup)
   u32* red_tot = nullptr;          // [red_nb + 1] pairs per bucket, then bucket starts
   u32* red_count = nullptr;        // [workgroups] pairs per workgroup
-  int red_nb = 0;                  // buckets allocated (<= kRedMaxBuckets)
+  int red_nb = 0;                  // buckets allocated (<= the bucket cap)
+  // bucket cap of this step's geometry: kRedMaxBuckets (0), or the vector
+  // records' vec_red_max_buckets (Engine: standard FM / MVM)
+  int red_maxb = 0;
   int64_t red_sorted_words = 0;    // u64 words of red_sorted
   // This step's bucket width is decided on the device: dests = slot*S + s lie
   // below red_bcap[0]*S (the scratch capacity the batch was deduplicated
@@ -221,6 +224,24 @@ constexpr int kRedMaxBuckets = 4096;
 // at most ~114 KB of LDS)
 constexpr int red_shift(int nv) {
   return nv == 1 ? kRedShift : (nv == 2 ? kRedShift - 1 : (nv <= 14 ? 10 : (nv <= 28 ? 9 : 8)));
+}
+// Vector records (standard FM / MVM, produced by k_fm_std_red<D>, NV = 1 + D):
+// twice the buckets where the producer's LDS -- its column table of 2 x BLOCK
+// slots (tag + NV int64) plus per-bucket counts and cursors -- still fits in
+// the CU's 160 KB, so a step of several slices keeps one LDS unit of dests per
+// bucket (each extra unit re-reads the bucket's records)
+constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128); }
+constexpr int kSegMaxGroups = 2048;  // producer workgroups of the scatter-free vector form
+constexpr int64_t fmstd_lds(int D, int maxb) {
+  return (int64_t)2 * fmstd_block(D) * 8 * (2 + D) + 2 * fmstd_block(D) + 2 * maxb * 4 + 1024;
+}
+// (only where the workgroups per CU stay the same)
+constexpr int vec_red_max_buckets(int D) {
+  return fmstd_lds(D, 2 * kRedMaxBuckets) <= 160 * 1024 &&
+                 (160 * 1024) / fmstd_lds(D, 2 * kRedMaxBuckets) ==
+                     (160 * 1024) / fmstd_lds(D, kRedMaxBuckets)
+             ? 2 * kRedMaxBuckets
+             : kRedMaxBuckets;
 }
 // 32-bit words of a standard-FM vector record (dest + nv values), 16-B padded
 constexpr int vec_rec_words(int nv) { return (1 + nv + 3) & ~3; }
