@@ -172,6 +172,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       red_hist_ = balloc<u32>(be, (size_t)nb * groups);
       red_tot_ = balloc<u32>(be, 2 * (size_t)nb + 2);
       red_count_ = balloc<u32>(be, groups);
+      red_groups_ = (int)groups;
       // MVM: T = loss*M per row; standard FM: (loss, loss*vs) per row (k_fm_std_fwd)
       if (mvm || fm_std) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
       if (mvm) {
@@ -341,6 +342,7 @@ void Engine::set_reduction(FwdArgs& fa) const {
   fa.red_hist = red_hist_;
   fa.red_tot = red_tot_;
   fa.red_count = red_count_;
+  fa.red_groups = red_groups_;
   fa.red_nb = red_nb_;
   fa.red_maxb = red_maxb_;
   fa.red_rowv = red_rowv_;

@@ -1808,6 +1808,21 @@ __global__ void __launch_bounds__(256) k_fm_fwd_mfma(FwdArgs a) {
 }
 
 // XFLOW_FMSTD_ATOMICS=1 keeps standard-math FM on the column-table + global
+// Rows per producer workgroup on the reduction path: the model's R, or --
+// when the batch fills at most an eighth of the CUs (a slice group of a step
+// of 256 slices or more) -- halved (down to 128) until it fills them, within
+// the workgroups the reduction's buffers hold.  A producer's time is its
+// column walk, nearly independent of its rows; narrower workgroups aggregate
+// less, so the records' sums cost more (A/B, profiles/r4_negative_ab.txt 13:
+// LR --slices 256 +5.5 %, --slices 64 -1.5 % when narrowed to fill the CUs).
+static int narrow_rows(const FwdArgs& a, int R) {
+  const int64_t rows = a.batch.rows;
+  auto groups = [&](int r) { return (rows + r - 1) / r; };
+  if (a.red_groups <= 0 || groups(R) * 8 > device_cus()) return R;
+  while (R > 128 && groups(R) < device_cus() && groups(R / 2) <= a.red_groups) R /= 2;
+  return R;
+}
+
 template <bool kGrad>
 static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
@@ -1833,8 +1848,15 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     const int gr = (int)((a.batch.rows + R - 1) / R);
     if (kGrad) {
       if (!red || !a.fm_compact) throw std::runtime_error("fm_vals: needs the compact reduction");
-      hipLaunchKernelGGL((k_fm_vals<R, true>), dim3(gr), dim3(R), 0, st, a);
-      launch_reduction<2>(a, gr, R, st);
+      const int Rn = narrow_rows(a, R);
+      const int gn = (int)((a.batch.rows + Rn - 1) / Rn);
+      switch (Rn) {
+        case 1024: hipLaunchKernelGGL((k_fm_vals<1024, true>), dim3(gn), dim3(Rn), 0, st, a); break;
+        case 512: hipLaunchKernelGGL((k_fm_vals<512, true>), dim3(gn), dim3(Rn), 0, st, a); break;
+        case 256: hipLaunchKernelGGL((k_fm_vals<256, true>), dim3(gn), dim3(Rn), 0, st, a); break;
+        default: hipLaunchKernelGGL((k_fm_vals<128, true>), dim3(gn), dim3(Rn), 0, st, a); break;
+      }
+      launch_reduction<2>(a, gn, Rn, st);
     } else {
       hipLaunchKernelGGL((k_fm_vals<R, false>), dim3(gr), dim3(R), 0, st, a);
     }
@@ -2159,9 +2181,14 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
       if (a.red_masks && a.S > 1 && !red)
         throw std::runtime_error("red_masks need the LR bucket reduction");
       if (red) {
-        constexpr int R = kLrGroupRows;
+        const int R = narrow_rows(a, kLrGroupRows);
         const int gr = (int)((a.batch.rows + R - 1) / R);
-        hipLaunchKernelGGL((k_lr<true, true, R, true>), dim3(gr), dim3(R), 0, st, a);
+        switch (R) {
+          case 1024: hipLaunchKernelGGL((k_lr<true, true, 1024, true>), dim3(gr), dim3(R), 0, st, a); break;
+          case 512: hipLaunchKernelGGL((k_lr<true, true, 512, true>), dim3(gr), dim3(R), 0, st, a); break;
+          case 256: hipLaunchKernelGGL((k_lr<true, true, 256, true>), dim3(gr), dim3(R), 0, st, a); break;
+          default: hipLaunchKernelGGL((k_lr<true, true, 128, true>), dim3(gr), dim3(R), 0, st, a); break;
+        }
         launch_reduction<1>(a, gr, R, st);
       } else if (grad && a.agg_ok)
         hipLaunchKernelGGL((k_lr<true, true, kLrBlock>), dim3(g), dim3(kLrBlock), 0, st, a);

@@ -190,6 +190,10 @@ struct FwdArgs {
   u32* red_vmax = nullptr;
   u32* red_vmax_next = nullptr;
   int red_nsub = 1;
+  // producer workgroups the reduction buffers hold (red_hist rows, red_count);
+  // 0: the model's fixed rows per workgroup.  A smaller batch (a slice group
+  // of a step of more than 32 slices) may then run narrower workgroups
+  int red_groups = 0;
   // S > 1: the reduction also writes each slot's slice-presence bits
   // (red_masks[slot] |= 1 << s for every (key, slice) with an occurrence),
   // replacing one global atomic per occurrence (slice_masks) on hot keys

@@ -330,6 +330,7 @@ class Engine {
   int red_nb_ = 0;
   int red_nsub_ = 1;
   int red_maxb_ = 0;  // FwdArgs::red_maxb
+  int red_groups_ = 0;  // FwdArgs::red_groups
   unsigned long long* bcap_ = nullptr;  // current worker set's batch scratch capacity
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
