@@ -581,6 +581,36 @@ void Engine::train_step(const BatchView& b) {
   }
   be_->table_pull(pa);
 
+  // LR over several whole slice groups: one producer pass over the batch
+  // with group-major dests (FwdArgs::red_gm) -- the pulled weights are the
+  // same for every group, so only the sums and the applies run per group
+  // (a producer's time is its column walk, nearly independent of its rows)
+  const bool gm = be_->is_gpu() && lr16 && uq && upos && ng > 1 && S % kSliceGroup == 0 &&
+                  (double)cfg_.max_nnz * ng * kSliceGroup * ps < 4294967295.0;
+  auto gm_args = [&](FwdArgs& fa) {
+    fa.batch = b;
+    fa.pos = pos_;
+    fa.wpull = wpull_;
+    fa.grad = grad_;
+    fa.stats = stats_;
+    fa.model = cfg_.model;
+    fa.S = S;
+    fa.agg_ok = true;  // (gm: the dest bound above)
+    fa.fx_bad = overflow_;
+    set_reduction(fa);
+    fa.red_nuq = n_uniq_;
+    fa.red_gm = 1;
+    fa.red_masks = lr_mask_;
+    fa.red_out = lr_grad_;
+    fa.red_inv = nullptr;
+  };
+  if (gm) {
+    FwdArgs fa;
+    gm_args(fa);
+    fa.red_phase = 1;
+    fa.red_rows = srows;
+    be_->forward_backward(fa);
+  }
   for (int k = 0; k < ng; ++k) {
     const u32* posk = pos_;
     const BatchView bk = group_view(b, S, k, posk);
@@ -628,6 +658,13 @@ void Engine::train_step(const BatchView& b) {
     if (rowu) {
       fa.red_out = row_grad_;
       fa.red_inv = oinv;
+    }
+    if (gm) {  // this group's sums of the one producer pass
+      fa = FwdArgs();
+      gm_args(fa);
+      fa.red_phase = 2;
+      fa.red_group = k;
+      fa.red_rows = srk;
     }
     be_->forward_backward(fa);
 
