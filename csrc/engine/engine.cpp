@@ -585,8 +585,10 @@ void Engine::train_step(const BatchView& b) {
   // with group-major dests (FwdArgs::red_gm) -- the pulled weights are the
   // same for every group, so only the sums and the applies run per group
   // (a producer's time is its column walk, nearly independent of its rows)
-  const bool gm = be_->is_gpu() && lr16 && uq && upos && ng > 1 && S % kSliceGroup == 0 &&
-                  (double)cfg_.max_nnz * ng * kSliceGroup * ps < 4294967295.0;
+  // (reference FM likewise: its compact (B, C) rows go to the unique-order
+  // output, so only the dests themselves must fit 32 bits)
+  const bool gm = be_->is_gpu() && (lr16 || fmu) && uq && upos && ng > 1 &&
+                  S % kSliceGroup == 0 && (double)cfg_.max_nnz * ng * kSliceGroup < 4294967295.0;
   auto gm_args = [&](FwdArgs& fa) {
     fa.batch = b;
     fa.pos = pos_;
@@ -601,14 +603,16 @@ void Engine::train_step(const BatchView& b) {
     fa.red_nuq = n_uniq_;
     fa.red_gm = 1;
     fa.red_masks = lr_mask_;
-    fa.red_out = lr_grad_;
+    fa.red_out = lr16 ? lr_grad_ : fm_grad_;
     fa.red_inv = nullptr;
+    fa.fm_compact = fmu;  // (normalised by the apply: no red_rows)
+    fa.fm_vals = fm_vals_;
   };
   if (gm) {
     FwdArgs fa;
     gm_args(fa);
     fa.red_phase = 1;
-    fa.red_rows = srows;
+    if (lr16) fa.red_rows = srows;
     be_->forward_backward(fa);
   }
   for (int k = 0; k < ng; ++k) {
@@ -664,7 +668,7 @@ void Engine::train_step(const BatchView& b) {
       gm_args(fa);
       fa.red_phase = 2;
       fa.red_group = k;
-      fa.red_rows = srk;
+      if (lr16) fa.red_rows = srk;
     }
     be_->forward_backward(fa);
 

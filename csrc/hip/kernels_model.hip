@@ -880,7 +880,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
           const u64 slot = dest / S, sl = dest - slot * S;
           const u32 o0 = uix(f.inv, slot);
           if (o0 == 0xFFFFFFFFu) return;
-          const u64 o = (u64)o0 * S + sl;
+          const u64 o = ((u64)o0 - obase) * S + sl;
           if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
             const double rows = (double)f.rows[0];
             reinterpret_cast<float2*>(f.out)[o] =
@@ -1003,8 +1003,8 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
     throw std::runtime_error("red_out with several slices needs the slice bits (red_masks)");
   if (a.red_out && a.red_rows && NV == 2 && a.S != 1)
     throw std::runtime_error("red_out: normalised compact FM rows are one-slice (send buffer)");
-  if (a.red_gm && (NV != 1 || !a.red_nuq || !a.red_out || a.red_inv))
-    throw std::runtime_error("group-major reduction: LR, unique positions, unique-order rows");
+  if (a.red_gm && (!a.red_nuq || !a.red_out || a.red_inv || (NV == 2 && (!a.fm_compact || a.red_rows))))
+    throw std::runtime_error("group-major reduction: unique positions, unique-order (compact) rows");
   RedFinal f{a.grad, a.wpull, a.red_gm ? kRedGroupSlices : a.S, a.model.pstride(), a.model.v_dim,
              a.red_out, a.red_inv, a.red_rows, NV == 2 && a.fm_compact,
              a.S > 1 ? a.red_masks : nullptr, a.red_gm ? a.red_nuq : nullptr, a.red_group};
@@ -1734,12 +1734,16 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
     st.add(p, lab);
   }
   if constexpr (kGrad) {
-    const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
-    const u32 S = (u32)a.S;
+    const u32 sg = active ? (u32)slice_of(b, r, a.S) : 0u;
+    // group-major dests (FwdArgs::red_gm, as k_lr): (u + g * unique) * 32 + s % 32
+    const bool gm = a.red_gm != 0;
+    const u32 S = gm ? (u32)kRedGroupSlices : (u32)a.S;
+    const u32 s = gm ? sg % (u32)kRedGroupSlices : sg;
+    const u32 off = gm ? (sg / (u32)kRedGroupSlices) * (u32)*a.red_nuq : 0u;
     const float lv = loss * vsum;
     for (int j = 0; j < maxlen; ++j) {
       const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
-      lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
+      lagg.column(j, pj != a.trash_pos, (pj + off) * S + s, loss, lv);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1879,7 +1883,10 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     if (a.model.fm_math != kFmReference) throw std::runtime_error("fm_vals: reference math only");
     constexpr int R = kFmGroupRows;
     const int gr = (int)((a.batch.rows + R - 1) / R);
-    if (kGrad) {
+    if (kGrad && a.red_phase == 2) {  // one group's sums of the group-major records
+      if (!red || !a.fm_compact) throw std::runtime_error("fm_vals: needs the compact reduction");
+      launch_reduction<2>(a, 0, 0, st);
+    } else if (kGrad) {
       if (!red || !a.fm_compact) throw std::runtime_error("fm_vals: needs the compact reduction");
       const int Rn = narrow_rows(a, R);
       const int gn = (int)((a.batch.rows + Rn - 1) / Rn);
