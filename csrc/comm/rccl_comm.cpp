@@ -66,19 +66,34 @@ void RcclComm::alltoallv_group(const std::vector<A2AOp>& ops, uintptr_t stream) 
   }
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  check(ncclGroupStart(), "ncclGroupStart");
-  for (const A2AOp& op : ops) {
-    const char* s = static_cast<const char*>(op.send);
-    char* r = static_cast<char*>(op.recv);
-    size_t so = 0, ro = 0;
-    for (int p = 0; p < world_; ++p) {
-      const size_t sb = (size_t)op.send_counts[p] * op.elem_bytes;
-      const size_t rb = (size_t)op.recv_counts[p] * op.elem_bytes;
-      if (sb) check(ncclSend(s + so, sb, ncclUint8, p, c, st), "ncclSend");
-      if (rb) check(ncclRecv(r + ro, rb, ncclUint8, p, c, st), "ncclRecv");
-      so += sb;
-      ro += rb;
+  grouped([&] {
+    for (const A2AOp& op : ops) {
+      const char* s = static_cast<const char*>(op.send);
+      char* r = static_cast<char*>(op.recv);
+      size_t so = 0, ro = 0;
+      for (int p = 0; p < world_; ++p) {
+        const size_t sb = (size_t)op.send_counts[p] * op.elem_bytes;
+        const size_t rb = (size_t)op.recv_counts[p] * op.elem_bytes;
+        if (sb) check(ncclSend(s + so, sb, ncclUint8, p, c, st), "ncclSend");
+        if (rb) check(ncclRecv(r + ro, rb, ncclUint8, p, c, st), "ncclRecv");
+        so += sb;
+        ro += rb;
+      }
     }
+  });
+}
+
+// ncclGroupStart, the calls, ncclGroupEnd -- and when a call inside fails,
+// the group is still closed before the error propagates (an open group
+// would swallow every later RCCL call of this thread into it)
+template <typename F>
+void RcclComm::grouped(F&& calls) {
+  check(ncclGroupStart(), "ncclGroupStart");
+  try {
+    calls();
+  } catch (...) {
+    (void)ncclGroupEnd();
+    throw;
   }
   check(ncclGroupEnd(), "ncclGroupEnd");
 }
@@ -97,16 +112,16 @@ void RcclComm::send_recv(const std::vector<int>& peers, const std::vector<uintpt
       throw std::invalid_argument("send_recv: bad peer or size");
   ncclComm_t c = static_cast<ncclComm_t>(comm_);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  check(ncclGroupStart(), "ncclGroupStart");
-  for (size_t i = 0; i < n; ++i) {
-    if (send_bytes[i] > 0)
-      check(ncclSend(reinterpret_cast<const void*>(sends[i]), (size_t)send_bytes[i], ncclUint8,
-                     peers[i], c, st), "ncclSend");
-    if (recv_bytes[i] > 0)
-      check(ncclRecv(reinterpret_cast<void*>(recvs[i]), (size_t)recv_bytes[i], ncclUint8,
-                     peers[i], c, st), "ncclRecv");
-  }
-  check(ncclGroupEnd(), "ncclGroupEnd");
+  grouped([&] {
+    for (size_t i = 0; i < n; ++i) {
+      if (send_bytes[i] > 0)
+        check(ncclSend(reinterpret_cast<const void*>(sends[i]), (size_t)send_bytes[i], ncclUint8,
+                       peers[i], c, st), "ncclSend");
+      if (recv_bytes[i] > 0)
+        check(ncclRecv(reinterpret_cast<void*>(recvs[i]), (size_t)recv_bytes[i], ncclUint8,
+                       peers[i], c, st), "ncclRecv");
+    }
+  });
 }
 
 void RcclComm::alltoall(const void* send, void* recv, int64_t count, int elem_bytes,

@@ -53,6 +53,8 @@ class RcclComm {
   void abort();
 
  private:
+  template <typename F>
+  void grouped(F&& calls);
   void* comm_ = nullptr;  // ncclComm_t
   int world_ = 1, rank_ = 0;
 };

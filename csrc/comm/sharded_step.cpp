@@ -58,20 +58,22 @@ ShardedStep::~ShardedStep() {
     for (auto& v : *vv)
       for (Buf& b : v) all.push_back(&b);
   for (Buf* b : all)
-    if (b->p) be.free(b->p);
+    if (b->p) be.free_stream(b->p);
+  be.synchronize();
 }
 
 void* ShardedStep::get(Buf& b, size_t bytes) {
   if (bytes < 256) bytes = 256;
   if (b.bytes < bytes) {
+    // Stream-ordered: the old buffer is released behind the queued work that
+    // still reads it, the new one is usable by the work queued next -- a
+    // buffer that grows mid-step costs no host wait (no device synchronize)
     Backend& be = e_.backend();
-    if (b.p) {
-      be.synchronize();  // (the old buffer may still be read by queued work)
-      be.free(b.p);
-    }
+    if (b.p) be.free_stream(b.p);
     const size_t n = bytes + bytes / 4 + 4096;
-    b.p = be.alloc(n);
+    b.p = be.alloc_stream(n);
     b.bytes = n;
+    ++buffer_growths;
   }
   return b.p;
 }

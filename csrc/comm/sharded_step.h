@@ -59,7 +59,8 @@ class ShardedStep {
   // was still in flight at a step start / in the middle of a step, the host
   // seconds those waits took, steps whose next keys rode with the gradients,
   // steps that prepared their own batch, steps no rank had data for, bytes
-  // sent + received
+  // sent + received, exchange buffers that grew (stream-ordered, no host wait)
+  int64_t buffer_growths = 0;
   int64_t host_waits = 0, mid_step_waits = 0, early_key_exchanges = 0, inline_prepares = 0,
           empty_steps = 0, bytes_moved = 0, drop_exchanges = 0;
   double host_wait_s = 0.0;

@@ -552,6 +552,7 @@ class CpuBackend final : public Backend {
     committed_ = fb_bytes_ = 0;
   }
   size_t table_committed() const override { return mm_bytes_ ? committed_ : fb_bytes_; }
+  bool table_in_place() const override { return mm_bytes_ != 0; }
   EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {
     // same definition as the HIP kernels: stable order by pctr descending
     EvalMetrics m;

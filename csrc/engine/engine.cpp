@@ -60,7 +60,7 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   if (max_log2_cap_ < log2_cap_) max_log2_cap_ = log2_cap_;
   if (!(cfg_.grow_start > 0.0 && cfg_.grow_start < cfg_.grow_load))
     cfg_.grow_start = 0.75 * cfg_.grow_load;
-  // geometry (backend.h TableView): segments of at most 2^24 slots
+  // geometry (backend.h TableView): segments of at most 2^kMaxSegLog2 (2^20) slots
   table_.seg_log2 = log2_cap_ < kMaxSegLog2 ? log2_cap_ : kMaxSegLog2;
   table_.level = log2_cap_ - table_.seg_log2;
   table_.split = 0;
@@ -699,7 +699,7 @@ void Engine::train_step(const BatchView& b) {
       aa.slice_rows = nullptr;
       aa.nz_stash = stash ? lr_nz_ : nullptr;
     }
-    if (lr16s) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
+    if (lr16s && stash) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
     if (grpst && stash) aa.nz_stash = grp_nz_;
     if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
       aa.grads = fm_grad_;
@@ -1378,12 +1378,14 @@ void Engine::split_to(u64 nseg) {
     const size_t have = be_->table_committed();
     if (bytes > have) {
       const size_t fr = be_->free_memory();
-      if (fr < bytes - have + (size_t)(256u << 20)) {
+      // (a re-allocating backend needs the whole new table next to the old one)
+      const size_t need = be_->table_in_place() ? bytes - have : bytes;
+      if (fr < need + (size_t)(256u << 20)) {
         if (grew) break;  // (what fits was added; the inserts run at a higher load)
         char msg[256];
         std::snprintf(msg, sizeof(msg),
                       "xflow: table growth to %llu slots needs %.2f GB more, %.2f GB free on the device",
-                      (unsigned long long)((N + k) << g), (bytes - have) / 1e9, fr / 1e9);
+                      (unsigned long long)((N + k) << g), need / 1e9, fr / 1e9);
         throw std::runtime_error(msg);
       }
     }

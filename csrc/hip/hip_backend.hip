@@ -95,6 +95,16 @@ class HipBackend final : public Backend {
   void free(void* p) override {
     if (p) (void)hipFree(p);
   }
+  void* alloc_stream(size_t bytes) override {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 16;
+    XF_HIP_CHECK(hipSetDevice(device_));
+    XF_HIP_CHECK(hipMallocAsync(&p, bytes, stream_));
+    return p;
+  }
+  void free_stream(void* p) override {
+    if (p) XF_HIP_CHECK(hipFreeAsync(p, stream_));
+  }
   void memset(void* p, int v, size_t bytes) override {
     if (bytes) XF_HIP_CHECK(hipMemsetAsync(p, v, bytes, stream_));
   }
@@ -281,6 +291,7 @@ class HipBackend final : public Backend {
       (void)hipGetLastError();
     }
     fb_bytes_ = 0;
+    fb_max_ = max_bytes;
     return nullptr;
   }
   void* table_commit(void* base, size_t bytes) override {
@@ -312,6 +323,16 @@ class HipBackend final : public Backend {
       return base;
     }
     if (bytes <= fb_bytes_) return base;
+    // (no virtual memory: every growth re-allocates and copies, so grow
+    // geometrically -- 1.5x, within the reservation and what is free next to
+    // the live table -- instead of one copy of the table per paced split)
+    if (base && fb_bytes_) {
+      size_t want = fb_bytes_ + fb_bytes_ / 2;
+      if (want > fb_max_) want = fb_max_;
+      size_t fr = 0, tot = 0;
+      if (want > bytes && hipMemGetInfo(&fr, &tot) == hipSuccess && want + (512u << 20) <= fr)
+        bytes = want;
+    }
     void* p = alloc(bytes);
     if (base && fb_bytes_) {
       copy_d2d(p, base, fb_bytes_);
@@ -340,6 +361,7 @@ class HipBackend final : public Backend {
     vm_committed_ = 0;
   }
   size_t table_committed() const override { return vm_on_ ? vm_committed_ : fb_bytes_; }
+  bool table_in_place() const override { return vm_on_; }
 
   EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) override {
     EvalMetrics m;
@@ -372,7 +394,7 @@ class HipBackend final : public Backend {
   };
   bool vm_on_ = false;
   void* vm_base_ = nullptr;
-  size_t vm_max_ = 0, vm_gran_ = 0, vm_committed_ = 0, fb_bytes_ = 0;
+  size_t vm_max_ = 0, vm_gran_ = 0, vm_committed_ = 0, fb_bytes_ = 0, fb_max_ = 0;
   hipMemAllocationProp vm_prop_{};
   std::vector<VmChunk> vm_chunks_;
 };

@@ -201,14 +201,21 @@ __device__ __forceinline__ double fx_to_double(long long a) {
 }
 // Fixed point with a per-step scale (MVM's T = loss*M: a product over
 // fields, no static range fits): the step's largest |input| (vmax, float
-// bits, found by the forward) sets 2^fx so that 2^18 inputs of that size
-// still sum inside int64 -- resolution vmax * 2^-44, i.e. float's relative
-// precision on the largest values and deterministic, order-free sums.
-__device__ __forceinline__ int fx_scale_bits(const u32* vmax) {
+// bits, found by the forward) sets 2^fx so that 2^head inputs of that size
+// still sum inside int64 -- head = log2 of the batch's rows (at least 18:
+// one dup-free row contributes one input per (key, slice)), resolution
+// vmax * 2^-(62 - head), i.e. float's relative precision on the largest
+// values and deterministic, order-free sums.
+__host__ __device__ inline int fx_head_bits(int64_t rows) {
+  int h = 0;
+  while (h < 62 && (1ll << h) < rows) ++h;
+  return h < 18 ? 18 : h;
+}
+__device__ __forceinline__ int fx_scale_bits(const u32* vmax, int head) {
   int e = 0;
   const float m = vmax ? __uint_as_float(*vmax) : 0.0f;
   if (m > 0.0f && m == m && m <= 3.0e38f) frexpf(m, &e);
-  const int fx = 44 - e;
+  const int fx = 62 - head - e;
   return fx < 0 ? 0 : (fx > 60 ? 60 : fx);
 }
 __device__ __forceinline__ long long fx_from_rt(float v, int fx) {

@@ -40,6 +40,7 @@ struct RedGeom {
   // below the batch's unique count times S
   const int64_t* nuq;
   int maxb;  // bucket cap (FwdArgs::red_maxb)
+  int fx_head;  // scaled fixed point (MVM): fx_head_bits of the batch's rows
   __device__ __forceinline__ u64 rows() const {
     return nuq ? (u64)*nuq : (bcap ? (u64)*bcap : cap);
   }
@@ -67,7 +68,8 @@ struct RedGeom {
 __host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
   // (group-major dests: every group spans unique x kRedGroupSlices of them)
   const int S = a.red_gm ? (a.S + kRedGroupSlices - 1) / kRedGroupSlices * kRedGroupSlices : a.S;
-  return RedGeom{a.red_bcap, a.red_cap, S, a.red_nuq, a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets};
+  return RedGeom{a.red_bcap, a.red_cap, S, a.red_nuq, a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets,
+                 fx_head_bits(a.batch.rows)};
 }
 
 __device__ __forceinline__ int red_active(const FwdArgs& a, int base) {
@@ -1145,7 +1147,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   constexpr int kFx = FxBits<1>::kFx;
   __shared__ u64 s_tag[1][kSlots];
   __shared__ long long s_acc[1][kSlots * NV];
-  const int fxs = kScaled ? fx_scale_bits(a.red_vmax) : kFx;
+  const int fxs = kScaled ? fx_scale_bits(a.red_vmax, fx_head_bits(a.batch.rows)) : kFx;
   __shared__ unsigned short s_list[1][BLOCK];
   constexpr int kMaxB = vec_red_max_buckets(D);
   __shared__ u32 s_hist[kMaxB];
@@ -1423,7 +1425,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   using Rec = typename VecRedRec<NV>::T;
   __shared__ long long acc[kR * NV];
   // MVM: the step's fixed-point scale (k_fm_std_red kScaled)
-  const int fxs = kMvm ? fx_scale_bits(vmax) : kFx;
+  const int fxs = kMvm ? fx_scale_bits(vmax, geom.fx_head) : kFx;
   __shared__ u32 seen[kR / 32];
   __shared__ u32 s_pre[kSeg ? G : 1];
   __shared__ u32 s_seg[kSeg ? G : 1];

@@ -478,6 +478,12 @@ class Backend {
   // memory
   virtual void* alloc(size_t bytes) = 0;
   virtual void free(void* p) = 0;
+  // Stream-ordered allocation (HIP: hipMallocAsync / hipFreeAsync on the
+  // backend's stream): a buffer freed this way may still be read by work
+  // queued before the free, and neither call waits on the host -- buffers
+  // that grow in the middle of a step (the sharded step's exchange buffers)
+  virtual void* alloc_stream(size_t bytes) { return alloc(bytes); }
+  virtual void free_stream(void* p) { free(p); }
   virtual void memset(void* p, int v, size_t bytes) = 0;
   virtual void fill_u64(u64* p, u64 v, size_t n) = 0;
   virtual void copy_h2d(void* dst, const void* src, size_t bytes) = 0;
@@ -617,6 +623,9 @@ class Backend {
   virtual void table_release(void* base) = 0;
   // bytes of device memory committed to the table range (>= the bytes asked)
   virtual size_t table_committed() const = 0;
+  // true when table_commit extends the range in place (virtual memory); false
+  // when it re-allocates: the new size must then fit NEXT to the old table
+  virtual bool table_in_place() const { return true; }
   // AUC / logloss sums of n predictions (backend memory; labels 0/1 floats)
   virtual EvalMetrics eval_metrics(const float* pctr, const float* labels, int64_t n) = 0;
 };

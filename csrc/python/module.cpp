@@ -261,6 +261,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def_readwrite("host_waits", &ShardedStep::host_waits)
       .def_readwrite("mid_step_waits", &ShardedStep::mid_step_waits)
+      .def_readwrite("buffer_growths", &ShardedStep::buffer_growths)
       .def_readwrite("early_key_exchanges", &ShardedStep::early_key_exchanges)
       .def_readwrite("inline_prepares", &ShardedStep::inline_prepares)
       .def_readwrite("empty_steps", &ShardedStep::empty_steps)

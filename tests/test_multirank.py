@@ -279,3 +279,35 @@ def test_unannounced_batch_drops_early_keys(tmp_path):
                                       np.load(tmp_path / f"k{r}_1.npy"))
         np.testing.assert_array_equal(np.load(tmp_path / f"v{r}_0.npy").view(np.uint32),
                                       np.load(tmp_path / f"v{r}_1.npy").view(np.uint32))
+
+
+def _parse_worker(rank, world, data_dir, out_dir, gpu_parse, resident):
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    # 4 KB blocks of variable-width rows (bundled data: fields 16/17 multi-valued):
+    # several CSR blocks per epoch, the next one announced before the current trains
+    cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
+                      test_prefix=os.path.join(data_dir, "small_test"), epochs=3, threads=4,
+                      pred_dir=out_dir, engine=EngineConfig(table_log2_cap=14),
+                      train_block_bytes=4096, gpu_parse=gpu_parse, resident=resident)
+    t = Trainer(cfg, device=torch.device("cpu"))
+    t.train_epochs(cfg.epochs)
+    t.predict(0)
+
+
+@pytest.mark.parametrize("resident", [False, True])
+def test_device_parse_two_workers_equals_host_parse(tmp_path, resident):
+    """The device tokeniser's stream (TextStream; on the CPU backend it parses
+    with reader.cpp's rules) feeds the 2-rank pipelined step -- which parses
+    block t+1 before block t trains -- and the --resident cache the same
+    variable-width CSR blocks as the host reader: identical models."""
+    from conftest import DATA
+
+    preds = []
+    for tag, gp, res in (("host", False, False), ("dev", True, resident)):
+        d = tmp_path / tag
+        d.mkdir()
+        run_world(_parse_worker, 2, DATA, str(d), gp, res)
+        preds.append(np.loadtxt(d / "pred_0_0.txt"))
+    np.testing.assert_array_equal(preds[0], preds[1])

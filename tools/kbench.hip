@@ -1,6 +1,6 @@
 // Kernel experiment harness (gfx950): times the dedup and LR forward/backward
 // launchers and a few memory-pattern probes on the bench's synthetic
-// Criteo-shaped batch with hipEvents.  Built by scripts/gpu_kbench.sh:
+// Criteo-shaped batch with hipEvents.  Built by scripts/gpu.sh kbench:
 //   hipcc --offload-arch=gfx950 -O3 tools/kbench.hip csrc/hip/kernels_*.hip
 #include <hip/hip_runtime.h>
 

@@ -140,9 +140,8 @@ class TextStream:
         self.stage_s = 0.0   # host seconds reading blocks into the pinned slots
         self.parse_s = 0.0   # host seconds waiting for parses (their counts)
         self.stop = False
-        # device output arrays, grown as needed: a line needs >= 2 bytes, a
-        # feature token >= 4 (" a:b")
-        self._out = None
+        # (device output arrays: one set per block, _arrays; a line needs >= 2
+        # bytes, a feature token >= 4 (" a:b"))
         self._texts = [None, None]  # device text buffers (block t parses while t+1 uploads)
         self._tb = 0
         self._pending = None        # an uploaded block not yet parsed
@@ -167,17 +166,18 @@ class TextStream:
         self.ready.put(None)
 
     def _arrays(self, n: int):
+        """Fresh output arrays for one block.  Every block owns its arrays (the
+        caching allocator on the compute stream recycles them once the block's
+        tensors die, stream-ordered): a multi-rank step announces block t+1 --
+        which parses right away -- before block t trains, and ``--resident``
+        keeps the first epoch's blocks, so reused arrays would alias them."""
         rows = n // 2 + 2
         nnz = n // 4 + 2
-        o = self._out
-        if o is None or o["labels"].numel() < rows or o["keys"].numel() < nnz:
-            dev = self.device
-            o = {"keys": torch.empty(nnz, dtype=torch.int64, device=dev),
-                 "fgid": torch.empty(nnz, dtype=torch.int32, device=dev),
-                 "row_ptr": torch.empty(rows + 1, dtype=torch.int32, device=dev),
-                 "labels": torch.empty(rows, dtype=torch.float32, device=dev)}
-            self._out = o
-        return o
+        dev = self.device
+        return {"keys": torch.empty(nnz, dtype=torch.int64, device=dev),
+                "fgid": torch.empty(nnz, dtype=torch.int32, device=dev),
+                "row_ptr": torch.empty(rows + 1, dtype=torch.int32, device=dev),
+                "labels": torch.empty(rows, dtype=torch.float32, device=dev)}
 
     def next(self) -> Optional[dict]:
         while True:
@@ -268,7 +268,7 @@ def parse_text_file(engine, path: str, block_bytes: int = 2 << 20):
             b = s.next()
             if b is None:
                 break
-            # (copies: the device arrays are reused by the next block)
+            # (host copies of the block's device arrays)
             out.append({k: (v.cpu().numpy().copy() if isinstance(v, torch.Tensor) else v)
                         for k, v in b.items()})
     finally:

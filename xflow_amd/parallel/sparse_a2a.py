@@ -436,6 +436,10 @@ class ShardedEngine:
             if next_batch is not None:
                 next_batch.check(e.device)
             e._sync_stream()
+            # The native step tells batches apart by id(): the announced batch
+            # stays referenced here until the step after it, so no other Batch
+            # can take its id while its prepared dedup and keys are pending.
+            self._native_announced = next_batch
             # (prefetch: called back once the pull is queued, as below)
             return bool(self._native.train_step(
                 batch.view(), id(batch), S, next_batch.view() if next_batch is not None else None,

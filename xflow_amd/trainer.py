@@ -229,8 +229,9 @@ class Trainer:
                 nxt = lambda: next(blocks, None)  # noqa: E731
             else:
                 xfb = binfmt.shard_file(path)
-                gpu_text = (cfg.gpu_parse and not xfb and self.device.type == "cuda"
-                            and self.concurrent)
+                # (on the CPU backend the same stream parses with reader.cpp's
+                # rules through Engine.parse_text: the multi-rank gloo tests)
+                gpu_text = cfg.gpu_parse and not xfb and self.concurrent
                 reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
                           else None if gpu_text
                           else nat.PrefetchReader(path, cfg.train_block_bytes))
