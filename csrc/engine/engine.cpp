@@ -52,6 +52,12 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     throw std::invalid_argument("v_dim must be in [1, 32]");
   be_ = cfg_.device >= 0 ? make_hip_backend(cfg_.device) : make_cpu_backend();
   Backend& be = *be_;
+  // the device kernels' latent widths: any other v_dim runs padded (inert
+  // padded dims, ModelSpec::pad_dim)
+  cfg_.model.pad_dim = 0;
+  if (be.is_gpu() && cfg_.model.kind != kLR &&
+      device_latent_width(cfg_.model.v_dim) != cfg_.model.v_dim)
+    cfg_.model.pad_dim = device_latent_width(cfg_.model.v_dim);
 
   // persistent table
   table_.L = TableLayout::make(cfg_.model, cfg_.opt);
@@ -139,7 +145,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     // values per record: 1 (LR), 2 (reference FM), the vector records of
     // standard FM (1 + D) and MVM (D: per-row T = loss*M sums)
     const bool vec = fm_std || mvm;
-    const int nv = fm_ref ? 2 : (fm_std ? 1 + cfg_.model.v_dim : (mvm ? cfg_.model.v_dim : 1));
+    const int kd = cfg_.model.kernel_dim();
+    const int nv = fm_ref ? 2 : (fm_std ? 1 + kd : (mvm ? kd : 1));
     const int shift = red_shift(nv);
     // u64 words per record slot: nv for LR / reference FM, the vector record otherwise
     const int recw = vec ? vec_rec_words(nv) / 2 : nv;

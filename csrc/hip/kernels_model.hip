@@ -538,7 +538,7 @@ __global__ void __launch_bounds__(fm_block(D)) k_fm(FwdArgs a) {
   if (kGrad) {
     const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
     const u32 S = (u32)a.S;
-    const float gw = standard ? loss : loss * (float)D;
+    const float gw = standard ? loss : loss * (float)a.model.v_dim;  // (real D: padded dims are inert)
     auto contrib = [&](u32 p, float* c) {
       const float4* src = wp4 + (size_t)p * (PS / 4);
       float w[PS];
@@ -1872,7 +1872,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     throw std::runtime_error("red_masks need the FM reduction path");
   if (!kGrad && a.model.fm_math == kFmStandard && a.model.fm_mfma) {
     const int g = (int)((a.batch.rows + 63) / 64);  // 4 waves x 16 rows
-    switch (a.model.v_dim) {
+    switch (a.model.kernel_dim()) {
       case 1: hipLaunchKernelGGL(k_fm_fwd_mfma<1>, dim3(g), dim3(256), 0, st, a); break;
       case 2: hipLaunchKernelGGL(k_fm_fwd_mfma<2>, dim3(g), dim3(256), 0, st, a); break;
       case 4: hipLaunchKernelGGL(k_fm_fwd_mfma<4>, dim3(g), dim3(256), 0, st, a); break;
@@ -1911,7 +1911,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     throw std::runtime_error("red_masks need the standard-FM reduction path");
   if (a.red_out && a.model.fm_math == kFmStandard && !red_std)
     throw std::runtime_error("standard FM red_out needs the vector-record reduction");
-  switch (a.model.v_dim) {
+  switch (a.model.kernel_dim()) {
 #define XF_FM_CASE(DD)                                                                   \
   case DD: {                                                                             \
     constexpr int B = fm_block(DD);                                                      \
@@ -2178,9 +2178,9 @@ static void dispatch_mvm(const FwdArgs& a, hipStream_t st) {
   const bool agg = kGrad && a.agg_ok;
   const bool red = agg && a.red_pairs && a.red_rowv && a.red_nb > 0 &&
                    a.red_nb <= (a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets);
-  if (a.red_masks && a.S > 1 && !(red && a.model.v_dim >= 2))
+  if (a.red_masks && a.S > 1 && !(red && a.model.kernel_dim() >= 2))
     throw std::runtime_error("red_masks need the MVM reduction path");
-  switch (a.model.v_dim) {
+  switch (a.model.kernel_dim()) {
 #define XF_MVM_CASE(DD)                                                                  \
   case DD: {                                                                             \
     constexpr int B = mvm_block(DD);                                                     \

@@ -33,13 +33,30 @@ struct ModelSpec {
   int mvm_math = kMvmCompat;
   int max_fields = 64;  // MVM per-row field buckets (device LDS budget)
   int fm_mfma = 0;      // standard-math FM forward on the matrix cores (HIP, v_dim <= 8)
+  // Latent width the device kernels run at (HIP: the kernels are compiled
+  // for v_dim 1, 2, 4, 8, 10, 16 and 32; any other v_dim runs at the next one
+  // of those, kernel_dim()).  The padded dims are inert: the table holds and
+  // pushes only the P() real params, the pull writes 0 into the padding of
+  // every value row, so a padded dim's latent sums, products and gradients
+  // are exactly 0 and never reach the table.  0: v_dim.
+  int pad_dim = 0;
 
   XF_HD int P() const { return kind == kLR ? 1 : (kind == kFM ? 1 + v_dim : v_dim); }
   XF_HD int p_w() const { return kind == kMVM ? 0 : 1; }
+  XF_HD int kernel_dim() const { return pad_dim > v_dim ? pad_dim : v_dim; }
   // Stride (floats) of one key's row in the pulled-weights / gradient buffers:
-  // 1 for LR, otherwise padded to 16 bytes so kernels use dwordx4 accesses.
-  XF_HD int pstride() const { int p = P(); return p == 1 ? 1 : ((p + 3) & ~3); }
+  // 1 for LR, otherwise (the kernel width's params) padded to 16 bytes so
+  // kernels use dwordx4 accesses.
+  XF_HD int pstride() const {
+    if (kind == kLR) return 1;
+    const int p = kind == kFM ? 1 + kernel_dim() : kernel_dim();
+    return p == 1 ? 1 : ((p + 3) & ~3);
+  }
 };
+// latent widths the HIP model kernels are instantiated for: the smallest >= d
+XF_HD int device_latent_width(int d) {
+  return d <= 2 ? d : (d <= 4 ? 4 : (d <= 8 ? 8 : (d <= 10 ? 10 : (d <= 16 ? 16 : 32))));
+}
 
 struct OptSpec {
   int kind = kFTRL;

@@ -155,3 +155,34 @@ def test_slice_normalisation_f32_division_equals_reference_double():
         f32 = x / np.float32(n)
         f64 = (x.astype(np.float64) / np.float64(n)).astype(np.float32)
         assert np.array_equal(f32.view(np.uint32), f64.view(np.uint32)), n
+
+
+# v_dim the device kernels are not compiled for runs padded to the next
+# compiled width (ModelSpec::pad_dim): the padded dims must stay inert.  MVM
+# with O(1) init and few fields so its products (and gradients) are live.
+ODD_VDIM = [("fm", "reference", "compat", d, 1, "csr", 1e-2) for d in (3, 5, 9, 12)] + \
+    [("fm", "standard", "compat", d, 3, "field", 1e-2) for d in (3, 9)] + \
+    [("mvm", "reference", "fixed", d, 1, "field", 1.0) for d in (3, 5, 9, 12)]
+
+
+def _odd(device, kind, fm_math, mvm_math, v_dim, slices, layout, v_scale):
+    got, want, eng = _run(device, kind, "ftrl", fm_math, mvm_math, slices, v_dim=v_dim,
+                          layout=layout, fields=4 if kind == "mvm" else 6, v_scale=v_scale)
+    assert got.shape[1] == (1 + v_dim if kind == "fm" else v_dim)
+    np.testing.assert_allclose(got, want, rtol=1e-3, atol=1e-5)
+    return eng
+
+
+@pytest.mark.parametrize("kind,fm_math,mvm_math,v_dim,slices,layout,v_scale", ODD_VDIM[:2])
+def test_odd_v_dim_cpu(kind, fm_math, mvm_math, v_dim, slices, layout, v_scale):
+    _odd(torch.device("cpu"), kind, fm_math, mvm_math, v_dim, slices, layout, v_scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,fm_math,mvm_math,v_dim,slices,layout,v_scale", ODD_VDIM)
+def test_odd_v_dim_gpu(gpu_device, kind, fm_math, mvm_math, v_dim, slices, layout, v_scale):
+    """The GPU matches torch_ref for v_dim in {3, 5, 9, 12} (kernels at 4, 8,
+    10, 16); the engine reports the padded kernel width in its row stride."""
+    eng = _odd(gpu_device, kind, fm_math, mvm_math, v_dim, slices, layout, v_scale)
+    p = (1 + v_dim) if kind == "fm" else v_dim
+    assert eng.pstride >= p
