@@ -211,6 +211,10 @@ def main():
         sharded.host_waits = 0
         sharded.mid_step_waits = 0
         sharded.host_wait_s = 0.0
+        sharded.bytes_moved = 0
+        sharded.csr_exchanges = 0
+        sharded.csr_waits = 0
+        sharded.csr_wait_s = 0.0
     mon0 = engine.monitor_wait_seconds
     sync()
     t0 = time.perf_counter()
@@ -221,8 +225,11 @@ def main():
     t_issue = time.perf_counter() - t0  # host time to queue the steps (bounded by monitor lag)
     # of which blocked: on the monitor's run-ahead bound (the device is
     # monitor_lag steps behind) and on split-size reads (multi-rank)
-    t_blocked = engine.monitor_wait_seconds - mon0 + (sharded.host_wait_s if sharded is not None
-                                                      else 0.0)
+    t_blocked = engine.monitor_wait_seconds - mon0 + (
+        sharded.host_wait_s + getattr(sharded, "csr_wait_s", 0.0) if sharded is not None else 0.0)
+    comm = ({"bytes_moved_per_step": int(sharded.bytes_moved) // max(a.steps, 1),
+             "csr_exchanges": int(getattr(sharded, "csr_exchanges", 0)),
+             "csr_waits": int(getattr(sharded, "csr_waits", 0))} if sharded is not None else {})
     sync()
     elapsed = time.perf_counter() - t0
     st = engine.read_stats(reset=True)
@@ -313,6 +320,11 @@ def main():
             **({"host_per_rank": [[round(x, 4) if isinstance(x, float) else x for x in h]
                                   for h in allh]} if world > 1 else {}),
             "monitor_lag": a.monitor_lag,
+            # multi-rank: bytes each rank sent + received per step (keys,
+            # values, gradients; several slices: only the touched (key, slice)
+            # entries), and the steps that ran on the CSR exchange
+            **comm,
+            "csr_steps": int(engine.csr_steps),
         }
         if a.model == "fm":
             out["config"]["v_dim"] = a.v_dim

@@ -1,6 +1,7 @@
 // xflow-amd: native lock-step sharded step (see sharded_step.h).
 #include "sharded_step.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -40,6 +41,9 @@ ShardedStep::ShardedStep(Engine& e, RcclComm* comm, int world, int rank, bool ea
   grads_in_.resize(1);
   masks_out_.resize(1);
   masks_in_.resize(1);
+  csr_tot_ = static_cast<int64_t*>(be.alloc(sizeof(int64_t) * 2 * world_));
+  csr_tot_host_ = static_cast<int64_t*>(be.host_alloc(sizeof(int64_t) * 2 * world_));
+  csr_tot_ready_ = be.event_create();
 }
 
 ShardedStep::~ShardedStep() {
@@ -51,7 +55,11 @@ ShardedStep::~ShardedStep() {
     be.host_free(counts_host_[i]);
     be.event_destroy(counts_ready_[i]);
   }
-  std::vector<Buf*> all = {&recv_keys_, &vals_, &pulled_, &ahead_keys_[0], &ahead_keys_[1]};
+  be.free(csr_tot_);
+  be.host_free(csr_tot_host_);
+  be.event_destroy(csr_tot_ready_);
+  std::vector<Buf*> all = {&recv_keys_, &vals_, &pulled_, &ahead_keys_[0], &ahead_keys_[1],
+                           &csr_cnt_o_, &csr_cnt_i_, &csr_ent_o_, &csr_ent_i_};
   for (auto* v : {&grads_out_, &grads_in_, &masks_out_, &masks_in_, &rk_, &vals_k_})
     for (Buf& b : *v) all.push_back(&b);
   for (auto* vv : {&gin_k_, &gout_k_, &min_k_, &mout_k_})
@@ -267,6 +275,12 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
   a2a_group(ops);
   if (next && !alias) counts_sent(prep_wb_);
 
+  if (e_.csr_slog2(S) >= 0 && e_.backend().csr_exchange()) {
+    // several slices as CSR entries: only the touched (key, slice) pairs move
+    csr_gradients(b, S, sp, pulled, n_send, n_recv, recv_keys, offsets, next, next_id);
+    e_.w_finish();
+    return true;
+  }
   // one gradient exchange per step; a step of more than 32 slices sends one
   // (gradients, masks) pair per slice group in it
   const int gw = e_.grad_width();
@@ -322,6 +336,94 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
   e_.w_finish();
   bytes_moved += (n_send + n_recv) * (8 + 4 * ps + 4 * (int64_t)S * gw);
   return true;
+}
+
+// Gradients of a step of several slices as CSR entries (Engine::
+// w_forward_backward_csr): the reference's per-slice pushes carry only the
+// keys the slice touched (lr_worker.cc:162-175), so instead of a dense
+// [n_send][S x width] block per slice group only the (key, slice) pairs that
+// exist move.  The entries' all-to-all sizes depend on the forward/backward,
+// so the exchange takes two group calls: (entry counts per key + entry
+// totals per owner [+ the next batch's keys]) then, once the host has read
+// the totals, the entries; owners apply source by source from the entries.
+void ShardedStep::csr_gradients(const BatchView& b, int S, const Split& sp, const float* pulled,
+                                int64_t n_send, int64_t n_recv, const u64* recv_keys,
+                                const std::vector<int64_t>& offsets, const BatchView* next,
+                                int64_t next_id) {
+  const int W = world_;
+  const bool alias = self_only();
+  ++csr_exchanges;
+  if (alias) {  // world 1: the owner reads the worker's entries in place
+    e_.w_forward_backward_csr(b, pulled, n_send, S, sp.wb, false, nullptr, nullptr, nullptr, 1,
+                              false, nullptr);
+    e_.s_apply_csr(recv_keys, nullptr, nullptr, offsets, S);
+    // (the logical exchange: keys, values, entry counts -- the entries'
+    // count stays on the device here)
+    bytes_moved += (n_send + n_recv) * (8 + 4 * e_.value_width() + 4);
+    return;
+  }
+  const int eb = e_.csr_entry_bytes();
+  // entries <= (key, slice) pairs <= occurrences
+  const int64_t emax = std::min<int64_t>(b.nnz, n_send * (int64_t)S);
+  u32* cnt_o = static_cast<u32*>(get(csr_cnt_o_, sizeof(u32) * (size_t)n_send));
+  void* ent_o = get(csr_ent_o_, (size_t)eb * (size_t)(emax > 0 ? emax : 1));
+  e_.w_forward_backward_csr(b, pulled, n_send, S, sp.wb, true, cnt_o, ent_o, counts_both_[sp.wb],
+                            W, W > 1, csr_tot_);
+  u32* cnt_i = static_cast<u32*>(get(csr_cnt_i_, sizeof(u32) * (size_t)n_recv));
+  std::vector<RcclComm::A2AOp> ops;
+  ops.push_back({cnt_o, sp.send, cnt_i, sp.recv, (int)sizeof(u32)});
+  RcclComm::A2AOp tot;
+  tot.send = csr_tot_;
+  tot.recv = csr_tot_ + W;
+  tot.send_counts.assign(W, 1);
+  tot.recv_counts.assign(W, 1);
+  tot.elem_bytes = sizeof(int64_t);
+  ops.push_back(tot);
+  if (next && early_keys_) {
+    // the next batch's keys ride in this group call (their split sizes came
+    // with the values exchange)
+    Split s2 = take(*next, next_id, true);
+    const int64_t n2s = last_send, n2r = last_recv;
+    ahead_no_ ^= 1;
+    u64* rk2 = static_cast<u64*>(get(ahead_keys_[ahead_no_], sizeof(u64) * (size_t)n2r));
+    ops.push_back({send_keys_[s2.wb], s2.send, rk2, s2.recv, (int)sizeof(u64)});
+    ahead_.valid = true;
+    ahead_.id = next_id;
+    ahead_.sp = s2;
+    ahead_.n_send = n2s;
+    ahead_.n_recv = n2r;
+    ahead_.keys = rk2;
+    ++early_key_exchanges;
+    last_send = n_send;
+    last_recv = n_recv;
+  }
+  a2a_group(ops);
+  Backend& be = e_.backend();
+  e_.download_small(csr_tot_host_, csr_tot_, sizeof(int64_t) * 2 * W);
+  be.event_record(csr_tot_ready_);
+  if (!be.event_done(csr_tot_ready_)) {
+    ++csr_waits;
+    const auto t0 = std::chrono::steady_clock::now();
+    be.event_wait(csr_tot_ready_);
+    csr_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  std::vector<int64_t> es(W), er(W);
+  int64_t ein = 0, eout = 0;
+  for (int r = 0; r < W; ++r) {
+    es[r] = csr_tot_host_[r];
+    er[r] = csr_tot_host_[W + r];
+    if (es[r] < 0 || er[r] < 0) throw std::runtime_error("CSR exchange: negative entry totals");
+    eout += es[r];
+    ein += er[r];
+  }
+  if (eout > emax) throw std::runtime_error("CSR exchange: more entries than (key, slice) pairs");
+  void* ent_i = get(csr_ent_i_, (size_t)eb * (size_t)(ein > 0 ? ein : 1));
+  ops.clear();
+  ops.push_back({ent_o, es, ent_i, er, eb});
+  a2a_group(ops);
+  e_.s_apply_csr(recv_keys, cnt_i, ent_i, offsets, S);
+  bytes_moved += (n_send + n_recv) * (8 + 4 * e_.value_width() + 4) + (eout + ein) * eb +
+                 16 * (int64_t)W;
 }
 
 void ShardedStep::push_ops(const Pending& p, std::vector<RcclComm::A2AOp>& ops) {

@@ -66,6 +66,11 @@ class ShardedStep {
   double host_wait_s = 0.0;
   int64_t last_send = 0, last_recv = 0;
   int64_t p2p_ops = 0;  // staleness k: push exchanges so far
+  // several slices on the CSR exchange: steps, and the host waits for the
+  // per-owner entry totals (the entries' all-to-all sizes are known only
+  // after the forward/backward)
+  int64_t csr_exchanges = 0, csr_waits = 0;
+  double csr_wait_s = 0.0;
 
  private:
   struct Buf {  // grow-only device buffer
@@ -140,6 +145,17 @@ class ShardedStep {
   std::vector<Buf> rk_, vals_k_;
   std::vector<std::vector<Buf>> gin_k_, gout_k_, min_k_, mout_k_;
   std::deque<Pending> pending_;
+  // CSR exchange: per-key entry counts out / in, packed entries out / in,
+  // per-owner totals (device [2 * world]: send | recv) and their pinned copy
+  Buf csr_cnt_o_, csr_cnt_i_, csr_ent_o_, csr_ent_i_;
+  int64_t* csr_tot_ = nullptr;
+  int64_t* csr_tot_host_ = nullptr;
+  void* csr_tot_ready_ = nullptr;
+  // the gradient half of a CSR step (forward/backward, the two exchanges,
+  // the per-source applies); ops holds the early next-keys op, if any
+  void csr_gradients(const BatchView& b, int S, const Split& sp, const float* pulled,
+                     int64_t n_send, int64_t n_recv, const u64* recv_keys,
+                     const std::vector<int64_t>& offsets, const BatchView* next, int64_t next_id);
 };
 
 }  // namespace xflow

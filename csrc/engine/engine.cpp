@@ -2,6 +2,7 @@
 #include <cstdlib>
 #include "xflow/engine.h"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -34,6 +35,15 @@ constexpr char kMagic[8] = {'X', 'F', 'L', 'O', 'W', 'T', 'B', '1'};
 bool monitor_disabled() {
   static const bool off = std::getenv("XFLOW_NO_MONITOR") != nullptr;
   return off;
+}
+
+// XFLOW_CSR=0: several-slice steps keep the slice-group path (A/B only)
+bool csr_xflow_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("XFLOW_CSR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 }  // namespace
@@ -211,6 +221,7 @@ Engine::~Engine() {
   be.synchronize();
   use_worker_set(cur_wb_);  // (records the current set)
   be.table_release(table_.words);
+  be.free_stream(csr_roff_);
   void* ptrs[] = {mon_, scratch_.keys, scratch_.stamps,
                   scratch_.claims, block_counts_, uniq_keys_, uniq_slot_, wpull_, grad_, tmask_,
                   stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
@@ -218,7 +229,8 @@ Engine::~Engine() {
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, grp_nz_, own_keys_, fm_grad_,
                   row_grad_,
-                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_};
+                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_,
+                  csr_cnt_, csr_doff_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
   for (SrvBuf& b : srv_) {
@@ -463,11 +475,230 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
 }
 
 
+// log2 of the padded slice count when a step of S slices takes the CSR path
+int Engine::csr_slog2(int S) const {
+  if (S <= 1 || cfg_.sum_slices || !red_pairs_ || !be_->remaps_positions()) return -1;
+  const TableLayout& L = table_.L;
+  const bool lr16 = cfg_.model.kind == kLR && L.stride == 4 && L.P == 1 && L.opt == kFTRL &&
+                    !L.has_flag;
+  if (!lr16 && !fm_vals_) return -1;
+  int sl = 0;
+  while ((1 << sl) < S) ++sl;
+  // (a key's dests inside one reduction bucket; dests = unique * 2^sl in 32 bits)
+  if (sl > red_shift(fm_vals_ ? 2 : 1) || (double)cfg_.max_nnz * (double)(1 << sl) >= 4294967295.0)
+    return -1;
+  return sl;
+}
+
+// Several slices, one pass: dedup -> pull (stash) -> one producer pass over
+// every slice with dests unique * 2^slog2 + slice -> the CSR reduction (only
+// the touched (key, slice) pairs) -> one apply whose per-key chains push the
+// slices in order.  Replaces the slice groups' per-group sums and applies.
+void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
+  const int32_t* srows = slice_rows_dev(b, S);
+  const bool fm = fm_vals_;
+  ensure_inv();
+  if (!csr_off_) {
+    csr_off_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
+    csr_cnt_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
+  }
+  float* stash;
+  if (fm) {
+    if (!grp_nz_) grp_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * table_.L.P);
+    stash = grp_nz_;
+  } else {
+    if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
+    stash = lr_nz_;
+  }
+  dedup_(b, 1, nullptr, true);
+  inv_valid_ = false;
+  be_->remap_pos(pos_, b.nnz, inv_, (u32)scratch_.cap);
+  guard_inserts(b.nnz);
+
+  PullArgs pa;
+  pa.table = table_;
+  pa.opt = cfg_.opt;
+  pa.keys = uniq_keys_;
+  pa.n_dev = n_uniq_;
+  pa.n_max = b.nnz;
+  pa.insert = true;
+  pa.out_slot = uniq_slot_;
+  pa.out_vals = wpull_;
+  pa.pstride = pstride();
+  pa.fm_vals = fm;
+  pa.out_nz = stash;
+  be_->table_pull(pa);
+
+  // (reference FM: the raw (B, C) are normalised by the apply, after the
+  // expansion, as the slice-group path does)
+  csr_forward_backward(b, slog2, srows, !fm);
+
+  ApplyArgs aa;
+  aa.table = table_;
+  aa.opt = cfg_.opt;
+  aa.keys = uniq_keys_;
+  aa.slots = uniq_slot_;
+  aa.n_dev = n_uniq_;
+  aa.n_max = b.nnz;
+  aa.S = S;
+  aa.pstride = pstride();
+  aa.P = cfg_.model.P();
+  aa.fm_compact = fm;
+  aa.fm_D = cfg_.model.v_dim;
+  aa.slice_rows = fm ? srows : nullptr;
+  aa.nz_stash = stash;
+  aa.csr_off = csr_off_;
+  aa.csr_cnt = csr_cnt_;
+  aa.csr_ent = red_pairs_;
+  attach_snapshot(aa);
+  be_->table_apply(aa);
+  end_step();
+}
+
+void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* srows,
+                                  bool normalise) {
+  if (!csr_off_) {
+    csr_off_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
+    csr_cnt_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
+  }
+  FwdArgs fa;
+  fa.batch = b;
+  fa.pos = pos_;
+  fa.wpull = wpull_;
+  fa.grad = grad_;
+  fa.stats = stats_;
+  fa.model = cfg_.model;
+  fa.S = 1 << slog2;
+  fa.agg_ok = true;  // (dests below max_nnz * 2^slog2 < 2^32: csr_slog2)
+  fa.fx_bad = overflow_;
+  set_reduction(fa);
+  fa.red_nuq = n_uniq_;
+  fa.fm_compact = fm_vals_;
+  fa.fm_vals = fm_vals_;
+  fa.red_csr.off = csr_off_;
+  fa.red_csr.cnt = csr_cnt_;
+  fa.red_csr.ent = red_pairs_;
+  fa.red_csr.slog2 = slog2;
+  fa.red_csr.rows = normalise ? srows : nullptr;
+  be_->forward_backward(fa);
+  ++csr_steps_;
+}
+
+void Engine::w_forward_backward_csr(const BatchView& b, const float* pulled, int64_t n_send,
+                                    int S_global, int wb, bool pack, u32* cnt_out, void* ent_out,
+                                    const int64_t* counts, int world, bool encoded,
+                                    int64_t* totals_out) {
+  use_worker_set(wb);
+  const int St = S_global > 0 ? S_global : slices_of(b);
+  const int sl = csr_slog2(St);
+  if (sl < 0 || St < slices_of(b) || St > cfg_.max_slices)
+    throw std::invalid_argument("w_forward_backward_csr: S_global off the CSR path");
+  // (a rank out of data -- a batch of 0 rows -- still takes part: no keys,
+  // zero entries per owner)
+  if (b.nnz > 0 && !inv_valid_)
+    throw std::logic_error("w_forward_backward_csr: needs the partitioned dedup's inv");
+  // unique-index (= send-order) positions, and the pulled rows (send order)
+  // as the forward's value rows; the trash slot's row stays zero
+  be_->remap_pos(pos_, b.nnz, inv_, (u32)scratch_.cap);
+  be_->scatter_rows(pulled, wpull_, nullptr, nullptr, n_send, vstride_);
+  // (rows per slice: the worker normalises, the owner does not know them)
+  csr_forward_backward(b, sl, slice_rows_dev(b, St), true);
+  last_nsend_ = n_send;
+  if (!pack) return;
+  if (!csr_doff_) csr_doff_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz + 1);
+  be_->scan_u32(csr_cnt_, csr_doff_, n_uniq_, cfg_.max_nnz);
+  be_->csr_pack(csr_off_, csr_cnt_, red_pairs_, csr_doff_, n_uniq_, cfg_.max_nnz, ent_out,
+                csr_entry_bytes());
+  be_->copy_d2d(cnt_out, csr_cnt_, sizeof(u32) * (size_t)n_send);
+  be_->csr_totals(counts, world, encoded, csr_doff_, totals_out);
+}
+
+void Engine::s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* recv_ent,
+                         const std::vector<int64_t>& src_offsets, int S, int buf) {
+  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, 8)");
+  SrvBuf& sb = srv_[buf];
+  sb.keys = nullptr;  // applied: no slot remap needed after a growth
+  bool stash = sb.nz_fresh;
+  stale_stashes();
+  const u32* off = csr_off_;
+  const u32* cnt = csr_cnt_;
+  const void* ent = red_pairs_;
+  const int64_t n = src_offsets.empty() ? 0 : src_offsets.back();
+  if (n > sb.n) throw std::invalid_argument("s_apply_csr: offsets beyond pull");
+  if (recv_cnt) {  // received entries: offsets by a scan of the counts
+    if (n + 1 > csr_roff_cap_) {
+      be_->free_stream(csr_roff_);
+      csr_roff_cap_ = n + n / 4 + 1024;
+      csr_roff_ = static_cast<u32*>(be_->alloc_stream(sizeof(u32) * (size_t)csr_roff_cap_));
+    }
+    be_->scan_u32(recv_cnt, csr_roff_, nullptr, n);
+    off = csr_roff_;
+    cnt = recv_cnt;
+    ent = recv_ent;
+  }
+  size_t first_src = 0;
+  while (first_src + 1 < src_offsets.size() && src_offsets[first_src + 1] <= src_offsets[first_src])
+    ++first_src;
+  for (size_t src = 0; src + 1 < src_offsets.size(); ++src) {
+    const int64_t o = src_offsets[src], c = src_offsets[src + 1] - o;
+    if (c <= 0) continue;
+    ApplyArgs aa;
+    aa.table = table_;
+    aa.opt = cfg_.opt;
+    aa.keys = recv_keys + o;
+    aa.slots = sb.slots + o;
+    aa.n_host = c;
+    aa.n_max = c;
+    aa.S = S;
+    aa.pstride = pstride();
+    aa.P = cfg_.model.P();
+    aa.fm_compact = fm_vals_;
+    aa.fm_D = cfg_.model.v_dim;
+    if (fm_vals_) {
+      aa.pulled = pulled_weights(buf, o);
+      if (!aa.pulled && src > first_src)
+        throw std::logic_error("s_apply_csr: compact FM rows of several sources need s_pull's weights");
+    }
+    // (entries normalised by the workers; entry indices are global)
+    aa.csr_off = off + o;
+    aa.csr_cnt = cnt + o;
+    aa.csr_ent = ent;
+    if (stash) aa.nz_stash = sb.nz ? sb.nz + 2 * o : nullptr;
+    stash = false;
+    attach_snapshot(aa);
+    be_->table_apply(aa);
+  }
+}
+
+void Engine::csr_debug(std::vector<u32>& off, std::vector<u32>& cnt, std::vector<u32>& words) {
+  off.clear();
+  cnt.clear();
+  words.clear();
+  if (!csr_off_) return;
+  const int64_t n = n_unique();
+  off.resize((size_t)n);
+  cnt.resize((size_t)n);
+  be_->copy_d2h(off.data(), csr_off_, sizeof(u32) * (size_t)n);
+  be_->copy_d2h(cnt.data(), csr_cnt_, sizeof(u32) * (size_t)n);
+  u64 end = 0;
+  for (int64_t i = 0; i < n; ++i) end = std::max<u64>(end, (u64)off[i] + cnt[i]);
+  const int w = csr_entry_bytes() / 4;
+  words.resize((size_t)end * w);
+  if (end) be_->copy_d2h(words.data(), red_pairs_, sizeof(u32) * (size_t)end * w);
+}
+
 void Engine::train_step(const BatchView& b) {
   stale_stashes();  // the table changes: server stashes are stale
   use_worker_set(0);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
+  {
+    const int sl = csr_xflow_env() ? csr_slog2(S) : -1;
+    if (sl >= 0) {
+      train_step_csr(b, S, sl);
+      return;
+    }
+  }
   const int ng = slice_groups(S);
   if (ng > 1 && cfg_.sum_slices)
     throw std::invalid_argument("sum_slices: at most 32 slices per step (ordered pushes: any count)");

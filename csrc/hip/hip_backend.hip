@@ -36,6 +36,11 @@ class HipBackend final : public Backend {
     }
     if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
     if (counter_) (void)hipFree(counter_);
+    if (scan_tiles_) {  // (stream-ordered allocation; the caller's stream may be gone)
+      (void)hipDeviceSynchronize();
+      (void)hipFreeAsync(scan_tiles_, own_stream_);
+      (void)hipStreamSynchronize(own_stream_);
+    }
     if (split_marks_) (void)hipFree(split_marks_);
     if (own_stream_) (void)hipStreamDestroy(own_stream_);
   }
@@ -211,6 +216,24 @@ class HipBackend final : public Backend {
   bool owner_grouping() const override { return true; }
   void owner_group(const OwnerGroupArgs& a) override { hip::launch_owner_group(a, stream_); }
   void gather_grads(const GatherGradArgs& a) override { hip::launch_gather_grads(a, stream_); }
+  bool csr_exchange() const override { return true; }
+  void scan_u32(const u32* in, u32* out, const int64_t* n_dev, int64_t n_max) override {
+    const size_t words = (size_t)(n_max / 4096 + 4);
+    if (words > scan_tiles_words_) {  // (grow-only, stream-ordered: no host wait)
+      if (scan_tiles_) free_stream(scan_tiles_);
+      scan_tiles_words_ = words + words / 2;
+      scan_tiles_ = static_cast<u32*>(alloc_stream(scan_tiles_words_ * sizeof(u32)));
+    }
+    hip::launch_scan_u32(in, out, n_dev, n_max, scan_tiles_, stream_);
+  }
+  void csr_pack(const u32* off, const u32* cnt, const void* src, const u32* doff,
+                const int64_t* n_dev, int64_t n_max, void* dst, int entry_bytes) override {
+    hip::launch_csr_pack(off, cnt, src, doff, n_dev, n_max, dst, entry_bytes, stream_);
+  }
+  void csr_totals(const int64_t* counts, int world, bool encoded, const u32* doff,
+                  int64_t* totals) override {
+    hip::launch_csr_totals(counts, world, encoded, doff, totals, stream_);
+  }
   void scatter_rows(const float* src, float* dst, const u32* map, const int64_t* n_dev,
                     int64_t n_max, int width, float* zero_out, int zero_width) override {
     hip::launch_scatter_rows(src, dst, map, n_dev, n_max, width, zero_out, zero_width, stream_);
@@ -395,6 +418,8 @@ class HipBackend final : public Backend {
   bool vm_on_ = false;
   void* vm_base_ = nullptr;
   size_t vm_max_ = 0, vm_gran_ = 0, vm_committed_ = 0, fb_bytes_ = 0, fb_max_ = 0;
+  u32* scan_tiles_ = nullptr;
+  size_t scan_tiles_words_ = 0;
   hipMemAllocationProp vm_prop_{};
   std::vector<VmChunk> vm_chunks_;
 };

@@ -30,6 +30,14 @@ void launch_gather_u32(const u32* src, u32* dst, const u32* map, const int64_t* 
 void launch_scatter_u32(const u32* src, u32* dst, const u32* map, const int64_t* n_dev,
                         int64_t n_max, hipStream_t st);
 void launch_fill_u64(u64* p, u64 v, size_t n, hipStream_t st);
+// CSR exchange: exclusive scan (out[n] = total; tiles: n_max / 4096 + 2 words)
+void launch_scan_u32(const u32* in, u32* out, const int64_t* n_dev, int64_t n_max, u32* tiles,
+                     hipStream_t st);
+void launch_csr_pack(const u32* off, const u32* cnt, const void* src, const u32* doff,
+                     const int64_t* n_dev, int64_t n_max, void* dst, int entry_bytes,
+                     hipStream_t st);
+void launch_csr_totals(const int64_t* counts, int world, bool encoded, const u32* doff,
+                       int64_t* totals, hipStream_t st);
 void launch_upload_small(void* dst, const void* src, size_t bytes, hipStream_t st);
 void launch_download_small(void* host_dst, const void* src, size_t bytes, hipStream_t st);
 void launch_snapshot(HostSnap* dst, const u32* mon, unsigned long long seq, hipStream_t st);

@@ -987,6 +987,239 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// CSR reduction (FwdArgs::red_csr): every slice of the step in one pass.
+// Dests are key * 2^slog2 + slice, so a bucket's dests are whole keys and
+// the bucket's distinct dests in dest order ARE its keys' entries in (key,
+// slice) order.  Per bucket (one workgroup), per window of 2^16 dests:
+//   1. a presence bitmap of the window's dests (one bit per dest: 8 KB) and
+//      its prefix popcounts -> the rank of every present dest;
+//   2. per key of the window: cnt = its present slices, off = rank of the
+//      first (entries start at the bucket's first record index: a bucket
+//      has at most as many distinct dests as records);
+//   3. the sums: an LDS hash table keyed by dest when the window holds at
+//      most kCsrHash / 2 records (the common case: a bucket's records are a
+//      sparse sample of its dests), else direct-indexed sub-windows of
+//      kCsrHash dests; fixed-point int64 (order-free, deterministic), each
+//      distinct dest written once at its rank.
+// A bucket of at most kCsrReg * kCsrBlock records keeps them in registers
+// across the passes.
+// ---------------------------------------------------------------------------
+constexpr int kCsrBlock = 512;
+constexpr int kCsrWinLog2 = 16;
+constexpr int kCsrWords = 1 << (kCsrWinLog2 - 5);
+constexpr int kCsrHash = 4096;
+constexpr int kCsrReg = 4;
+
+template <int NV>
+__global__ void __launch_bounds__(kCsrBlock) k_red_csr(const void* __restrict__ sorted,
+                                                       const u32* __restrict__ start, CsrOut c,
+                                                       RedGeom geom, int nb) {
+  using T = typename RedRec<NV>::T;
+  constexpr int kFx = FxBits<NV>::kFx;
+  constexpr int kWaves = kCsrBlock / kWave;
+  __shared__ u32 bits[kCsrWords];
+  __shared__ u32 wscan[kCsrWords];
+  __shared__ u32 tag[kCsrHash];
+  __shared__ long long acc[kCsrHash * NV];
+  __shared__ u32 s_part[kWaves];
+  const int shift = geom.shift(red_shift(NV));
+  const int b = (int)blockIdx.x;
+  if (b >= geom.active(shift, nb)) return;
+  const u32 beg = start[b], end = start[b + 1];
+  if (beg == end) return;  // (no records: no key of the batch has a dest here)
+  const u64 nuq = *geom.nuq;
+  const T* src = static_cast<const T*>(sorted);
+  const u64 blo = (u64)b << shift, bhi = blo + (1ull << shift);
+  const int wl2 = shift < kCsrWinLog2 ? shift : kCsrWinLog2;
+  const u32 wn = 1u << wl2;
+  const int sl = c.slog2;
+  const u32 smask = (1u << sl) - 1u;
+  const u32 nrec = end - beg;
+  const int tid = (int)threadIdx.x;
+  const bool reg = nrec <= (u32)(kCsrReg * kCsrBlock) && shift <= kCsrWinLog2;
+  T pr[kCsrReg];
+  u32 pd[kCsrReg];  // (reg) the record's dest - blo, ~0: none
+#pragma unroll
+  for (int q = 0; q < kCsrReg; ++q) {
+    pd[q] = ~0u;
+    const u32 i = beg + (u32)tid + (u32)q * kCsrBlock;
+    if (reg && i < end) {
+      pr[q] = src[i];
+      pd[q] = (u32)((u64)RedRec<NV>::dest(pr[q]) - blo);
+    }
+  }
+  auto rank = [&](u32 d) -> u32 {
+    return wscan[d >> 5] + (u32)__popc(bits[d >> 5] & ((1u << (d & 31)) - 1u));
+  };
+  auto emit = [&](u32 o, u32 d, const long long* a) {
+    const u32 slice = d & smask;
+    const double rows = c.rows ? (double)c.rows[slice] : 1.0;
+    if constexpr (NV == 1) {
+      const float v = (float)(fx_to_double<kFx>(a[0]) / rows);
+      static_cast<u64*>(c.ent)[o] = (u64)slice | ((u64)__float_as_uint(v) << 32);
+    } else {
+      const float B = (float)(fx_to_double<kFx>(a[0]) / rows);
+      const float C = (float)(fx_to_double<kFx>(a[1]) / rows);
+      static_cast<uint3*>(c.ent)[o] = make_uint3(slice, __float_as_uint(B), __float_as_uint(C));
+    }
+  };
+  auto add = [&](u32 h, const T& r) {
+    if constexpr (NV == 1) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[h]),
+                (unsigned long long)fx_from<kFx>(__uint_as_float((u32)(r >> 32))));
+    } else {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[2 * h]),
+                (unsigned long long)fx_from<kFx>(__uint_as_float(r.y)));
+      atomicAdd(reinterpret_cast<unsigned long long*>(&acc[2 * h + 1]),
+                (unsigned long long)fx_from<kFx>(__uint_as_float(r.z)));
+    }
+  };
+  u32 out = beg;
+  for (u64 wlo = blo; wlo < bhi; wlo += wn) {
+    const u32 woff = (u32)(wlo - blo);
+    // 1. presence bitmap of the window
+    for (u32 i = (u32)tid; i < (wn >> 5); i += kCsrBlock) bits[i] = 0u;
+    lds_barrier();
+    u32 mine = 0;
+    if (reg) {
+#pragma unroll
+      for (int q = 0; q < kCsrReg; ++q) {
+        const u32 d = pd[q] - woff;
+        if (pd[q] != ~0u && d < wn) {
+          atomicOr(&bits[d >> 5], 1u << (d & 31));
+          ++mine;
+        }
+      }
+    } else {
+      for (u32 i = beg + (u32)tid; i < end; i += kCsrBlock) {
+        const u64 d = (u64)RedRec<NV>::dest(src[i]) - wlo;
+        if (d < wn) {
+          atomicOr(&bits[d >> 5], 1u << (d & 31));
+          ++mine;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o);
+    if (tid % kWave == 0) s_part[tid / kWave] = mine;
+    lds_barrier();
+    u32 nwin = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) nwin += s_part[w];
+    if (nwin == 0) continue;  // (block-uniform)
+    // prefix popcounts: each lane scans wn / 32 / kCsrBlock consecutive words
+    constexpr int kPer = kCsrWords / kCsrBlock;
+    const u32 nwords = wn >> 5;
+    u32 loc[kPer], tl = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const u32 w = (u32)tid * kPer + (u32)q;
+      loc[q] = w < nwords ? (u32)__popc(bits[w]) : 0u;
+      tl += loc[q];
+    }
+    u32 total;
+    u32 ex = block_exclusive_scan<kCsrBlock>(tl, &total);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const u32 w = (u32)tid * kPer + (u32)q;
+      if (w < nwords) wscan[w] = ex;
+      ex += loc[q];
+    }
+    lds_barrier();
+    // 2. per key: entry count and first entry
+    {
+      const u64 k0 = wlo >> sl;
+      const u32 nk = wn >> sl;
+      for (u32 kk = (u32)tid; kk < nk; kk += kCsrBlock) {
+        const u64 k = k0 + kk;
+        if (k >= nuq) break;
+        const u32 o = kk << sl;
+        u32 cnt = 0, first = ~0u;
+        if (sl < 5) {  // (the key's 2^sl presence bits inside one word)
+          const u32 m = (bits[o >> 5] >> (o & 31)) & ((1u << (1u << sl)) - 1u);
+          cnt = (u32)__popc(m);
+          if (m) first = o + (u32)__ffs(m) - 1u;
+        } else {
+          for (u32 w = 0; w < (1u << (sl - 5)); ++w) {
+            const u32 x = bits[(o >> 5) + w];
+            cnt += (u32)__popc(x);
+            if (x && first == ~0u) first = o + 32u * w + (u32)__ffs(x) - 1u;
+          }
+        }
+        c.cnt[k] = cnt;
+        c.off[k] = out + (cnt ? rank(first) : 0u);
+      }
+    }
+    // 3. sums, each distinct dest written once at its rank
+    if (nwin <= (u32)(kCsrHash / 2)) {
+      for (u32 i = (u32)tid; i < (u32)kCsrHash; i += kCsrBlock) {
+        tag[i] = ~0u;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[i * NV + v] = 0ll;
+      }
+      lds_barrier();
+      auto insert = [&](u32 d, const T& r) {
+        u32 h = (d * 0x9E3779B1u) >> (32 - ilog2c(kCsrHash));
+        while (true) {
+          const u32 cur = tag[h];
+          if (cur == d) break;
+          if (cur == ~0u) {
+            const u32 old = atomicCAS(&tag[h], ~0u, d);
+            if (old == ~0u || old == d) break;
+          }
+          h = (h + 1) & (kCsrHash - 1);
+        }
+        add(h, r);
+      };
+      if (reg) {
+#pragma unroll
+        for (int q = 0; q < kCsrReg; ++q) {
+          const u32 d = pd[q] - woff;
+          if (pd[q] != ~0u && d < wn) insert(d, pr[q]);
+        }
+      } else {
+        for (u32 i = beg + (u32)tid; i < end; i += kCsrBlock) {
+          const T r = src[i];
+          const u64 d = (u64)RedRec<NV>::dest(r) - wlo;
+          if (d < wn) insert((u32)d, r);
+        }
+      }
+      lds_barrier();
+      for (u32 i = (u32)tid; i < (u32)kCsrHash; i += kCsrBlock) {
+        const u32 d = tag[i];
+        if (d != ~0u) emit(out + rank(d), d, &acc[i * NV]);
+      }
+      lds_barrier();
+    } else {
+      for (u32 sub = 0; sub < wn; sub += kCsrHash) {
+        for (u32 i = (u32)tid; i < (u32)(kCsrHash * NV); i += kCsrBlock) acc[i] = 0ll;
+        lds_barrier();
+        if (reg) {
+#pragma unroll
+          for (int q = 0; q < kCsrReg; ++q) {
+            const u32 d = pd[q] - woff - sub;
+            if (pd[q] != ~0u && d < (u32)kCsrHash && pd[q] - woff < wn) add(d, pr[q]);
+          }
+        } else {
+          for (u32 i = beg + (u32)tid; i < end; i += kCsrBlock) {
+            const T r = src[i];
+            const u64 d = (u64)RedRec<NV>::dest(r) - wlo - sub;
+            if (d < (u64)kCsrHash) add((u32)d, r);
+          }
+        }
+        lds_barrier();
+        for (u32 l = (u32)tid; l < (u32)kCsrHash; l += kCsrBlock) {
+          const u32 d = sub + l;
+          if ((bits[d >> 5] >> (d & 31)) & 1u) emit(out + rank(d), d, &acc[l * NV]);
+        }
+        lds_barrier();
+      }
+    }
+    out += total;
+  }
+}
+
 template <int NV>
 static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, hipStream_t st) {
   u32* start = a.red_tot + a.red_nb + 1;
@@ -999,6 +1232,14 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
                        red_geom(a));
   }
   if (a.red_phase == 1) return;
+  if (a.red_csr.cnt) {
+    if (!a.red_nuq || a.red_gm || a.red_out || a.S != (1 << a.red_csr.slog2) ||
+        a.red_csr.slog2 > red_shift(NV) || (NV == 2 && !a.fm_compact))
+      throw std::runtime_error("CSR reduction: unique positions, S = 2^slog2 <= 2^shift, no other outputs");
+    hipLaunchKernelGGL(k_red_csr<NV>, dim3(a.red_nb), dim3(kCsrBlock), 0, st,
+                       static_cast<const void*>(a.red_sorted), start, a.red_csr, red_geom(a), a.red_nb);
+    return;
+  }
   if (a.red_out && (NV == 2 ? !a.fm_compact : false))
     throw std::runtime_error("red_out: compact rows (reference FM)");
   if (a.red_out && a.S != 1 && !a.red_masks)

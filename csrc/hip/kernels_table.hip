@@ -1063,6 +1063,55 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
   }
 }
 
+// LR-FTRL, 16-byte slots, CSR gradients (ApplyArgs::csr_*, one launch for
+// every slice of the step): a key's entries are its slices' normalised sums in
+// slice order -- the reference's per-slice pushes of only the keys a slice
+// touched (lr_worker.cc:162-175) -- applied as a chain on (n, z) held in
+// registers (sqrt(n) carried), the slot written once.  The first entries of
+// the next keys are loaded before this key's chain.
+__global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
+  XF_APPLY_SNAPSHOT(a);
+  const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const FtrlParams fp = a.opt.ftrl;
+  const u64* __restrict__ ent = static_cast<const u64*>(a.csr_ent);
+  struct In {
+    u32 slot, off, cnt;
+    u64 e0;
+    float2 nz;
+  };
+  auto load = [&](int64_t i) {
+    In x;
+    x.slot = a.slots[i];
+    x.off = a.csr_off[i];
+    x.cnt = a.csr_cnt[i];
+    x.e0 = x.cnt ? ent[x.off] : 0ull;
+    x.nz = make_float2(0.0f, 0.0f);
+    if (x.slot != kNoSlot && x.cnt)
+      x.nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i]
+                        : *reinterpret_cast<const float2*>(a.table.words + (u64)x.slot * 4 + 2);
+    return x;
+  };
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  In nx;
+  if (i < n) nx = load(i);
+  for (; i < n; i += stride) {
+    const In x = nx;
+    if (i + stride < n) nx = load(i + stride);
+    if (x.slot == kNoSlot || !x.cnt) continue;
+    float2 nz = x.nz;
+    float sn = sqrtf(nz.x);
+    u64 e = x.e0;
+    for (u32 j = 0;;) {
+      const float w = ftrl_weight_sn(nz.y, sn, fp);
+      ftrl_push_sn(nz.x, nz.y, sn, w, __uint_as_float((u32)(e >> 32)), fp);
+      if (++j == x.cnt) break;
+      e = ent[x.off + j];
+    }
+    *reinterpret_cast<float2*>(a.table.words + (u64)x.slot * 4 + 2) = nz;
+  }
+}
+
 __global__ void __launch_bounds__(kBlock) k_apply_generic(ApplyArgs a) {
   XF_APPLY_SNAPSHOT(a);
   int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
@@ -1307,6 +1356,21 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
           e = (u32)v;
         }
         const u32 row = a.grad_map ? a.grad_map[e] : e;
+        if (a.csr_cnt) {
+          // CSR entries (slice, B, C) of compact reference-FM rows, in slice
+          // order; the raw sums are normalised here (slice_rows) or by the
+          // producing worker (null)
+          const u32 c0 = a.csr_off[row], cn = a.csr_cnt[row];
+          const uint3* ce = static_cast<const uint3*>(a.csr_ent) + c0;
+          any |= cn;
+          for (u32 j = 0; j < cn; ++j) {
+            const uint3 x = ce[j];
+            const float Bv = __uint_as_float(x.y), Cv = __uint_as_float(x.z);
+            const float raw = p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
+            push(norm_grad(raw, a.slice_rows, (int)x.x));
+          }
+          continue;
+        }
         const float* g = a.grads + (size_t)row * S * gs;
         const u32 m = a.masks ? a.masks[row] : all;
         if (a.masks_clear && p == 0) const_cast<u32*>(a.masks)[row] = 0u;
@@ -1355,7 +1419,14 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
                            !a.grp.oidx;
   if (a.nz_stash && !a.keys && !a.grp.oidx && L.P > 1)
     throw std::runtime_error("table_apply: a stash needs the entries' keys");
-  if (a.grp.oidx) {
+  if (a.csr_cnt) {
+    if (a.zero_after || a.reset_pos || a.sum_slices || a.grp.oidx || a.grad_map)
+      throw std::runtime_error("CSR apply: bad arguments");
+    if (lr16_slot) hipLaunchKernelGGL(k_apply_lr16_csr, dim3(grid), dim3(kBlock), 0, st, a);
+    else if (a.fm_compact && L.P <= kWave)
+      hipLaunchKernelGGL(k_apply_group<true>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+    else throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots or compact reference-FM rows");
+  } else if (a.grp.oidx) {
     if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");
     if (lr16) hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);
     else if (a.S > 1)
@@ -1373,6 +1444,142 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   } else {
     hipLaunchKernelGGL(k_apply_generic, dim3(grid), dim3(kBlock), 0, st, a);
   }
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// CSR exchange helpers (the multi-rank step of several slices): exclusive
+// scan of per-key entry counts, dense packing of the entries in send order,
+// per-owner entry totals.
+// ---------------------------------------------------------------------------
+constexpr int kScanItems = 16;                     // u32 per lane
+constexpr int kScanTile = kBlock * kScanItems;     // 4096 per workgroup
+
+// 1: per-tile sums
+__global__ void __launch_bounds__(kBlock) k_scan_tiles(const u32* __restrict__ in,
+                                                       const int64_t* __restrict__ n_dev,
+                                                       int64_t n_host, u32* __restrict__ tiles) {
+  const int64_t n = n_dev ? *n_dev : n_host;
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
+  if (t0 >= n) return;
+  u32 v = 0;
+#pragma unroll
+  for (int q = 0; q < kScanItems; ++q) {
+    const int64_t i = t0 + (int64_t)threadIdx.x * kScanItems + q;
+    if (i < n) v += in[i];
+  }
+  u32 tot;
+  (void)block_exclusive_scan<kBlock>(v, &tot);
+  if (threadIdx.x == 0) tiles[blockIdx.x] = tot;
+}
+
+// 2: exclusive scan of the tile sums (one workgroup), total into tiles[nt]
+__global__ void __launch_bounds__(kScanBlock) k_scan_top(u32* __restrict__ tiles,
+                                                         const int64_t* __restrict__ n_dev,
+                                                         int64_t n_host) {
+  const int64_t n = n_dev ? *n_dev : n_host;
+  const int nt = (int)((n + kScanTile - 1) / kScanTile);
+  u32 carry = 0;
+  for (int c0 = 0; c0 < nt; c0 += kScanBlock) {
+    const int i = c0 + (int)threadIdx.x;
+    const u32 v = i < nt ? tiles[i] : 0u;
+    u32 t;
+    const u32 ex = block_exclusive_scan<kScanBlock>(v, &t);
+    if (i < nt) tiles[i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) tiles[nt] = carry;
+}
+
+// 3: out[i] = exclusive prefix, out[n] = total
+__global__ void __launch_bounds__(kBlock) k_scan_write(const u32* __restrict__ in,
+                                                       const int64_t* __restrict__ n_dev,
+                                                       int64_t n_host, const u32* __restrict__ tiles,
+                                                       u32* __restrict__ out) {
+  const int64_t n = n_dev ? *n_dev : n_host;
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTile;
+  if (t0 > n) return;
+  const int nt = (int)((n + kScanTile - 1) / kScanTile);
+  if (t0 == n) {  // (n a multiple of the tile: the total has no tile of its own)
+    if (threadIdx.x == 0) out[n] = tiles[nt];
+    return;
+  }
+  u32 loc[kScanItems], v = 0;
+#pragma unroll
+  for (int q = 0; q < kScanItems; ++q) {
+    const int64_t i = t0 + (int64_t)threadIdx.x * kScanItems + q;
+    loc[q] = i < n ? in[i] : 0u;
+    v += loc[q];
+  }
+  u32 tot;
+  u32 ex = tiles[blockIdx.x] + block_exclusive_scan<kBlock>(v, &tot);
+#pragma unroll
+  for (int q = 0; q < kScanItems; ++q) {
+    const int64_t i = t0 + (int64_t)threadIdx.x * kScanItems + q;
+    if (i < n) out[i] = ex;
+    ex += loc[q];
+  }
+  if (blockIdx.x == (unsigned)(nt - 1) && threadIdx.x == kBlock - 1) out[n] = ex;
+}
+
+void launch_scan_u32(const u32* in, u32* out, const int64_t* n_dev, int64_t n_max, u32* tiles,
+                     hipStream_t st) {
+  const int g = (int)((n_max + kScanTile - 1) / kScanTile) + 1;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(g), dim3(kBlock), 0, st, in, n_dev, n_max, tiles);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, st, tiles, n_dev, n_max);
+  hipLaunchKernelGGL(k_scan_write, dim3(g), dim3(kBlock), 0, st, in, n_dev, n_max, tiles, out);
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// entries of key i from the producer layout (off, cnt) to doff[i] (dense)
+template <typename E>
+__global__ void __launch_bounds__(kBlock) k_csr_pack(const u32* __restrict__ off,
+                                                     const u32* __restrict__ cnt,
+                                                     const E* __restrict__ src,
+                                                     const u32* __restrict__ doff,
+                                                     const int64_t* __restrict__ n_dev,
+                                                     int64_t n_host, E* __restrict__ dst) {
+  const int64_t n = n_dev ? *n_dev : n_host;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u32 c = cnt[i], o = off[i], d = doff[i];
+    for (u32 j = 0; j < c; ++j) dst[d + j] = src[o + j];
+  }
+}
+
+// per-owner entry totals: owner r's keys are the send-order range of the
+// (decoded) key counts before it
+__global__ void k_csr_totals(const int64_t* __restrict__ counts, int world, int encoded,
+                             const u32* __restrict__ doff, int64_t* __restrict__ totals) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t o = 0;
+  for (int r = 0; r < world; ++r) {
+    int64_t c = counts[r];
+    if (encoded) c = (c & ((1ll << kCountBits) - 1)) - 1;
+    c = c > 0 ? c : 0;
+    totals[r] = (int64_t)doff[o + c] - (int64_t)doff[o];
+    o += c;
+  }
+}
+
+void launch_csr_pack(const u32* off, const u32* cnt, const void* src, const u32* doff,
+                     const int64_t* n_dev, int64_t n_max, void* dst, int entry_bytes,
+                     hipStream_t st) {
+  const int g = grid_for(n_max);
+  if (entry_bytes == 8)
+    hipLaunchKernelGGL(k_csr_pack<u64>, dim3(g), dim3(kBlock), 0, st, off, cnt,
+                       static_cast<const u64*>(src), doff, n_dev, n_max, static_cast<u64*>(dst));
+  else if (entry_bytes == 12)
+    hipLaunchKernelGGL(k_csr_pack<uint3>, dim3(g), dim3(kBlock), 0, st, off, cnt,
+                       static_cast<const uint3*>(src), doff, n_dev, n_max, static_cast<uint3*>(dst));
+  else throw std::runtime_error("csr_pack: entries of 8 or 12 bytes");
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+void launch_csr_totals(const int64_t* counts, int world, bool encoded, const u32* doff,
+                       int64_t* totals, hipStream_t st) {
+  hipLaunchKernelGGL(k_csr_totals, dim3(1), dim3(kWave), 0, st, counts, world, encoded ? 1 : 0,
+                     doff, totals);
   XF_HIP_CHECK(hipGetLastError());
 }
 

@@ -138,6 +138,22 @@ struct DedupOut {
   unsigned long long* cap_out = nullptr;  // optional: the capacity this batch was deduplicated with
 };
 
+// Sparse per-(key, slice) gradient sums in CSR form -- the step's pushes as
+// the reference makes them: each Hogwild slice pushes only the keys it
+// touched (lr_worker.cc:162-175), so only touched (key, slice) pairs exist.
+// Key i (unique / send order) owns entries ent[off[i] .. off[i] + cnt[i]),
+// in slice order.  An entry is (slice, value): LR u64 slice | value << 32,
+// reference FM u32x3 (slice, B, C).  Dests of the producers are
+// key * 2^slog2 + slice (the slice count padded to a power of two), so a
+// key's dests never straddle a reduction bucket.
+struct CsrOut {
+  u32* off = nullptr;            // [unique] first entry of the key
+  u32* cnt = nullptr;            // [unique] entries of the key (>= 1 for every key of the batch)
+  void* ent = nullptr;           // entries (FwdArgs: the producers' record regions, free by then)
+  int slog2 = 0;
+  const int32_t* rows = nullptr;  // values divided by rows[slice] (null: raw sums)
+};
+
 struct FwdArgs {
   BatchView batch;
   const u32* pos = nullptr;        // [nnz]
@@ -223,6 +239,9 @@ struct FwdArgs {
   // loss*M_k/(1+v_ik), so records are (dest | row << 32), red_rowv[row] holds
   // T = loss*M ([rows][pstride]) and the sum divides Σ T by (1 + v) per key.
   float* red_rowv = nullptr;
+  // CSR outputs (red_csr.cnt != null; LR / reference FM with unique-index
+  // positions, S = 2^slog2): one reduction over every slice of the step
+  CsrOut red_csr;
   // set to 2 (OR) when a row's prediction is non-finite or out of [0, 1], or
   // a fixed-point input is out of range (a diverged model): the values are
   // clamped before the fixed-point conversion and the capacity monitor
@@ -408,6 +427,11 @@ struct ApplyArgs {
   // Optional fused reset of the worker dedup scratch (single-device path).
   ScratchView scratch;
   const u32* reset_pos = nullptr;
+  // CSR gradients (csr_cnt != null, CsrOut): entry i's pushes are its CSR
+  // entries in order (the entries carry their slices; grads / masks unused)
+  const u32* csr_off = nullptr;
+  const u32* csr_cnt = nullptr;
+  const void* csr_ent = nullptr;
   // Several sources in one launch (grp.oidx != null): n counts all received
   // entries; an entry's gradient row / mask / pulled values / stash are
   // indexed by the entry, and each key is applied by its first source's entry.
@@ -571,6 +595,26 @@ class Backend {
   virtual void owner_group(const OwnerGroupArgs& a) {
     (void)a;
     throw std::runtime_error("owner grouping is not supported by this backend");
+  }
+  // CSR exchange of the multi-rank step (HIP only): out[i] = sum of in[< i],
+  // out[n] = total, n = *n_dev (or n_max); dense packing of key i's entries
+  // (entry_bytes each) from src[off[i]..] to dst[doff[i]..]; per-owner entry
+  // totals from the step's (encoded) key counts per owner and the dense offsets
+  virtual bool csr_exchange() const { return false; }
+  virtual void scan_u32(const u32* in, u32* out, const int64_t* n_dev, int64_t n_max) {
+    (void)in, (void)out, (void)n_dev, (void)n_max;
+    throw std::runtime_error("scan_u32 is not supported by this backend");
+  }
+  virtual void csr_pack(const u32* off, const u32* cnt, const void* src, const u32* doff,
+                        const int64_t* n_dev, int64_t n_max, void* dst, int entry_bytes) {
+    (void)off, (void)cnt, (void)src, (void)doff, (void)n_dev, (void)n_max, (void)dst,
+        (void)entry_bytes;
+    throw std::runtime_error("csr_pack is not supported by this backend");
+  }
+  virtual void csr_totals(const int64_t* counts, int world, bool encoded, const u32* doff,
+                          int64_t* totals) {
+    (void)counts, (void)world, (void)encoded, (void)doff, (void)totals;
+    throw std::runtime_error("csr_totals is not supported by this backend");
   }
   virtual void gather_grads(const GatherGradArgs& a) = 0;
   // rows of `width` floats: dst[map? map[i] : i] = src[i]   (scatter)

@@ -126,6 +126,24 @@ class Engine {
   void w_forward_backward(const BatchView& b, const float* pulled, int64_t n_send,
                           float* grads_out, u32* masks_out, int S_global = 0, int wb = 0,
                           int group = 0);
+  // ---- the CSR exchange (several slices, GPU: LR-FTRL / reference FM) ----
+  // log2 of the padded slice count when a step of S slices runs its gradients
+  // as CSR entries (-1: the dense slice-group layout)
+  int csr_slog2(int S) const;
+  int csr_entry_bytes() const { return fm_vals_ ? 12 : 8; }
+  // worker: forward/backward of every slice of the step at once.  pack:
+  // entries packed densely in send order into ent_out (cnt_out: entries per
+  // key, u32 [n_send]; totals_out: entries per owner, from the step's owner
+  // key counts `counts` (encoded: world > 1)); else they stay in the engine's
+  // CSR layout (world 1, read in place by s_apply_csr with null arrays).
+  void w_forward_backward_csr(const BatchView& b, const float* pulled, int64_t n_send,
+                              int S_global, int wb, bool pack, u32* cnt_out, void* ent_out,
+                              const int64_t* counts, int world, bool encoded, int64_t* totals_out);
+  // server: apply received CSR gradients source by source: recv_cnt [n] per
+  // key, entries of all sources back to back (null recv_cnt: the worker's own
+  // entries of this step, world 1)
+  void s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* recv_ent,
+                   const std::vector<int64_t>& src_offsets, int S, int buf = 0);
   // server: apply received gradients source by source (deterministic order).
   // src_offsets has world+1 entries delimiting each source's rows.
   void s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
@@ -152,6 +170,11 @@ class Engine {
   // and segments split so far, host waits the monitor needed, and an explicit
   // growth to at least 2^log2_cap slots
   int64_t table_growths() const { return growths_; }
+  // steps (fused or worker-side) whose several slices ran on the CSR path
+  int64_t csr_steps() const { return csr_steps_; }
+  // host copies of the last CSR step's per-key (off, cnt) and its entry words
+  // (tests / debugging; syncs)
+  void csr_debug(std::vector<u32>& off, std::vector<u32>& cnt, std::vector<u32>& words);
   int64_t table_splits() const { return splits_; }
   // geometry: {segment slots log2, level, split, segments}
   std::vector<int64_t> table_geometry() const {
@@ -335,6 +358,19 @@ class Engine {
   u32* inv_ = nullptr;          // [scratch cap] slot -> send index (partitioned dedup, LR)
   bool inv_valid_ = false;      // inv_ describes the batch of the last w_prepare
   void set_reduction(FwdArgs& fa) const;
+  // CSR gradients (CsrOut): the single-rank step of several slices, LR-FTRL on
+  // 16-byte slots or compact reference-FM rows -- one producer pass, one
+  // reduction and one apply for any slice count
+  u32* csr_off_ = nullptr;      // [max_nnz]
+  u32* csr_cnt_ = nullptr;      // [max_nnz]
+  int64_t csr_steps_ = 0;
+  void train_step_csr(const BatchView& b, int S, int slog2);
+  u32* csr_doff_ = nullptr;     // [max_nnz + 1] dense offsets (worker pack)
+  u32* csr_roff_ = nullptr;     // received entries' offsets (server)
+  int64_t csr_roff_cap_ = 0;
+  // the forward/backward both CSR entry points run: producer pass over every
+  // slice with dests unique * 2^slog2 + slice, CSR reduction into csr_*_
+  void csr_forward_backward(const BatchView& b, int slog2, const int32_t* srows, bool normalise);
   bool reduction_masks(bool unique_positions) const;
   void ensure_inv();
   LossStats* stats_ = nullptr;  // [1]

@@ -262,6 +262,9 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_readwrite("host_waits", &ShardedStep::host_waits)
       .def_readwrite("mid_step_waits", &ShardedStep::mid_step_waits)
       .def_readwrite("buffer_growths", &ShardedStep::buffer_growths)
+      .def_readwrite("csr_exchanges", &ShardedStep::csr_exchanges)
+      .def_readwrite("csr_waits", &ShardedStep::csr_waits)
+      .def_readwrite("csr_wait_s", &ShardedStep::csr_wait_s)
       .def_readwrite("early_key_exchanges", &ShardedStep::early_key_exchanges)
       .def_readwrite("inline_prepares", &ShardedStep::inline_prepares)
       .def_readwrite("empty_steps", &ShardedStep::empty_steps)
@@ -301,6 +304,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("table_grow") = true, py::arg("grow_load") = 0.8, py::arg("max_log2_cap") = 0,
            py::arg("monitor_lag") = 2, py::arg("owner_group") = 0, py::arg("grow_start") = 0.6)
       .def_property_readonly("table_growths", &Engine::table_growths)
+      .def_property_readonly("csr_steps", &Engine::csr_steps)
       .def_property_readonly("table_splits", &Engine::table_splits)
       .def_property_readonly("table_geometry", &Engine::table_geometry)
       .def_property_readonly("table_committed", &Engine::table_committed)
@@ -435,6 +439,12 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def("read_stats",
            [](Engine& e, bool reset, int which) { return stats_dict(e.read_stats(reset, which)); },
            py::arg("reset") = false, py::arg("which") = 0)
+      .def("csr_debug",
+           [](Engine& e) {
+             std::vector<u32> o, c, w;
+             e.csr_debug(o, c, w);
+             return py::make_tuple(to_np(o), to_np(c), to_np(w));
+           })
       .def("n_unique", &Engine::n_unique)
       .def("table_size", &Engine::table_size)
       .def("scratch_capacity", &Engine::scratch_capacity)

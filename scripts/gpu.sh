@@ -41,8 +41,10 @@ for x in list(csv.DictReader(open(sys.argv[1])))[:14]:
 PY
 }
 
-run_tests() {
-  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread "$@" \
+run_tests() {  # [pytest args]: default the whole GPU suite (-x); with args, just those
+  local sel=(tests -x)
+  [ $# -gt 0 ] && sel=()
+  timeout -k 10 900 python -u -m pytest "${sel[@]}" -q -m gpu --timeout 170 --timeout-method thread "$@" \
       > "$O/pytest_gpu.log" 2>&1 || { echo "pytest gpu failed"; tail -60 "$O/pytest_gpu.log"; exit 1; }
   tail -1 "$O/pytest_gpu.log"
 }

@@ -228,3 +228,59 @@ def test_rccl_processes_bench_scale_equals_single_engine(gpu_device, tmp_path, k
         assert (owner_of(np.load(tmp_path / f"bk{r}.npy"), BS_W) == r).all()
     assert len(np.unique(k)) == len(k) == ref.table_size()
     np.testing.assert_allclose(v, ref.pull(k), rtol=1e-4, atol=1e-6)
+
+
+# ---- several Hogwild slices per rank over RCCL: the CSR exchange (only the
+# touched (key, slice) entries move; reference: each slice pushes its own
+# keys, lr_worker.cc:162-175)
+CSR_W, CSR_S, CSR_STEPS = 2, 64, 3
+
+
+def _csr_worker(rank, world, kind, out_dir):
+    from xflow_amd.parallel.sparse_a2a import ShardedEngine
+
+    dev = torch.device("cuda", 0)
+    eng = _bs_engine(dev, BS_ROWS, 22, slices=CSR_S, kind=kind)
+    sh = ShardedEngine(eng)
+    assert sh.transport == "rccl", sh.transport
+    bs = _bs_batches(rank, dev)[:CSR_STEPS]
+    for b in bs:
+        b.slice_rows = BS_ROWS // CSR_S
+    for s in range(CSR_STEPS):
+        assert sh.train_step(bs[s], S=CSR_S, next_batch=bs[s + 1] if s + 1 < CSR_STEPS else None)
+    torch.cuda.synchronize(dev)
+    assert not eng.overflowed()
+    assert sh.csr_exchanges == CSR_STEPS, sh.csr_exchanges
+    keys, _ = eng.export_table()
+    np.save(os.path.join(out_dir, f"ck{rank}.npy"), keys)
+    np.save(os.path.join(out_dir, f"cv{rank}.npy"), eng.pull(keys))
+    np.save(os.path.join(out_dir, f"cb{rank}.npy"), np.array([sh.bytes_moved]))
+
+
+@pytest.mark.parametrize("kind", ["lr", "fm"])
+def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kind):
+    """2 processes x 32 768 Criteo-shaped rows x 64 slices each, 3 pipelined
+    steps over RCCL with the CSR gradient exchange == one engine trained on
+    both ranks' rows as 128 ordered slices per step (source 0's slices, then
+    source 1's); the bytes moved are the touched pairs', far below the dense
+    [keys][64 x width] blocks."""
+    from xflow_amd.engine import Batch
+
+    run_world_gpu(_csr_worker, CSR_W, kind, str(tmp_path))
+    data = [_bs_batches(r, gpu_device)[:CSR_STEPS] for r in range(CSR_W)]
+    ref = _bs_engine(gpu_device, CSR_W * BS_ROWS, 24, slices=CSR_W * CSR_S, kind=kind)
+    for s in range(CSR_STEPS):
+        keys = torch.cat([data[r][s].keys.view(39, BS_ROWS) for r in range(CSR_W)],
+                         dim=1).reshape(-1)
+        lab = torch.cat([data[r][s].labels for r in range(CSR_W)])
+        ref.train_step(Batch(keys=keys.contiguous(), labels=lab, nnz_per_row=39,
+                             field_major=True, slice_rows=BS_ROWS // CSR_S))
+    assert ref.csr_steps == CSR_STEPS
+    k = np.concatenate([np.load(tmp_path / f"ck{r}.npy") for r in range(CSR_W)])
+    v = np.concatenate([np.load(tmp_path / f"cv{r}.npy") for r in range(CSR_W)])
+    assert len(np.unique(k)) == len(k) == ref.table_size()
+    np.testing.assert_allclose(v, ref.pull(k), rtol=1e-4, atol=1e-6)
+    # dense per-slice blocks would move >= n_keys x 64 x 4 bytes per step
+    dense = CSR_STEPS * len(k) * CSR_S * 4 / CSR_W
+    for r in range(CSR_W):
+        assert np.load(tmp_path / f"cb{r}.npy")[0] < dense / 4

@@ -330,6 +330,12 @@ class Engine:
         return int(self._e.table_growths)
 
     @property
+    def csr_steps(self) -> int:
+        """Steps of several slices that ran on the CSR path (one reduction and
+        one apply of only the touched (key, slice) pairs, Engine::train_step_csr)."""
+        return int(self._e.csr_steps)
+
+    @property
     def table_splits(self) -> int:
         """Segments split so far (each added one segment of memory)."""
         return int(self._e.table_splits)

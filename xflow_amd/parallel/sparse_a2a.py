@@ -119,6 +119,11 @@ class ShardedEngine:
     drop_exchanges = _native_counter("drop_exchanges")
     last_send = _native_counter("last_send")
     last_recv = _native_counter("last_recv")
+    # several slices as CSR entries (native GPU step): steps, and host waits
+    # for the per-owner entry totals (the entries' all-to-all sizes)
+    csr_exchanges = _native_counter("csr_exchanges")
+    csr_waits = _native_counter("csr_waits")
+    csr_wait_s = _native_counter("csr_wait_s")
 
     def __init__(self, engine: Engine, group: Optional[dist.ProcessGroup] = None,
                  world: Optional[int] = None, rank: Optional[int] = None,
