@@ -222,6 +222,7 @@ Engine::~Engine() {
   use_worker_set(cur_wb_);  // (records the current set)
   be.table_release(table_.words);
   be.free_stream(csr_roff_);
+  be.free_stream(csr_long_);
   void* ptrs[] = {mon_, scratch_.keys, scratch_.stamps,
                   scratch_.claims, block_counts_, uniq_keys_, uniq_slot_, wpull_, grad_, tmask_,
                   stats_, bucket_ws_, slice_rows_, st_keys_, st_fgid_, st_rowptr_, st_labels_,
@@ -550,6 +551,7 @@ void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   aa.csr_off = csr_off_;
   aa.csr_cnt = csr_cnt_;
   aa.csr_ent = red_pairs_;
+  aa.csr_long = csr_long_list(b.nnz);
   attach_snapshot(aa);
   be_->table_apply(aa);
   end_step();
@@ -582,6 +584,16 @@ void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* 
   fa.red_csr.rows = normalise ? srows : nullptr;
   be_->forward_backward(fa);
   ++csr_steps_;
+}
+
+u32* Engine::csr_long_list(int64_t n) {
+  if (!be_->is_gpu()) return nullptr;
+  if (n + 1 > csr_long_cap_) {
+    be_->free_stream(csr_long_);
+    csr_long_cap_ = n + n / 4 + 1024;
+    csr_long_ = static_cast<u32*>(be_->alloc_stream(sizeof(u32) * (size_t)csr_long_cap_));
+  }
+  return csr_long_;
 }
 
 void Engine::w_forward_backward_csr(const BatchView& b, const float* pulled, int64_t n_send,
@@ -663,6 +675,7 @@ void Engine::s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* 
     aa.csr_off = off + o;
     aa.csr_cnt = cnt + o;
     aa.csr_ent = ent;
+    aa.csr_long = csr_long_list(c);
     if (stash) aa.nz_stash = sb.nz ? sb.nz + 2 * o : nullptr;
     stash = false;
     attach_snapshot(aa);

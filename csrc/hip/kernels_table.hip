@@ -1069,25 +1069,41 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
 // touched (lr_worker.cc:162-175) -- applied as a chain on (n, z) held in
 // registers (sqrt(n) carried), the slot written once.  The first entries of
 // the next keys are loaded before this key's chain.
+constexpr int kCsrChunk = 8;  // CSR entries a lane loads at once
+// Chains longer than this run in a second launch over the list of such keys
+// (ApplyArgs::csr_long: [0] = count, then the entries' indices)
+constexpr u32 kCsrShortChain = 16;
+
+// list of the deferred long-chain keys: one atomic per wave
+__device__ __forceinline__ void csr_defer(u32* list, bool pred, u32 i) {
+  const u32 slot = wave_append<u32>(list, pred);
+  if (pred) list[1 + slot] = i;
+}
+
+// kLong: the second launch (entries of the deferred list), else the first
+template <bool kLong>
 __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
-  XF_APPLY_SNAPSHOT(a);
-  const int64_t n = dev_count(a.n_dev, a.n_host, a.n_max);
+  if (!kLong) XF_APPLY_SNAPSHOT(a);
+  const int64_t n = kLong ? (int64_t)a.csr_long[0] : dev_count(a.n_dev, a.n_host, a.n_max);
+  const u32* __restrict__ lst = a.csr_long + 1;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const FtrlParams fp = a.opt.ftrl;
   const u64* __restrict__ ent = static_cast<const u64*>(a.csr_ent);
   struct In {
-    u32 slot, off, cnt;
+    u32 key, slot, off, cnt;
     u64 e0;
     float2 nz;
   };
-  auto load = [&](int64_t i) {
+  auto load = [&](int64_t j) {
     In x;
+    const int64_t i = kLong ? (int64_t)lst[j] : j;
+    x.key = (u32)i;
     x.slot = a.slots[i];
     x.off = a.csr_off[i];
     x.cnt = a.csr_cnt[i];
     x.e0 = x.cnt ? ent[x.off] : 0ull;
     x.nz = make_float2(0.0f, 0.0f);
-    if (x.slot != kNoSlot && x.cnt)
+    if (x.slot != kNoSlot && x.cnt && (kLong || !a.csr_long || x.cnt <= kCsrShortChain))
       x.nz = a.nz_stash ? reinterpret_cast<const float2*>(a.nz_stash)[i]
                         : *reinterpret_cast<const float2*>(a.table.words + (u64)x.slot * 4 + 2);
     return x;
@@ -1098,15 +1114,28 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
   for (; i < n; i += stride) {
     const In x = nx;
     if (i + stride < n) nx = load(i + stride);
+    if (!kLong && a.csr_long) {
+      const bool defer = x.slot != kNoSlot && x.cnt > kCsrShortChain;
+      csr_defer(a.csr_long, defer, x.key);
+      if (defer) continue;
+    }
     if (x.slot == kNoSlot || !x.cnt) continue;
     float2 nz = x.nz;
     float sn = sqrtf(nz.x);
-    u64 e = x.e0;
-    for (u32 j = 0;;) {
+    auto push = [&](u64 e) {
       const float w = ftrl_weight_sn(nz.y, sn, fp);
       ftrl_push_sn(nz.x, nz.y, sn, w, __uint_as_float((u32)(e >> 32)), fp);
-      if (++j == x.cnt) break;
-      e = ent[x.off + j];
+    };
+    push(x.e0);
+    // a hot key's chain (up to one entry per slice): its entries are loaded
+    // kCsrChunk at a time, all in flight together, not one round trip each
+    for (u32 j = 1; j < x.cnt; j += kCsrChunk) {
+      u64 e[kCsrChunk];
+#pragma unroll
+      for (int q = 0; q < kCsrChunk; ++q) e[q] = j + q < x.cnt ? ent[x.off + j + q] : 0ull;
+#pragma unroll
+      for (int q = 0; q < kCsrChunk; ++q)
+        if (j + q < x.cnt) push(e[q]);
     }
     *reinterpret_cast<float2*>(a.table.words + (u64)x.slot * 4 + 2) = nz;
   }
@@ -1341,6 +1370,7 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
       // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
       const float w_pre = a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : w_next) : 0.0f;
       u32 any = 0;
+      bool deferred = false;  // (CSR: a long chain, applied by the second launch)
       if (gpipe) {
         any = 1u;
         const float raw = !a.fm_compact ? gv.x
@@ -1361,8 +1391,14 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
           // order; the raw sums are normalised here (slice_rows) or by the
           // producing worker (null)
           const u32 c0 = a.csr_off[row], cn = a.csr_cnt[row];
+          if (a.csr_long && cn > kCsrShortChain) {  // (uniform over the key's lanes)
+            csr_defer(a.csr_long, p == 0, (u32)i);
+            deferred = true;
+            break;
+          }
           const uint3* ce = static_cast<const uint3*>(a.csr_ent) + c0;
           any |= cn;
+          // (short chains here: the long ones run in k_apply_group_csr_long)
           for (u32 j = 0; j < cn; ++j) {
             const uint3 x = ce[j];
             const float Bv = __uint_as_float(x.y), Cv = __uint_as_float(x.z);
@@ -1390,9 +1426,11 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
             if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
         }
       }
-      if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
-      else sp[2 + p] = __float_as_uint(n0);
-      if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
+      if (!deferred) {
+        if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
+        else sp[2 + p] = __float_as_uint(n0);
+        if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
+      }
     }
     if (!multi && a.zero_after) {
       const u32 row = gpipe ? grow_i : (a.grad_map ? a.grad_map[i] : (u32)i);
@@ -1402,6 +1440,53 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
         for (int c = p; c < w; c += L.P) g[s * gs + c] = 0.0f;
       if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }
+  }
+}
+
+// The deferred long chains of the packed CSR apply (ApplyArgs::csr_long):
+// one key group (P lanes) per listed entry, its row read from the table (or
+// the pull's stash), every entry pushed in order, the row written once.
+__global__ void __launch_bounds__(kBlock) k_apply_group_csr_long(ApplyArgs a) {
+  const int64_t n = (int64_t)a.csr_long[0];
+  const TableLayout& L = a.table.L;
+  const int ps = a.pstride;
+  const PackedLane pl = packed_lane(L.P);
+  const int p = pl.p;
+  const bool ftrl = L.opt == kFTRL;
+  if (!pl.on) return;
+  for (int64_t j = pl.first; j < n; j += pl.stride) {
+    const int64_t i = a.csr_long[1 + j];
+    const u32 slot = a.slots[i];
+    u32* sp = a.table.words + (u64)slot * L.stride;
+    const RowPre rp = a.nz_stash && ftrl
+                          ? row_stash(reinterpret_cast<const float2*>(a.nz_stash), a.keys, i, p, L.P)
+                          : row_pre(a.table.words, slot, p, L);
+    float n0 = rp.s0, z0 = rp.s1;
+    const float w0 = state_weight(rp.key, rp.flag != 0u, n0, z0, p, L, a.opt);
+    const float w_pre = a.pulled ? a.pulled[(size_t)i * ps + p] : w0;
+    float w_next = w0, sn = ftrl ? sqrtf(n0) : 0.0f;
+    bool stale = false;
+    const u32 c0 = a.csr_off[i], cn = a.csr_cnt[i];
+    const uint3* ce = static_cast<const uint3*>(a.csr_ent) + c0;
+    for (u32 jj = 0; jj < cn; jj += kCsrChunk) {
+      uint3 x[kCsrChunk];
+#pragma unroll
+      for (int q = 0; q < kCsrChunk; ++q) x[q] = jj + q < cn ? ce[jj + q] : make_uint3(0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < kCsrChunk; ++q) {
+        if (jj + q >= cn) break;
+        const float Bv = __uint_as_float(x[q].y), Cv = __uint_as_float(x[q].z);
+        const float g = norm_grad(p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv, a.slice_rows,
+                                  (int)x[q].x);
+        if (stale) w_next = ftrl ? ftrl_weight_sn(z0, sn, a.opt.ftrl) : n0;
+        if (ftrl) ftrl_push_sn(n0, z0, sn, w_next, g, a.opt.ftrl);
+        else n0 = w_next - a.opt.sgd.lr * g;
+        stale = true;
+      }
+    }
+    if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
+    else sp[2 + p] = __float_as_uint(n0);
+    if (L.has_flag && p == 0) sp[L.flag_word] = 1u;
   }
 }
 
@@ -1422,10 +1507,17 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (a.csr_cnt) {
     if (a.zero_after || a.reset_pos || a.sum_slices || a.grp.oidx || a.grad_map)
       throw std::runtime_error("CSR apply: bad arguments");
-    if (lr16_slot) hipLaunchKernelGGL(k_apply_lr16_csr, dim3(grid), dim3(kBlock), 0, st, a);
-    else if (a.fm_compact && L.P <= kWave)
+    if (a.csr_long) XF_HIP_CHECK(hipMemsetAsync(a.csr_long, 0, sizeof(u32), st));
+    if (lr16_slot) {
+      hipLaunchKernelGGL(k_apply_lr16_csr<false>, dim3(grid), dim3(kBlock), 0, st, a);
+      if (a.csr_long) hipLaunchKernelGGL(k_apply_lr16_csr<true>, dim3(grid), dim3(kBlock), 0, st, a);
+    } else if (a.fm_compact && L.P <= kWave) {
       hipLaunchKernelGGL(k_apply_group<true>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
-    else throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots or compact reference-FM rows");
+      if (a.csr_long)
+        hipLaunchKernelGGL(k_apply_group_csr_long, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+    } else {
+      throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots or compact reference-FM rows");
+    }
   } else if (a.grp.oidx) {
     if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");
     if (lr16) hipLaunchKernelGGL(k_apply_lr16_multi, dim3(grid), dim3(kBlock), 0, st, a);

@@ -432,6 +432,11 @@ struct ApplyArgs {
   const u32* csr_off = nullptr;
   const u32* csr_cnt = nullptr;
   const void* csr_ent = nullptr;
+  // (HIP) keys with more than kCsrShortChain entries are deferred to a second
+  // launch over the list of them (u32 [n] + a u32 counter): a wave then holds
+  // chains of similar length instead of one hot key's slice-long chain and 63
+  // idle lanes
+  u32* csr_long = nullptr;
   // Several sources in one launch (grp.oidx != null): n counts all received
   // entries; an entry's gradient row / mask / pulled values / stash are
   // indexed by the entry, and each key is applied by its first source's entry.

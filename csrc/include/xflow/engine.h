@@ -366,6 +366,9 @@ class Engine {
   int64_t csr_steps_ = 0;
   void train_step_csr(const BatchView& b, int S, int slog2);
   u32* csr_doff_ = nullptr;     // [max_nnz + 1] dense offsets (worker pack)
+  u32* csr_long_ = nullptr;     // [1 + max keys] the applies' deferred long chains
+  int64_t csr_long_cap_ = 0;
+  u32* csr_long_list(int64_t n);
   u32* csr_roff_ = nullptr;     // received entries' offsets (server)
   int64_t csr_roff_cap_ = 0;
   // the forward/backward both CSR entry points run: producer pass over every
