@@ -551,7 +551,9 @@ void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   aa.csr_off = csr_off_;
   aa.csr_cnt = csr_cnt_;
   aa.csr_ent = red_pairs_;
-  aa.csr_long = csr_long_list(b.nnz);
+  // (a chain has at most S entries: with S <= 16 nothing is ever deferred)
+  aa.csr_long = S > 16 ? csr_long_list(b.nnz) : nullptr;
+  aa.csr_long_cap = csr_long_cap_;
   attach_snapshot(aa);
   be_->table_apply(aa);
   end_step();
@@ -588,9 +590,13 @@ void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* 
 
 u32* Engine::csr_long_list(int64_t n) {
   if (!be_->is_gpu()) return nullptr;
-  if (n + 1 > csr_long_cap_) {
+  // (wave-private lists: n plus a grid-stride iteration of every wave's keys,
+  // <= 8192 x 4 waves x 64, and the per-wave counts)
+  // (+ the dense list of n, the offsets and the scan tiles)
+  const int64_t need = 2 * n + (int64_t)(2u << 20) + 4 * 65536;
+  if (need > csr_long_cap_) {
     be_->free_stream(csr_long_);
-    csr_long_cap_ = n + n / 4 + 1024;
+    csr_long_cap_ = need + n / 4;
     csr_long_ = static_cast<u32*>(be_->alloc_stream(sizeof(u32) * (size_t)csr_long_cap_));
   }
   return csr_long_;
@@ -675,7 +681,8 @@ void Engine::s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* 
     aa.csr_off = off + o;
     aa.csr_cnt = cnt + o;
     aa.csr_ent = ent;
-    aa.csr_long = csr_long_list(c);
+    aa.csr_long = S > 16 ? csr_long_list(c) : nullptr;
+    aa.csr_long_cap = csr_long_cap_;
     if (stash) aa.nz_stash = sb.nz ? sb.nz + 2 * o : nullptr;
     stash = false;
     attach_snapshot(aa);

@@ -1383,16 +1383,16 @@ template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kScaled
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int NV = 1 + D;
-  constexpr int LOG2 = ilog2c(2 * BLOCK);
-  constexpr int kSlots = 1 << LOG2;
+  static_assert(BLOCK == fmstd_block(D), "producer block");
+  constexpr u32 kSlots = (u32)fmstd_slots(D);  // (not a power of two: 1.5 x BLOCK at D = 8)
   constexpr int kFx = FxBits<1>::kFx;
   __shared__ u64 s_tag[1][kSlots];
   __shared__ long long s_acc[1][kSlots * NV];
   const int fxs = kScaled ? fx_scale_bits(a.red_vmax, fx_head_bits(a.batch.rows)) : kFx;
   __shared__ unsigned short s_list[1][BLOCK];
   constexpr int kMaxB = vec_red_max_buckets(D);
+  // per-bucket counts, then (kSeg) each bucket's record cursor in the region
   __shared__ u32 s_hist[kMaxB];
-  __shared__ u32 s_off[kSeg ? kMaxB : 1];
   __shared__ u32 s_nlist[3];
   __shared__ int s_wmax[BLOCK / kWave];
   const BatchView& b = a.batch;
@@ -1453,7 +1453,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     live = nz || S > 1u;
   }
   if constexpr (kSeg) {
-    // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (s_off)
+    // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (the cursors)
     for (int j = 0; j < len && live; ++j) {
       const u32 pj = pos[rs.at(j)];
       if (pj != a.trash_pos) atomicAdd(&s_hist[(pj * S + sl) >> shift], 1u);
@@ -1475,9 +1475,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     for (int q = 0; q < kPer; ++q) {
       const int i = (int)threadIdx.x * kPer + q;
       if (i < nb) {
-        s_off[i] = ex;
         sub_out[(size_t)i * gridDim.x + blockIdx.x] = ex;
-        s_hist[i] = 0u;  // now the record cursor
+        s_hist[i] = ex;  // now the record cursor
       }
       ex += c[q];
     }
@@ -1536,8 +1535,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     if (has) {
       const u32 dest = pj * S + sl;
       const u64 key = ((u64)(u32)j << 32) | dest;
-      h = (dest * 0x9E3779B1u) >> (32 - LOG2);
-      while (true) {  // <= BLOCK keys per column in 2 * BLOCK slots: terminates
+      h = (u32)(((u64)(dest * 0x9E3779B1u) * kSlots) >> 32);
+      while (true) {  // <= BLOCK keys per column in > BLOCK slots: terminates
         const u64 cur = s_tag[t][h];
         if (cur == key) break;
         if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
@@ -1549,7 +1548,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
           }
           if (old == key) break;
         }
-        h = (h + 1) & (kSlots - 1);
+        h = h + 1 == kSlots ? 0u : h + 1;
       }
       // factorised: Σ loss*(vs_k - v_k) = C_k - v_k*B with B = Σ loss and
       // C_k = Σ loss*vs_k (v_k is the key's pulled value, one per step), so the
@@ -1600,8 +1599,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       for (int q = 0; q < W / 4; ++q)
         rec.q[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
       if constexpr (kSeg) {
-        const u32 bk = d >> shift;
-        region[s_off[bk] + atomicAdd(&s_hist[bk], 1u)] = rec;
+        region[atomicAdd(&s_hist[d >> shift], 1u)] = rec;
       } else {
         region[written + i] = rec;
         atomicAdd(&s_hist[d >> shift], 1u);
@@ -1615,8 +1613,12 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     a.red_count[blockIdx.x] = written;
     if (a.red_records) atomicAdd(a.red_records, (unsigned long long)written);
   }
-  for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK)
-    a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
+  // (kSeg: the cursor ends at the bucket's start in the region + its records)
+  const u32* sub_start = reinterpret_cast<const u32*>(a.red_sorted);
+  for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) {
+    const size_t at = (size_t)i * gridDim.x + blockIdx.x;
+    a.red_hist[at] = kSeg ? s_hist[i] - sub_start[at] : s_hist[i];
+  }
   st.bad |= bad;
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
 }

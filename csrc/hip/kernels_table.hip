@@ -1070,23 +1070,62 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16(ApplyArgs a) {
 // registers (sqrt(n) carried), the slot written once.  The first entries of
 // the next keys are loaded before this key's chain.
 constexpr int kCsrChunk = 8;  // CSR entries a lane loads at once
-// Chains longer than this run in a second launch over the list of such keys
-// (ApplyArgs::csr_long: [0] = count, then the entries' indices)
+// Chains longer than this run in a second launch over the deferred keys
 constexpr u32 kCsrShortChain = 16;
 
-// list of the deferred long-chain keys: one atomic per wave
-__device__ __forceinline__ void csr_defer(u32* list, bool pred, u32 i) {
-  const u32 slot = wave_append<u32>(list, pred);
-  if (pred) list[1 + slot] = i;
+// Wave-private deferral lists (ApplyArgs::csr_long): wave w of a launch of W
+// waves owns [W + w * R, W + (w + 1) * R) (R = the keys one wave visits, kpi
+// per iteration of the grid-stride loop) and writes its count to [w]; the
+// second launch has the same grid and takes its own wave's list -- no global
+// counter (a single one serialised ~10^4 atomics per step at one L2 channel)
+struct CsrDefer {
+  u32* list = nullptr;
+  u32 gw = 0, waves = 0;
+  u64 R = 0;
+  __device__ __forceinline__ CsrDefer(u32* l, int64_t n_max, int64_t stride, int kpi) : list(l) {
+    gw = blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    waves = gridDim.x * (blockDim.x / kWave);
+    R = (u64)kpi * (u64)((n_max + stride - 1) / stride);
+  }
+  __device__ __forceinline__ u32* region() const { return list + waves + (u64)gw * R; }
+};
+// After the first pass the counts are scanned into offsets (waves + 1) and
+// the regions gathered into one dense list, so the second pass packs 64 long
+// chains per wave (a wave-private list holds ~2 of them: lanes idle)
+struct CsrDense {
+  const u32* offs;
+  const u32* list;
+  __device__ __forceinline__ CsrDense(const u32* l, const CsrDefer& d)
+      : offs(l + d.waves + (u64)d.waves * d.R), list(offs + d.waves + 1) {}
+};
+
+// one wave per source region: its deferred keys to their dense positions
+__global__ void __launch_bounds__(kBlock) k_csr_gather(u32* __restrict__ l, int64_t n_max,
+                                                       int64_t stride, int kpi, u32 waves) {
+  const u32 w = blockIdx.x * (kBlock / kWave) + threadIdx.x / kWave;
+  if (w >= waves) return;
+  const u64 R = (u64)kpi * (u64)((n_max + stride - 1) / stride);
+  const u32* offs = l + waves + (u64)waves * R;
+  u32* dense = const_cast<u32*>(offs) + waves + 1;
+  const u32* src = l + waves + (u64)w * R;
+  const u32 c = l[w], o = offs[w];
+  for (u32 k = lane_id(); k < c; k += kWave) dense[o + k] = src[k];
 }
 
 // kLong: the second launch (entries of the deferred list), else the first
 template <bool kLong>
 __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
   if (!kLong) XF_APPLY_SNAPSHOT(a);
-  const int64_t n = kLong ? (int64_t)a.csr_long[0] : dev_count(a.n_dev, a.n_host, a.n_max);
-  const u32* __restrict__ lst = a.csr_long + 1;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t stride0 = (int64_t)gridDim.x * blockDim.x;
+  const CsrDefer df(a.csr_long, a.n_max, stride0, kWave);
+  __shared__ u32 s_def[kBlock / kWave];
+  const int wib = threadIdx.x / kWave, lane = lane_id();
+  if (!kLong && lane == 0) s_def[wib] = 0u;
+  // (pass 2: the dense list of every wave's deferred keys, csr_dense)
+  const CsrDense dn(a.csr_long, df);
+  const int64_t n = kLong ? (int64_t)dn.offs[df.waves] : dev_count(a.n_dev, a.n_host, a.n_max);
+  const u32* __restrict__ lst = dn.list;
+  const int64_t stride = stride0;
   const FtrlParams fp = a.opt.ftrl;
   const u64* __restrict__ ent = static_cast<const u64*>(a.csr_ent);
   struct In {
@@ -1114,10 +1153,9 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
   for (; i < n; i += stride) {
     const In x = nx;
     if (i + stride < n) nx = load(i + stride);
-    if (!kLong && a.csr_long) {
-      const bool defer = x.slot != kNoSlot && x.cnt > kCsrShortChain;
-      csr_defer(a.csr_long, defer, x.key);
-      if (defer) continue;
+    if (!kLong && a.csr_long && x.slot != kNoSlot && x.cnt > kCsrShortChain) {
+      df.region()[atomicAdd(&s_def[wib], 1u)] = x.key;  // (LDS counter of this wave)
+      continue;
     }
     if (x.slot == kNoSlot || !x.cnt) continue;
     float2 nz = x.nz;
@@ -1127,18 +1165,24 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
       ftrl_push_sn(nz.x, nz.y, sn, w, __uint_as_float((u32)(e >> 32)), fp);
     };
     push(x.e0);
-    // a hot key's chain (up to one entry per slice): its entries are loaded
-    // kCsrChunk at a time, all in flight together, not one round trip each
-    for (u32 j = 1; j < x.cnt; j += kCsrChunk) {
-      u64 e[kCsrChunk];
+    if (!kLong) {  // (a short chain: a load per entry)
+      for (u32 j = 1; j < x.cnt; ++j) push(ent[x.off + j]);
+    } else {
+      // a hot key's chain (up to one entry per slice): its entries are loaded
+      // kCsrChunk at a time, all in flight together, not one round trip each
+      for (u32 j = 1; j < x.cnt; j += kCsrChunk) {
+        u64 e[kCsrChunk];
 #pragma unroll
-      for (int q = 0; q < kCsrChunk; ++q) e[q] = j + q < x.cnt ? ent[x.off + j + q] : 0ull;
+        for (int q = 0; q < kCsrChunk; ++q) e[q] = j + q < x.cnt ? ent[x.off + j + q] : 0ull;
 #pragma unroll
-      for (int q = 0; q < kCsrChunk; ++q)
-        if (j + q < x.cnt) push(e[q]);
+        for (int q = 0; q < kCsrChunk; ++q)
+          if (j + q < x.cnt) push(e[q]);
+      }
     }
     *reinterpret_cast<float2*>(a.table.words + (u64)x.slot * 4 + 2) = nz;
   }
+  // (every lane has left the loop: lane 0, the wave's last, saw every defer)
+  if (!kLong && a.csr_long && lane == 0) a.csr_long[df.gw] = s_def[wib];
 }
 
 __global__ void __launch_bounds__(kBlock) k_apply_generic(ApplyArgs a) {
@@ -1296,6 +1340,10 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
   const int p = pl.p;
   const bool multi = a.grp.oidx != nullptr;
   const bool ftrl = L.opt == kFTRL;
+  // (CSR: this wave's list of deferred long chains, k_apply_group_csr_long)
+  const CsrDefer cdf(a.csr_long, a.n_max, pl.stride, pl.K);
+  __shared__ u32 s_def[kBlock / kWave];
+  if (a.csr_long && lane_id() == 0) s_def[threadIdx.x / kWave] = 0u;
   int64_t i = pl.on ? pl.first : n;
   // (row words loaded an iteration ahead: another entry's slot -- keys are
   // unique per launch, and of a key's entries only the leader writes)
@@ -1392,7 +1440,7 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
           // producing worker (null)
           const u32 c0 = a.csr_off[row], cn = a.csr_cnt[row];
           if (a.csr_long && cn > kCsrShortChain) {  // (uniform over the key's lanes)
-            csr_defer(a.csr_long, p == 0, (u32)i);
+            if (p == 0) cdf.region()[atomicAdd(&s_def[threadIdx.x / kWave], 1u)] = (u32)i;
             deferred = true;
             break;
           }
@@ -1441,21 +1489,27 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
       if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }
   }
+  // (lane 0 -- key group 0 -- visits the wave's first key of every iteration:
+  // the wave's last lane to leave the loop)
+  if (a.csr_long && lane_id() == 0) a.csr_long[cdf.gw] = s_def[threadIdx.x / kWave];
 }
 
 // The deferred long chains of the packed CSR apply (ApplyArgs::csr_long):
 // one key group (P lanes) per listed entry, its row read from the table (or
 // the pull's stash), every entry pushed in order, the row written once.
 __global__ void __launch_bounds__(kBlock) k_apply_group_csr_long(ApplyArgs a) {
-  const int64_t n = (int64_t)a.csr_long[0];
   const TableLayout& L = a.table.L;
   const int ps = a.pstride;
   const PackedLane pl = packed_lane(L.P);
+  const CsrDefer cdf(a.csr_long, a.n_max, pl.stride, pl.K);
+  const CsrDense dn(a.csr_long, cdf);
+  const int64_t n = (int64_t)dn.offs[cdf.waves];
+  const u32* __restrict__ lst = dn.list;
   const int p = pl.p;
   const bool ftrl = L.opt == kFTRL;
   if (!pl.on) return;
   for (int64_t j = pl.first; j < n; j += pl.stride) {
-    const int64_t i = a.csr_long[1 + j];
+    const int64_t i = lst[j];
     const u32 slot = a.slots[i];
     u32* sp = a.table.words + (u64)slot * L.stride;
     const RowPre rp = a.nz_stash && ftrl
@@ -1507,14 +1561,34 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
   if (a.csr_cnt) {
     if (a.zero_after || a.reset_pos || a.sum_slices || a.grp.oidx || a.grad_map)
       throw std::runtime_error("CSR apply: bad arguments");
-    if (a.csr_long) XF_HIP_CHECK(hipMemsetAsync(a.csr_long, 0, sizeof(u32), st));
+    // deferral lists (CsrDefer, CsrDense): [counts W][regions W x R][offsets
+    // W + 1][dense list <= n][scan tiles]
+    const int g2 = lr16_slot ? grid : packed_grid(nm, L.P);
+    const int64_t waves = (int64_t)g2 * (kBlock / kWave);
+    const int per = lr16_slot ? kWave : kWave / L.P;
+    const int64_t stride = waves * per;
+    const int64_t R = per * ((nm + stride - 1) / stride);
+    u32* offs = a.csr_long + waves + waves * R;
+    u32* tiles = offs + waves + 1 + nm;
+    if (a.csr_long && (tiles - a.csr_long) + waves / 4096 + 8 > a.csr_long_cap)
+      throw std::runtime_error("CSR apply: deferral list too small");
+    auto dense = [&] {
+      launch_scan_u32(a.csr_long, offs, nullptr, waves, tiles, st);
+      hipLaunchKernelGGL(k_csr_gather, dim3((unsigned)((waves + 3) / 4)), dim3(kBlock), 0, st,
+                         a.csr_long, nm, stride, per, (u32)waves);
+    };
     if (lr16_slot) {
       hipLaunchKernelGGL(k_apply_lr16_csr<false>, dim3(grid), dim3(kBlock), 0, st, a);
-      if (a.csr_long) hipLaunchKernelGGL(k_apply_lr16_csr<true>, dim3(grid), dim3(kBlock), 0, st, a);
+      if (a.csr_long) {
+        dense();
+        hipLaunchKernelGGL(k_apply_lr16_csr<true>, dim3(grid), dim3(kBlock), 0, st, a);
+      }
     } else if (a.fm_compact && L.P <= kWave) {
-      hipLaunchKernelGGL(k_apply_group<true>, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
-      if (a.csr_long)
-        hipLaunchKernelGGL(k_apply_group_csr_long, dim3(packed_grid(nm, L.P)), dim3(kBlock), 0, st, a);
+      hipLaunchKernelGGL(k_apply_group<true>, dim3(g2), dim3(kBlock), 0, st, a);
+      if (a.csr_long) {
+        dense();
+        hipLaunchKernelGGL(k_apply_group_csr_long, dim3(g2), dim3(kBlock), 0, st, a);
+      }
     } else {
       throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots or compact reference-FM rows");
     }

@@ -264,9 +264,22 @@ constexpr int red_shift(int nv) {
 // bucket (each extra unit re-reads the bucket's records)
 constexpr int fmstd_block(int D) { return D <= 10 ? 512 : (D <= 16 ? 256 : 128); }
 constexpr int kSegMaxGroups = 2048;  // producer workgroups of the scatter-free vector form
-constexpr int64_t fmstd_lds(int D, int maxb) {
-  return (int64_t)2 * fmstd_block(D) * 8 * (2 + D) + 2 * fmstd_block(D) + 2 * maxb * 4 + 1024;
+// LDS of the producer: column-table slots (tag + NV int64 each), the row
+// list, per-bucket record cursors
+constexpr int64_t fmstd_lds_at(int D, int slots, int maxb) {
+  return (int64_t)slots * 8 * (2 + D) + 2 * fmstd_block(D) + (int64_t)maxb * 4 + 1024;
 }
+// Column-table slots: the largest table of 2, 1.75, 1.5 or 1.25 x BLOCK
+// (load <= 0.8 for a column of BLOCK distinct keys) that leaves the CU room
+// for two producer workgroups -- the column walk is a chain of barriers and
+// LDS round trips, a second workgroup hides them -- else 2 x BLOCK
+constexpr int fmstd_slots(int D) {
+  for (int q = 8; q >= 5; --q)
+    if (fmstd_lds_at(D, fmstd_block(D) * q / 4, kRedMaxBuckets) <= 80 * 1024)
+      return fmstd_block(D) * q / 4;
+  return 2 * fmstd_block(D);
+}
+constexpr int64_t fmstd_lds(int D, int maxb) { return fmstd_lds_at(D, fmstd_slots(D), maxb); }
 // (only where the workgroups per CU stay the same)
 constexpr int vec_red_max_buckets(int D) {
   return fmstd_lds(D, 2 * kRedMaxBuckets) <= 160 * 1024 &&
@@ -437,6 +450,7 @@ struct ApplyArgs {
   // chains of similar length instead of one hot key's slice-long chain and 63
   // idle lanes
   u32* csr_long = nullptr;
+  int64_t csr_long_cap = 0;        // u32 words at csr_long
   // Several sources in one launch (grp.oidx != null): n counts all received
   // entries; an entry's gradient row / mask / pulled values / stash are
   // indexed by the entry, and each key is applied by its first source's entry.
