@@ -203,8 +203,17 @@ def main():
                 x = torch.mm(x, x).clamp_(-1.0, 1.0)
             torch.cuda.synchronize(device)
         del x
+    # MVM: the field products can vanish (FTRL's first push sets a latent from
+    # (z, n), not from its init, and a product of ~fields small factors
+    # underflows): the untimed warmup records each step's train logloss, so
+    # the JSON says whether -- and after which step -- the model went dead
+    warm_ll = []
     for _ in range(a.warmup):
         step()
+        if a.model == "mvm":
+            sync()
+            stw = engine.read_stats(reset=True)
+            warm_ll.append(stw["ln_loss"] / max(stw["rows"], 1.0))
     sync()
     engine.read_stats(reset=True)
     if sharded is not None:
@@ -337,6 +346,10 @@ def main():
             out["config"]["v_dim"] = a.v_dim
             # a live MVM: the field products did not all vanish (logloss != ln 2)
             out["mvm_live"] = abs(out["logloss"] - 0.6931471805599453) > 1e-4
+            out["mvm_warmup_logloss"] = [round(x, 6) for x in warm_ll]
+            dead = [i for i, x in enumerate(warm_ll) if abs(x - 0.6931471805599453) <= 1e-4]
+            # first warmup step (0-based) whose rows all predicted exactly 0.5
+            out["mvm_dead_from_step"] = dead[0] if dead else None
         if a.optimizer == "sgd":
             out["config"]["sgd_v_init"] = a.sgd_v_init
         if a.async_p2p:
