@@ -441,11 +441,16 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
   if (b.rows > cfg_.max_rows) throw std::invalid_argument("batch rows exceed max_rows");
   if (b.col_stride > 0 && (b.row_ptr || b.col_stride < b.rows || b.nnz != b.rows * b.nnz_per_row))
     throw std::invalid_argument("field-major batch needs fixed nnz_per_row and col_stride >= rows");
-  if (parts != scratch_.parts) {
-    // slots depend on the partitioning: start from an empty scratch table
+  // table-ordered unique lists (ScratchView::home_bits) on the one-owner GPU path
+  const int hb = be_->is_gpu() && parts == 1
+                     ? table_.seg_log2 + table_.level + (table_.split > 0 ? 1 : 0)
+                     : 0;
+  if (parts != scratch_.parts || hb != scratch_.home_bits) {
+    // slots depend on the partitioning / home bits: start from an empty scratch table
     be_->fill_u64(scratch_.keys, kEmptyKey, scratch_.cap);
     be_->memset(scratch_.claims, 0, sizeof(unsigned long long));
     scratch_.parts = parts;
+    scratch_.home_bits = hb;
   }
   // (n_uniq is written, not accumulated, by both backends' dedup)
   if (++scratch_.epoch > kStampEpochs) {

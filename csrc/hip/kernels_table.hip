@@ -125,6 +125,9 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
   const u64 cap = active_cap(sv), mask = cap - 1;
   const u32 parts = (u32)sv.parts;
   const u64 R = parts > 1 ? cap / parts : cap;  // probe range per owner
+  // (ScratchView::home_bits: the top bits of the table home's hash bits)
+  const int clog = 63 - __clzll((long long)cap);
+  const int hshift = sv.home_bits > clog ? sv.home_bits - clog : 0;
   const int64_t base = (int64_t)blockIdx.x * kDedupChunk + threadIdx.x;
   for (u32 i = threadIdx.x; i < kL; i += kBlock) t_key[i] = kEmptyKey;
   u64 k[kDedupItems], s[kDedupItems];
@@ -135,7 +138,7 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
     k[j] = i < nnz ? sanitize_key(keys[i]) : 0ull;
     const u64 f = fmix64(k[j]);
     s[j] = parts > 1 ? (u64)((u32)(f >> 32) % parts) * R + (((f & 0xffffffffull) * R) >> 32)
-                     : f & mask;
+                     : (f >> hshift) & mask;
     h[j] = (u32)(f >> (64 - kDedupLog2));
   }
   __syncthreads();

@@ -110,6 +110,14 @@ struct ScratchView {
   // list comes out grouped by owner -- the all-to-all send order -- and the
   // per-owner counts are range counts (Backend::partition_counts).
   int parts = 1;
+  // HIP, parts == 1: > 0 = the number of hash bits the parameter table's home
+  // slot uses (TableView: seg_log2 + level, + 1 while segments are split).
+  // The scratch home is then the TOP log2(active cap) of those bits instead
+  // of the lowest: the compaction's slot-ordered unique list comes out sorted
+  // by table home, so the pull's and the apply's random slot accesses sweep
+  // the table in address order -- neighbouring lanes share pages and TLB
+  // entries instead of each missing in a 34 GB range.
+  int home_bits = 0;
 };
 constexpr int kMaxParts = 1024;
 
