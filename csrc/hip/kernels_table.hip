@@ -1343,10 +1343,6 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
   const int p = pl.p;
   const bool multi = a.grp.oidx != nullptr;
   const bool ftrl = L.opt == kFTRL;
-  // (CSR: this wave's list of deferred long chains, k_apply_group_csr_long)
-  const CsrDefer cdf(a.csr_long, a.n_max, pl.stride, pl.K);
-  __shared__ u32 s_def[kBlock / kWave];
-  if (a.csr_long && lane_id() == 0) s_def[threadIdx.x / kWave] = 0u;
   int64_t i = pl.on ? pl.first : n;
   // (row words loaded an iteration ahead: another entry's slot -- keys are
   // unique per launch, and of a key's entries only the leader writes)
@@ -1421,7 +1417,6 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
       // (pulled) weight, the float recipe k_red_sum<2> uses for full rows
       const float w_pre = a.fm_compact ? (a.pulled ? a.pulled[(size_t)i * ps + p] : w_next) : 0.0f;
       u32 any = 0;
-      bool deferred = false;  // (CSR: a long chain, applied by the second launch)
       if (gpipe) {
         any = 1u;
         const float raw = !a.fm_compact ? gv.x
@@ -1437,27 +1432,6 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
           e = (u32)v;
         }
         const u32 row = a.grad_map ? a.grad_map[e] : e;
-        if (a.csr_cnt) {
-          // CSR entries (slice, B, C) of compact reference-FM rows, in slice
-          // order; the raw sums are normalised here (slice_rows) or by the
-          // producing worker (null)
-          const u32 c0 = a.csr_off[row], cn = a.csr_cnt[row];
-          if (a.csr_long && cn > kCsrShortChain) {  // (uniform over the key's lanes)
-            if (p == 0) cdf.region()[atomicAdd(&s_def[threadIdx.x / kWave], 1u)] = (u32)i;
-            deferred = true;
-            break;
-          }
-          const uint3* ce = static_cast<const uint3*>(a.csr_ent) + c0;
-          any |= cn;
-          // (short chains here: the long ones run in k_apply_group_csr_long)
-          for (u32 j = 0; j < cn; ++j) {
-            const uint3 x = ce[j];
-            const float Bv = __uint_as_float(x.y), Cv = __uint_as_float(x.z);
-            const float raw = p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
-            push(norm_grad(raw, a.slice_rows, (int)x.x));
-          }
-          continue;
-        }
         const float* g = a.grads + (size_t)row * S * gs;
         const u32 m = a.masks ? a.masks[row] : all;
         if (a.masks_clear && p == 0) const_cast<u32*>(a.masks)[row] = 0u;
@@ -1477,11 +1451,9 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
             if (m & (1u << s)) push(norm_grad(raw_of(s), a.slice_rows, s));
         }
       }
-      if (!deferred) {
-        if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
-        else sp[2 + p] = __float_as_uint(n0);
-        if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
-      }
+      if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
+      else sp[2 + p] = __float_as_uint(n0);
+      if (L.has_flag && p == 0 && any) sp[L.flag_word] = 1u;
     }
     if (!multi && a.zero_after) {
       const u32 row = gpipe ? grow_i : (a.grad_map ? a.grad_map[i] : (u32)i);
@@ -1492,59 +1464,106 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
       if (p == 0 && a.masks_rw) a.masks_rw[row] = 0u;
     }
   }
-  // (lane 0 -- key group 0 -- visits the wave's first key of every iteration:
-  // the wave's last lane to leave the loop)
-  if (a.csr_long && lane_id() == 0) a.csr_long[cdf.gw] = s_def[threadIdx.x / kWave];
 }
 
-// The deferred long chains of the packed CSR apply (ApplyArgs::csr_long):
-// one key group (P lanes) per listed entry, its row read from the table (or
-// the pull's stash), every entry pushed in order, the row written once.
-__global__ void __launch_bounds__(kBlock) k_apply_group_csr_long(ApplyArgs a) {
+// CSR apply of compact reference-FM rows on packed lane groups (P lanes per
+// key, lane p owns param p): the key's entries (slice, B, C) expand with its
+// pre-step weight (g_w = D*B, g_v = C - v*B, fm_worker.cc:126-157) and push
+// in slice order.  Two-stage pipeline over the grid-stride loop: slot and
+// (off, cnt) two iterations ahead, the row words and the first entry one
+// ahead, so a key's first push waits for nothing.  kLong: the second launch,
+// over the dense list of the deferred long chains (entries 8 at a time).
+template <bool kLong>
+__global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
+  if (!kLong) XF_APPLY_SNAPSHOT(a);
   const TableLayout& L = a.table.L;
   const int ps = a.pstride;
   const PackedLane pl = packed_lane(L.P);
   const CsrDefer cdf(a.csr_long, a.n_max, pl.stride, pl.K);
   const CsrDense dn(a.csr_long, cdf);
-  const int64_t n = (int64_t)dn.offs[cdf.waves];
-  const u32* __restrict__ lst = dn.list;
+  __shared__ u32 s_def[kBlock / kWave];
+  const int wib = threadIdx.x / kWave;
+  if (!kLong && a.csr_long && lane_id() == 0) s_def[wib] = 0u;
+  const int64_t n = kLong ? (int64_t)dn.offs[cdf.waves] : dev_count(a.n_dev, a.n_host, a.n_max);
   const int p = pl.p;
   const bool ftrl = L.opt == kFTRL;
-  if (!pl.on) return;
-  for (int64_t j = pl.first; j < n; j += pl.stride) {
-    const int64_t i = lst[j];
-    const u32 slot = a.slots[i];
-    u32* sp = a.table.words + (u64)slot * L.stride;
-    const RowPre rp = a.nz_stash && ftrl
-                          ? row_stash(reinterpret_cast<const float2*>(a.nz_stash), a.keys, i, p, L.P)
-                          : row_pre(a.table.words, slot, p, L);
-    float n0 = rp.s0, z0 = rp.s1;
-    const float w0 = state_weight(rp.key, rp.flag != 0u, n0, z0, p, L, a.opt);
-    const float w_pre = a.pulled ? a.pulled[(size_t)i * ps + p] : w0;
+  const uint3* __restrict__ ent = static_cast<const uint3*>(a.csr_ent);
+  const float2* stash = ftrl ? reinterpret_cast<const float2*>(a.nz_stash) : nullptr;
+  struct A {  // stage A: independent loads
+    u32 i, slot, off, cnt;
+  };
+  struct B {  // stage B: the row words and the first entry
+    RowPre r;
+    uint3 e0;
+  };
+  auto stage_a = [&](int64_t j) {
+    A x;
+    x.i = kLong ? dn.list[j] : (u32)j;
+    x.slot = a.slots[x.i];
+    x.off = a.csr_off[x.i];
+    x.cnt = a.csr_cnt[x.i];
+    return x;
+  };
+  auto stage_b = [&](const A& x) {
+    B y;
+    y.r = stash ? row_stash(stash, a.keys, x.i, p, L.P) : row_pre(a.table.words, x.slot, p, L);
+    y.e0 = x.cnt ? ent[x.off] : make_uint3(0u, 0u, 0u);
+    return y;
+  };
+  int64_t j = pl.on ? pl.first : n;
+  const int64_t st = pl.stride;
+  A a0, a1;
+  B b0;
+  if (j < n) a0 = stage_a(j);
+  if (j + st < n) a1 = stage_a(j + st);
+  if (j < n) b0 = stage_b(a0);
+  for (; j < n; j += st) {
+    const A x = a0;
+    const B y = b0;
+    a0 = a1;
+    if (j + st < n) b0 = stage_b(a0);
+    if (j + 2 * st < n) a1 = stage_a(j + 2 * st);
+    if (x.slot == kNoSlot || !x.cnt) continue;
+    if (!kLong && a.csr_long && x.cnt > kCsrShortChain) {  // (uniform over the key's lanes)
+      if (p == 0) cdf.region()[atomicAdd(&s_def[wib], 1u)] = x.i;
+      continue;
+    }
+    float n0 = y.r.s0, z0 = y.r.s1;
+    const float w0 = state_weight(y.r.key, y.r.flag != 0u, n0, z0, p, L, a.opt);
+    const float w_pre = a.pulled ? a.pulled[(size_t)x.i * ps + p] : w0;
     float w_next = w0, sn = ftrl ? sqrtf(n0) : 0.0f;
     bool stale = false;
-    const u32 c0 = a.csr_off[i], cn = a.csr_cnt[i];
-    const uint3* ce = static_cast<const uint3*>(a.csr_ent) + c0;
-    for (u32 jj = 0; jj < cn; jj += kCsrChunk) {
-      uint3 x[kCsrChunk];
+    auto push = [&](const uint3& e) {
+      const float Bv = __uint_as_float(e.y), Cv = __uint_as_float(e.z);
+      const float g = norm_grad(p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv, a.slice_rows,
+                                (int)e.x);
+      if (stale) w_next = ftrl ? ftrl_weight_sn(z0, sn, a.opt.ftrl) : n0;
+      if (ftrl) ftrl_push_sn(n0, z0, sn, w_next, g, a.opt.ftrl);
+      else n0 = w_next - a.opt.sgd.lr * g;
+      stale = true;
+    };
+    push(y.e0);
+    if (!kLong) {
+      for (u32 q = 1; q < x.cnt; ++q) push(ent[x.off + q]);
+    } else {
+      for (u32 q0 = 1; q0 < x.cnt; q0 += kCsrChunk) {
+        uint3 e[kCsrChunk];
 #pragma unroll
-      for (int q = 0; q < kCsrChunk; ++q) x[q] = jj + q < cn ? ce[jj + q] : make_uint3(0, 0, 0);
+        for (int q = 0; q < kCsrChunk; ++q)
+          e[q] = q0 + q < x.cnt ? ent[x.off + q0 + q] : make_uint3(0u, 0u, 0u);
 #pragma unroll
-      for (int q = 0; q < kCsrChunk; ++q) {
-        if (jj + q >= cn) break;
-        const float Bv = __uint_as_float(x[q].y), Cv = __uint_as_float(x[q].z);
-        const float g = norm_grad(p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv, a.slice_rows,
-                                  (int)x[q].x);
-        if (stale) w_next = ftrl ? ftrl_weight_sn(z0, sn, a.opt.ftrl) : n0;
-        if (ftrl) ftrl_push_sn(n0, z0, sn, w_next, g, a.opt.ftrl);
-        else n0 = w_next - a.opt.sgd.lr * g;
-        stale = true;
+        for (int q = 0; q < kCsrChunk; ++q)
+          if (q0 + q < x.cnt) push(e[q]);
       }
     }
+    u32* sp = a.table.words + (u64)x.slot * L.stride;
     if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
     else sp[2 + p] = __float_as_uint(n0);
     if (L.has_flag && p == 0) sp[L.flag_word] = 1u;
   }
+  // (lane 0 -- key group 0, the wave's first key of every iteration -- is the
+  // last to leave the loop)
+  if (!kLong && a.csr_long && lane_id() == 0) a.csr_long[cdf.gw] = s_def[wib];
 }
 
 void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
@@ -1587,10 +1606,10 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
         hipLaunchKernelGGL(k_apply_lr16_csr<true>, dim3(grid), dim3(kBlock), 0, st, a);
       }
     } else if (a.fm_compact && L.P <= kWave) {
-      hipLaunchKernelGGL(k_apply_group<true>, dim3(g2), dim3(kBlock), 0, st, a);
+      hipLaunchKernelGGL(k_apply_group_csr<false>, dim3(g2), dim3(kBlock), 0, st, a);
       if (a.csr_long) {
         dense();
-        hipLaunchKernelGGL(k_apply_group_csr_long, dim3(g2), dim3(kBlock), 0, st, a);
+        hipLaunchKernelGGL(k_apply_group_csr<true>, dim3(g2), dim3(kBlock), 0, st, a);
       }
     } else {
       throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots or compact reference-FM rows");
