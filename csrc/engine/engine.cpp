@@ -37,15 +37,6 @@ bool monitor_disabled() {
   return off;
 }
 
-// XFLOW_CSR=0: several-slice steps keep the slice-group path (A/B only)
-bool csr_xflow_env() {
-  static const bool on = [] {
-    const char* e = std::getenv("XFLOW_CSR");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 }  // namespace
 
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
@@ -483,7 +474,7 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
 
 // log2 of the padded slice count when a step of S slices takes the CSR path
 int Engine::csr_slog2(int S) const {
-  if (S <= 1 || cfg_.sum_slices || !red_pairs_ || !be_->remaps_positions()) return -1;
+  if (!cfg_.csr || S <= 1 || cfg_.sum_slices || !red_pairs_ || !be_->remaps_positions()) return -1;
   const TableLayout& L = table_.L;
   const bool lr16 = cfg_.model.kind == kLR && L.stride == 4 && L.P == 1 && L.opt == kFTRL &&
                     !L.has_flag;
@@ -718,7 +709,7 @@ void Engine::train_step(const BatchView& b) {
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
   {
-    const int sl = csr_xflow_env() ? csr_slog2(S) : -1;
+    const int sl = csr_slog2(S);
     if (sl >= 0) {
       train_step_csr(b, S, sl);
       return;
@@ -844,40 +835,6 @@ void Engine::train_step(const BatchView& b) {
   }
   be_->table_pull(pa);
 
-  // LR over several whole slice groups: one producer pass over the batch
-  // with group-major dests (FwdArgs::red_gm) -- the pulled weights are the
-  // same for every group, so only the sums and the applies run per group
-  // (a producer's time is its column walk, nearly independent of its rows)
-  // (reference FM likewise: its compact (B, C) rows go to the unique-order
-  // output, so only the dests themselves must fit 32 bits)
-  const bool gm = be_->is_gpu() && (lr16 || fmu) && uq && upos && ng > 1 &&
-                  S % kSliceGroup == 0 && (double)cfg_.max_nnz * ng * kSliceGroup < 4294967295.0;
-  auto gm_args = [&](FwdArgs& fa) {
-    fa.batch = b;
-    fa.pos = pos_;
-    fa.wpull = wpull_;
-    fa.grad = grad_;
-    fa.stats = stats_;
-    fa.model = cfg_.model;
-    fa.S = S;
-    fa.agg_ok = true;  // (gm: the dest bound above)
-    fa.fx_bad = overflow_;
-    set_reduction(fa);
-    fa.red_nuq = n_uniq_;
-    fa.red_gm = 1;
-    fa.red_masks = lr_mask_;
-    fa.red_out = lr16 ? lr_grad_ : fm_grad_;
-    fa.red_inv = nullptr;
-    fa.fm_compact = fmu;  // (normalised by the apply: no red_rows)
-    fa.fm_vals = fm_vals_;
-  };
-  if (gm) {
-    FwdArgs fa;
-    gm_args(fa);
-    fa.red_phase = 1;
-    if (lr16) fa.red_rows = srows;
-    be_->forward_backward(fa);
-  }
   for (int k = 0; k < ng; ++k) {
     const u32* posk = pos_;
     const BatchView bk = group_view(b, S, k, posk);
@@ -925,13 +882,6 @@ void Engine::train_step(const BatchView& b) {
     if (rowu) {
       fa.red_out = row_grad_;
       fa.red_inv = oinv;
-    }
-    if (gm) {  // this group's sums of the one producer pass
-      fa = FwdArgs();
-      gm_args(fa);
-      fa.red_phase = 2;
-      fa.red_group = k;
-      if (lr16) fa.red_rows = srk;
     }
     be_->forward_backward(fa);
 

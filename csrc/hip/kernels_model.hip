@@ -66,8 +66,7 @@ struct RedGeom {
 };
 
 __host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
-  // (group-major dests: every group spans unique x kRedGroupSlices of them)
-  const int S = a.red_gm ? (a.S + kRedGroupSlices - 1) / kRedGroupSlices * kRedGroupSlices : a.S;
+  const int S = a.S;
   return RedGeom{a.red_bcap, a.red_cap, S, a.red_nuq, a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets,
                  fx_head_bits(a.batch.rows)};
 }
@@ -381,13 +380,8 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   }
   StatAcc st;
   float loss = 0.0f;
-  const u32 sg = active ? (u32)slice_of(b, r, a.S) : 0u;
-  // group-major dests (FwdArgs::red_gm): (g * unique + u) * 32 + s % 32 =
-  // (u + off) * S + s with S = 32, off = g * unique
-  const bool gm = kRed && a.red_gm;
-  const u32 S = gm ? (u32)kRedGroupSlices : (u32)a.S;
-  const u32 s = gm ? sg % (u32)kRedGroupSlices : sg;
-  const u32 off = gm ? (sg / (u32)kRedGroupSlices) * (u32)*a.red_nuq : 0u;
+  const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+  const u32 S = (u32)a.S;
   if (maxlen <= C) {
     u32 pv[C];
 #pragma unroll
@@ -415,7 +409,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
 #pragma unroll
         for (int j = 0; j < C; ++j) {
           if (j >= maxlen) continue;
-          if constexpr (kRed) lagg.column(j, j < len && pv[j] != a.trash_pos, (pv[j] + off) * S + s, loss);
+          if constexpr (kRed) lagg.column(j, j < len && pv[j] != a.trash_pos, pv[j] * S + s, loss);
           else lr_column<LOG2>(agg, j, j < len, pv[j] * S + s, loss, a.grad);
         }
       }
@@ -446,7 +440,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
       } else {
         for (int j = 0; j < maxlen; ++j) {
           const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
-          const u32 dest = (pj + off) * S + s;
+          const u32 dest = pj * S + s;
           if constexpr (kRed) lagg.column(j, pj != a.trash_pos, dest, loss);
           else lr_column<LOG2>(agg, j, j < len, dest, loss, a.grad);
         }
@@ -709,10 +703,6 @@ struct RedFinal {
   const int32_t* rows;
   bool compact;        // NV == 2: store (B, C) only (FwdArgs::fm_compact)
   u32* masks;          // slice-presence bits (FwdArgs::red_masks; unique order with out), or null
-  // group-major dests (FwdArgs::red_gm): the sums of group `gm_group` only --
-  // dests [g * unique * S, (g + 1) * unique * S), output rows slot - g * unique
-  const int64_t* gm_nuq;
-  int gm_group;
 };
 
 // Slice bits of one slot from the presence bitmap: its dests slot*S + s that
@@ -759,13 +749,10 @@ __device__ __forceinline__ void unit_masks(const u32* pbits, u64 lo, u64 S, u32*
 // One (bucket, sub) unit of k_red_sum: records [beg, end) of bucket b, dests
 // [lo, lo + kR).  Barriers are LDS-only: a unit's global stores need not land
 // before the next unit starts.
-// (dlo, dhi: the dest range summed -- one group's of group-major dests, else
-// everything; obase: that group's first slot, subtracted from output rows)
 template <int NV>
 __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
                                              const void* __restrict__ sorted, const RedFinal& f,
-                                             long long* acc, u32* pbits, u32* cbits,
-                                             u64 dlo = 0, u64 dhi = ~0ull, u64 obase = 0) {
+                                             long long* acc, u32* pbits, u32* cbits) {
   using T = typename RedRec<NV>::T;
   constexpr int kShift = red_shift(NV);
   constexpr u32 kR = 1u << kShift;
@@ -805,7 +792,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
       for (int q = 0; q < kRedUnroll; ++q) {
         if (i0 + (u32)q * kRedBlock >= end) continue;
         const u64 d = (u64)RedRec<NV>::dest(pr[q]), l = d - lo;
-        if (l < kR && d >= dlo && d < dhi) add(pr[q], (u32)l);  // (else another unit's / group's dest)
+        if (l < kR) add(pr[q], (u32)l);  // (else another unit's dest)
       }
     }
   } else {
@@ -816,7 +803,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
       if (i < end) {
         pr[q] = src[i];
         const u64 d = (u64)RedRec<NV>::dest(pr[q]), l = d - lo;
-        if (l < kR && d >= dlo && d < dhi) lr[q] = (u32)l;
+        if (l < kR) lr[q] = (u32)l;
       }
     }
     // zero what the records touch (same-value plain stores), and for the
@@ -848,7 +835,6 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
     if (f.out) {  // (NV == 1, S > 1) unique order
       m = uix(f.inv, slot);
       if (m == 0xFFFFFFFFu) return;
-      m -= obase;
     }
     if (slot * S >= lo && slot * S + S <= lo + kR) f.masks[m] = bits;
     else atomicOr(&f.masks[m], bits);
@@ -867,7 +853,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
         const u64 slot = dest / S, sl = dest - slot * S;
         const u32 o = uix(f.inv, slot);
         if (o != 0xFFFFFFFFu)  // (not the trash slot)
-          f.out[((u64)o - obase) * S + sl] = (float)(fx_to_double<kFx>(a) / (double)f.rows[sl]);
+          f.out[(u64)o * S + sl] = (float)(fx_to_double<kFx>(a) / (double)f.rows[sl]);
       } else {
         f.grad[dest] = (float)fx_to_double<kFx>(a);
       }
@@ -882,7 +868,7 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
           const u64 slot = dest / S, sl = dest - slot * S;
           const u32 o0 = uix(f.inv, slot);
           if (o0 == 0xFFFFFFFFu) return;
-          const u64 o = ((u64)o0 - obase) * S + sl;
+          const u64 o = (u64)o0 * S + sl;
           if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
             const double rows = (double)f.rows[0];
             reinterpret_cast<float2*>(f.out)[o] =
@@ -955,34 +941,22 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum(const void* __restrict__ 
   __shared__ u32 pbits[kR / 32];  // (f.masks) dests some record reached
   __shared__ u32 cbits[kR / 32];  // (sparse) dests whose sum is being stored
   const int shift = geom.shift(kShift);
-  u32 act = (u32)geom.active(shift, nb);
-  // group-major dests: only the buckets of the group's dest range
-  u64 dlo = 0, dhi = ~0ull, obase = 0;
-  u32 b0 = 0;
-  if (f.gm_nuq) {
-    obase = (u64)f.gm_group * (u64)*f.gm_nuq;
-    dlo = obase * (u64)f.S;
-    dhi = dlo + (u64)*f.gm_nuq * (u64)f.S;
-    if (dhi <= dlo) return;
-    b0 = (u32)(dlo >> shift);
-    const u32 b1 = (u32)((dhi - 1) >> shift) + 1;
-    act = (b1 < act ? b1 : act) > b0 ? (b1 < act ? b1 : act) - b0 : 0u;
-  }
+  const u32 act = (u32)geom.active(shift, nb);
   const u32 units = act << (shift - kShift);
   u32 id = blockIdx.x, nbeg = 0, nend = 0;
   if (id < units) {
-    nbeg = start[b0 + id % act];
-    nend = start[b0 + id % act + 1];
+    nbeg = start[id % act];
+    nend = start[id % act + 1];
   }
   for (; id < units; id += gridDim.x) {
-    const u32 beg = nbeg, end = nend, b = b0 + id % act, sub = id / act;
+    const u32 beg = nbeg, end = nend, b = id % act, sub = id / act;
     const u32 nid = id + gridDim.x;
     if (nid < units) {
-      nbeg = start[b0 + nid % act];
-      nend = start[b0 + nid % act + 1];
+      nbeg = start[nid % act];
+      nend = start[nid % act + 1];
     }
     const u64 lo = ((u64)b << shift) + ((u64)sub << kShift);
-    red_sum_unit<NV>(lo, beg, end, sorted, f, acc, pbits, cbits, dlo, dhi, obase);
+    red_sum_unit<NV>(lo, beg, end, sorted, f, acc, pbits, cbits);
     lds_barrier();  // the next unit reinitialises what this one read
   }
 }
@@ -1223,17 +1197,14 @@ __global__ void __launch_bounds__(kCsrBlock) k_red_csr(const void* __restrict__ 
 template <int NV>
 static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, hipStream_t st) {
   u32* start = a.red_tot + a.red_nb + 1;
-  if (a.red_phase != 2) {
-    hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
-                       a.red_tot, red_geom(a), red_shift(NV));
-    hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
-                       rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
-                       a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
-                       red_geom(a));
-  }
-  if (a.red_phase == 1) return;
+  hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
+                     a.red_tot, red_geom(a), red_shift(NV));
+  hipLaunchKernelGGL(k_red_scatter<NV>, dim3(groups), dim3(kRedBlock), 0, st, a.batch,
+                     rows_per_group, static_cast<const void*>(a.red_pairs), a.red_count,
+                     a.red_hist, a.red_tot, start, a.red_nb, static_cast<void*>(a.red_sorted),
+                     red_geom(a));
   if (a.red_csr.cnt) {
-    if (!a.red_nuq || a.red_gm || a.red_out || a.S != (1 << a.red_csr.slog2) ||
+    if (!a.red_nuq || a.red_out || a.S != (1 << a.red_csr.slog2) ||
         a.red_csr.slog2 > red_shift(NV) || (NV == 2 && !a.fm_compact))
       throw std::runtime_error("CSR reduction: unique positions, S = 2^slog2 <= 2^shift, no other outputs");
     hipLaunchKernelGGL(k_red_csr<NV>, dim3(a.red_nb), dim3(kCsrBlock), 0, st,
@@ -1246,11 +1217,9 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
     throw std::runtime_error("red_out with several slices needs the slice bits (red_masks)");
   if (a.red_out && a.red_rows && NV == 2 && a.S != 1)
     throw std::runtime_error("red_out: normalised compact FM rows are one-slice (send buffer)");
-  if (a.red_gm && (!a.red_nuq || !a.red_out || a.red_inv || (NV == 2 && (!a.fm_compact || a.red_rows))))
-    throw std::runtime_error("group-major reduction: unique positions, unique-order (compact) rows");
-  RedFinal f{a.grad, a.wpull, a.red_gm ? kRedGroupSlices : a.S, a.model.pstride(), a.model.v_dim,
+  RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim,
              a.red_out, a.red_inv, a.red_rows, NV == 2 && a.fm_compact,
-             a.S > 1 ? a.red_masks : nullptr, a.red_gm ? a.red_nuq : nullptr, a.red_group};
+             a.S > 1 ? a.red_masks : nullptr};
   const u32 grid = std::min<u32>((u32)(a.red_nb * a.red_nsub), (u32)device_cus());
   hipLaunchKernelGGL(k_red_sum<NV>, dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, f, red_geom(a), a.red_nb);
@@ -1979,16 +1948,12 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
     st.add(p, lab);
   }
   if constexpr (kGrad) {
-    const u32 sg = active ? (u32)slice_of(b, r, a.S) : 0u;
-    // group-major dests (FwdArgs::red_gm, as k_lr): (u + g * unique) * 32 + s % 32
-    const bool gm = a.red_gm != 0;
-    const u32 S = gm ? (u32)kRedGroupSlices : (u32)a.S;
-    const u32 s = gm ? sg % (u32)kRedGroupSlices : sg;
-    const u32 off = gm ? (sg / (u32)kRedGroupSlices) * (u32)*a.red_nuq : 0u;
+    const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
+    const u32 S = (u32)a.S;
     const float lv = loss * vsum;
     for (int j = 0; j < maxlen; ++j) {
       const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
-      lagg.column(j, pj != a.trash_pos, (pj + off) * S + s, loss, lv);
+      lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2128,10 +2093,7 @@ static void dispatch_fm(const FwdArgs& a, hipStream_t st) {
     if (a.model.fm_math != kFmReference) throw std::runtime_error("fm_vals: reference math only");
     constexpr int R = kFmGroupRows;
     const int gr = (int)((a.batch.rows + R - 1) / R);
-    if (kGrad && a.red_phase == 2) {  // one group's sums of the group-major records
-      if (!red || !a.fm_compact) throw std::runtime_error("fm_vals: needs the compact reduction");
-      launch_reduction<2>(a, 0, 0, st);
-    } else if (kGrad) {
+    if (kGrad) {
       if (!red || !a.fm_compact) throw std::runtime_error("fm_vals: needs the compact reduction");
       const int Rn = narrow_rows(a, R);
       const int gn = (int)((a.batch.rows + Rn - 1) / Rn);
@@ -2465,9 +2427,7 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
         throw std::runtime_error("red_out needs the LR bucket reduction (S > 1: with slice bits)");
       if (a.red_masks && a.S > 1 && !red)
         throw std::runtime_error("red_masks need the LR bucket reduction");
-      if (red && a.red_phase == 2) {  // one group's sums of the group-major records
-        launch_reduction<1>(a, 0, 0, st);
-      } else if (red) {
+      if (red) {
         const int R = narrow_rows(a, kLrGroupRows);
         const int gr = (int)((a.batch.rows + R - 1) / R);
         switch (R) {

@@ -218,14 +218,6 @@ struct FwdArgs {
   // 0: the model's fixed rows per workgroup.  A smaller batch (a slice group
   // of a step of more than 32 slices) may then run narrower workgroups
   int red_groups = 0;
-  // Several slice groups (of kRedGroupSlices) in one producer pass (LR,
-  // Engine::train_step): dests are group-major, ((s / 32) * unique + u) * 32 +
-  // s % 32 (needs red_nuq), so each group's sums are one contiguous dest
-  // range of one record set.  red_phase 1: producer and bucket partition only;
-  // 2: the sums of group red_group only (0: the whole reduction)
-  int red_gm = 0;
-  int red_phase = 0;
-  int red_group = 0;
   // S > 1: the reduction also writes each slot's slice-presence bits
   // (red_masks[slot] |= 1 << s for every (key, slice) with an occurrence),
   // replacing one global atomic per occurrence (slice_masks) on hot keys
@@ -256,7 +248,6 @@ struct FwdArgs {
   // raises (Engine::poll_snapshots)
   u32* fx_bad = nullptr;
 };
-constexpr int kRedGroupSlices = 32;  // slices per group-major dest block (Engine::kSliceGroup)
 constexpr int kRedShift = 14;      // 16384 gradient destinations per bucket (64 KB of LDS)
 constexpr int kRedMaxBuckets = 4096;
 // destinations per bucket for NV aggregated values per key (NV x 2^shift x 4 B <= 64 KB)

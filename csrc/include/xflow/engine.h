@@ -58,6 +58,12 @@ struct EngineConfig {
   // 687, FM-8 846 vs 893, MVM-10 1082 vs 1184:
   // profiles/r3s3_w8_owner_apply_ab.txt).
   int owner_group = 0;
+  // Steps of several slices on the GPU for LR-FTRL / reference FM: CSR
+  // gradients (one reduction and one apply of the touched (key, slice)
+  // pairs, Engine::train_step_csr) -- else slice groups of kSliceGroup
+  // (the same pushes, dense per-group buffers; also what a slice count the
+  // CSR dests cannot address falls back to)
+  bool csr = true;
 };
 
 class Engine {

@@ -278,9 +278,10 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,
                        int64_t max_nnz, int max_slices, bool sum_slices, double scratch_factor,
                        int device, bool table_grow, double grow_load, int max_log2_cap,
-                       int monitor_lag, int owner_group, double grow_start) {
+                       int monitor_lag, int owner_group, double grow_start, bool csr) {
              EngineConfig c;
              c.owner_group = owner_group;
+             c.csr = csr;
              c.table_grow = table_grow;
              c.grow_load = grow_load;
              c.grow_start = grow_start;
@@ -302,7 +303,8 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("max_slices") = 1, py::arg("sum_slices") = false,
            py::arg("scratch_factor") = 2.5, py::arg("device") = -1,
            py::arg("table_grow") = true, py::arg("grow_load") = 0.8, py::arg("max_log2_cap") = 0,
-           py::arg("monitor_lag") = 2, py::arg("owner_group") = 0, py::arg("grow_start") = 0.6)
+           py::arg("monitor_lag") = 2, py::arg("owner_group") = 0, py::arg("grow_start") = 0.6,
+           py::arg("csr") = true)
       .def_property_readonly("table_growths", &Engine::table_growths)
       .def_property_readonly("csr_steps", &Engine::csr_steps)
       .def_property_readonly("table_splits", &Engine::table_splits)

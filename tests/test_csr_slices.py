@@ -30,11 +30,11 @@ CASES = [
 ]
 
 
-def _train(device, kind, fm_math, v_dim, slices, v_scale, steps=3, fields=39):
+def _train(device, kind, fm_math, v_dim, slices, v_scale, steps=3, fields=39, csr=True):
     m = ModelConfig(kind=kind, v_dim=v_dim, fm_math=fm_math, mvm_math="fixed")
     eng = Engine(m, OptimConfig(kind="ftrl", v_init_scale=v_scale),
                  EngineConfig(table_log2_cap=22, max_rows=ROWS, max_nnz=ROWS * fields,
-                              max_slices=slices), device=device)
+                              max_slices=slices, csr=csr), device=device)
     # (MVM: few fields keep the field products -- and the gradients -- live)
     cfg = SynthConfig(seed=11, n_fields=fields, total_features=10_000_000,
                       hash_space=10_000_000)
@@ -71,5 +71,18 @@ def test_csr_step_deterministic(gpu_device):
     sums; the entries' order is the dests' order, not the records')."""
     a = _train(gpu_device, "lr", "reference", 4, 256, 1e-2)
     b = _train(gpu_device, "lr", "reference", 4, 256, 1e-2)
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,fm_math,slices", [("lr", "reference", 64), ("lr", "reference", 256),
+                                                 ("fm", "reference", 64), ("fm", "reference", 8)])
+def test_csr_equals_slice_groups_bitwise(gpu_device, kind, fm_math, slices):
+    """The CSR step and the slice-group step (EngineConfig.csr = False) push
+    the same floats in the same order: bit-identical tables."""
+    a = _train(gpu_device, kind, fm_math, 8, slices, 1e-2)
+    b = _train(gpu_device, kind, fm_math, 8, slices, 1e-2, csr=False)
+    assert a[0].csr_steps == 3 and b[0].csr_steps == 0
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_array_equal(a[2], b[2])

@@ -101,6 +101,9 @@ class EngineConfig:
     # owner apply of a multi-source sharded step on the GPU: 0 one launch per
     # source (default), 1 one grouped launch (csrc/include/xflow/engine.h)
     owner_group: int = 0
+    # several slices on the GPU (LR-FTRL, reference FM): CSR gradients of the
+    # touched (key, slice) pairs; False: slice groups of 32 (same pushes)
+    csr: bool = True
 
 
 @dataclass

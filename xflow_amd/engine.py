@@ -143,7 +143,7 @@ class Engine:
                            device=_device_index(self.device), table_grow=self.cfg.table_grow,
                            grow_load=self.cfg.grow_load, max_log2_cap=self.cfg.max_log2_cap,
                            monitor_lag=self.cfg.monitor_lag, owner_group=self.cfg.owner_group,
-                           grow_start=self.cfg.grow_start)
+                           grow_start=self.cfg.grow_start, csr=self.cfg.csr)
         if self.is_gpu != (self.device.type == "cuda"):
             raise RuntimeError("native engine backend does not match the requested device")
 
