@@ -121,24 +121,38 @@ def test_sigmoid_reference_clamps(native):
 
 @pytest.mark.parametrize("devname", DEVICES)
 def test_ftrl_single_key_closed_form(devname):
-    """One key, explicit gradients: table state follows ftrl.h:58-74 exactly."""
+    """One key, explicit gradients: table state follows ftrl.h:58-74 -- bit for
+    bit with the engine's recipe (its two divisions by alpha are products with
+    float(1/alpha), common.h), and within 1e-6 of the reference's quotients."""
     dev = _dev(devname)
     eng = Engine(ModelConfig(), OptimConfig(), EngineConfig(table_log2_cap=8, max_rows=8,
                                                             max_nnz=64), device=dev)
     a, b, l1, l2 = np.float32(0.05), np.float32(1.0), np.float32(5e-5), np.float32(10.0)
+    ia = np.float32(np.float32(1.0) / a)
     w = n = z = np.float32(0)
+    wr = nr = zr = np.float32(0)  # the reference's float recipe, divisions as written
     for g in [0.3, -0.2, 1e-5, 0.7, -0.9]:
         g = np.float32(g)
         eng.push([12345], [g])
         nn = np.float32(n + g * g)
-        z = np.float32(z + np.float32(g - np.float32(np.float32(np.sqrt(nn) - np.sqrt(n)) / a) * w))
+        z = np.float32(z + np.float32(g - np.float32(np.float32(np.sqrt(nn) - np.sqrt(n)) * ia) * w))
         n = nn
         if abs(z) <= l1:
             w = np.float32(0)
         else:
             tmpr = np.float32(z - l1) if z > 0 else np.float32(z + l1)
-            w = np.float32(tmpr / np.float32(-1.0 * np.float32(np.float32(b + np.sqrt(n)) / a + l2)))
-        assert eng.pull([12345])[0, 0] == w
+            w = np.float32(tmpr / np.float32(-1.0 * np.float32(np.float32(b + np.sqrt(n)) * ia + l2)))
+        nnr = np.float32(nr + g * g)
+        zr = np.float32(zr + np.float32(g - np.float32(np.float32(np.sqrt(nnr) - np.sqrt(nr)) / a) * wr))
+        nr = nnr
+        if abs(zr) <= l1:
+            wr = np.float32(0)
+        else:
+            tmpr = np.float32(zr - l1) if zr > 0 else np.float32(zr + l1)
+            wr = np.float32(tmpr / np.float32(-1.0 * np.float32(np.float32(b + np.sqrt(nr)) / a + l2)))
+        got = eng.pull([12345])[0, 0]
+        assert got == w
+        assert got == pytest.approx(wr, rel=1e-6, abs=1e-9)
 
 
 @pytest.mark.gpu
