@@ -526,9 +526,9 @@ void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   pa.out_nz = stash;
   be_->table_pull(pa);
 
-  // (reference FM: the raw (B, C) are normalised by the apply, after the
-  // expansion, as the slice-group path does)
-  csr_forward_backward(b, slog2, srows, !fm);
+  // (entries normalised by the reduction; reference FM: B and C before the
+  // expansion, as the slice-group path and the multi-rank send buffer do)
+  csr_forward_backward(b, slog2, srows, true);
 
   ApplyArgs aa;
   aa.table = table_;
@@ -542,7 +542,6 @@ void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   aa.P = cfg_.model.P();
   aa.fm_compact = fm;
   aa.fm_D = cfg_.model.v_dim;
-  aa.slice_rows = fm ? srows : nullptr;
   aa.nz_stash = stash;
   aa.csr_off = csr_off_;
   aa.csr_cnt = csr_cnt_;
@@ -875,9 +874,10 @@ void Engine::train_step(const BatchView& b) {
       fa.red_inv = oinv;
       fa.red_rows = srk;
     }
-    if (fmu) {
+    if (fmu) {  // (B, C) normalised before the expansion: 2 divisions a key, not P
       fa.red_out = fm_grad_;
       fa.red_inv = oinv;
+      fa.red_rows = srk;
     }
     if (rowu) {
       fa.red_out = row_grad_;
@@ -914,10 +914,11 @@ void Engine::train_step(const BatchView& b) {
     }
     if (lr16s && stash) aa.nz_stash = lr_nz_;  // (unique order, as the apply's entries)
     if (grpst && stash) aa.nz_stash = grp_nz_;
-    if (fmu) {  // unique-order raw (B, C), zeroed by the next pull
+    if (fmu) {  // unique-order normalised (B, C), zeroed by the next pull
       aa.grads = fm_grad_;
       aa.grad_map = nullptr;
       aa.zero_after = false;
+      aa.slice_rows = nullptr;
       aa.gstride = 2;
     }
     if (rowu) {  // unique-order rows, zeroed by the next pull

@@ -869,11 +869,12 @@ __device__ __forceinline__ void red_sum_unit(u64 lo, u32 beg, u32 end,
           const u32 o0 = uix(f.inv, slot);
           if (o0 == 0xFFFFFFFFu) return;
           const u64 o = (u64)o0 * S + sl;
-          if (f.rows) {  // normalised like the gather would (multi-rank send buffer)
-            const double rows = (double)f.rows[0];
+          if (f.rows) {  // normalised before the expansion (the send buffer, the fused step)
+            const double rows = (double)f.rows[sl];  // (one rounding, as k_red_csr)
             reinterpret_cast<float2*>(f.out)[o] =
-                make_float2((float)((double)B / rows), (float)((double)C / rows));
-          } else {  // normalised by the apply (fused step)
+                make_float2((float)(fx_to_double<kFx>(acc[2 * l]) / rows),
+                            (float)(fx_to_double<kFx>(acc[2 * l + 1]) / rows));
+          } else {  // normalised by the apply
             reinterpret_cast<float2*>(f.out)[o] = make_float2(B, C);
           }
         } else {
@@ -1215,8 +1216,6 @@ static void launch_reduction(const FwdArgs& a, int groups, int rows_per_group, h
     throw std::runtime_error("red_out: compact rows (reference FM)");
   if (a.red_out && a.S != 1 && !a.red_masks)
     throw std::runtime_error("red_out with several slices needs the slice bits (red_masks)");
-  if (a.red_out && a.red_rows && NV == 2 && a.S != 1)
-    throw std::runtime_error("red_out: normalised compact FM rows are one-slice (send buffer)");
   RedFinal f{a.grad, a.wpull, a.S, a.model.pstride(), a.model.v_dim,
              a.red_out, a.red_inv, a.red_rows, NV == 2 && a.fm_compact,
              a.S > 1 ? a.red_masks : nullptr};
