@@ -473,18 +473,111 @@ void Engine::dedup_(const BatchView& b, int parts, u64* uniq_keys_out, bool want
 
 
 // log2 of the padded slice count when a step of S slices takes the CSR path
-int Engine::csr_slog2(int S) const {
-  if (!cfg_.csr || S <= 1 || cfg_.sum_slices || !red_pairs_ || !be_->remaps_positions()) return -1;
-  const TableLayout& L = table_.L;
-  const bool lr16 = cfg_.model.kind == kLR && L.stride == 4 && L.P == 1 && L.opt == kFTRL &&
-                    !L.has_flag;
-  if (!lr16 && !fm_vals_) return -1;
-  int sl = 0;
-  while ((1 << sl) < S) ++sl;
-  // (a key's dests inside one reduction bucket; dests = unique * 2^sl in 32 bits)
-  if (sl > red_shift(fm_vals_ ? 2 : 1) || (double)cfg_.max_nnz * (double)(1 << sl) >= 4294967295.0)
-    return -1;
-  return sl;
+const char* grad_path_name(GradPath g) {
+  switch (g) {
+    case GradPath::kCsr: return "csr";
+    case GradPath::kUniqueLR: return "unique_lr";
+    case GradPath::kUniqueFmBC: return "unique_fm_bc";
+    case GradPath::kUniqueRows: return "unique_rows";
+    case GradPath::kSlotSums: return "slot_sums";
+    case GradPath::kSlotRows: return "slot_rows";
+  }
+  return "?";
+}
+
+StepInputs Engine::step_inputs() const {
+  StepInputs in;
+  in.gpu = be_->is_gpu();
+  in.remaps = be_->remaps_positions();
+  in.red_pairs = red_pairs_ != nullptr;
+  in.red_rowv = red_rowv_ != nullptr;
+  in.fm_vals = fm_vals_;
+  in.csr = cfg_.csr;
+  in.sum_slices = cfg_.sum_slices;
+  in.kind = cfg_.model.kind;
+  in.fm_math = cfg_.model.fm_math;
+  in.L = table_.L;
+  in.scratch_cap = (double)scratch_.cap;
+  in.max_nnz = (double)cfg_.max_nnz;
+  in.pstride = pstride();
+  in.slice_cap = slice_cap_;
+  return in;
+}
+
+StepPlan plan_step(const StepInputs& in, int S) {
+  constexpr double k32 = 4294967295.0;  // (32-bit dest * width bounds)
+  StepPlan p;
+  p.S = S;
+  const TableLayout& L = in.L;
+  const bool lr16_slot = in.kind == kLR && L.stride == 4 && L.P == 1 && L.opt == kFTRL &&
+                         !L.has_flag;
+  // CSR: several ordered slices of LR-FTRL 16-byte slots or reference FM, on
+  // unique-index positions; dests = unique * 2^sl + slice inside one bucket
+  // and in 32 bits
+  if (in.csr && S > 1 && !in.sum_slices && in.red_pairs && in.remaps && (lr16_slot || in.fm_vals)) {
+    int sl = 0;
+    while ((1 << sl) < S) ++sl;
+    if (sl <= red_shift(in.fm_vals ? 2 : 1) && in.max_nnz * (double)(1 << sl) < k32) {
+      p.csr_slog2 = sl;
+      p.grad = GradPath::kCsr;
+      return p;
+    }
+  }
+  p.groups = Engine::slice_groups(S);
+  // (slice groups always run the masked multi-slice paths: every group has >= 2 slices)
+  p.Sf = p.groups > 1 ? Engine::kSliceGroup : S;
+  p.masks = p.Sf > 1 && !in.sum_slices;
+  // LR-FTRL on 16-byte slots, bucket reduction: the reduction writes
+  // normalised gradients in unique order (through the compaction's slot ->
+  // unique index map; S > 1: [unique][slice] plus the slice bits) and the
+  // apply takes (n, z) from the pull, so it reads nothing at random and
+  // writes the slot once
+  const bool lr16_ok = in.gpu && lr16_slot && in.red_pairs && in.scratch_cap < k32;
+  // unique-index positions: pulled rows, gradient destinations and every
+  // gradient / mask buffer in unique order -- the reductions span the unique
+  // keys (S x that with S slices), not the 4x-headroom scratch slots.  The
+  // remap pass costs ~40 us per 10.2 M occurrences; same-box A/B
+  // (profiles/r4_unique_positions_ab.txt): a win with several slices (FM-8
+  // std S = 8 143 -> 222 M samples/s, FM-8 S = 8 +1.9 %, LR S = 8 +0.8 %),
+  // for standard FM (+10.5 %) and MVM (live +13 %, degenerate +2.3 %), a loss
+  // for one-slice LR (-5.1 %) and reference FM (-1.4 %)
+  p.upos = in.remaps && in.red_pairs &&
+           (p.Sf > 1 || in.kind == kMVM || (in.kind == kFM && in.fm_math == kFmStandard));
+  // slice bits from the reduction (dest * pstride in 32 bits)
+  const double key_bound = p.upos ? in.max_nnz : in.scratch_cap;
+  const bool red_masks = in.red_pairs && key_bound * in.slice_cap * in.pstride < k32 &&
+                         (in.kind == kLR || in.kind == kFM || (in.kind == kMVM && in.red_rowv));
+  p.lr16 = lr16_ok && (p.Sf == 1 || (p.masks && red_masks));
+  // summed slices: slot-indexed sums (packed apply), still the (n, z) stash
+  p.lr16s = lr16_ok && p.Sf > 1 && !p.lr16;
+  // several slices on the reduction path: unique-order [unique][slice]
+  // gradients plus the slice bits the reduction writes; the pull clears the
+  // bits, the apply reads only the present slices
+  p.uqm = p.masks && red_masks;
+  // reference FM: the normalised (B, C) sums land in unique order
+  p.fmu = in.fm_vals && (p.Sf == 1 || p.uqm);
+  // compact reference-FM rows of a grouped step: the (B, C) of later groups
+  // expand with the PULLED weights, not the table's (updated by the earlier
+  // groups), so the pull keeps the per-parameter weights
+  p.fm_keep_w = in.fm_vals && p.groups > 1;
+  // MVM (one slice) and standard-math FM (any slices) on their reduction
+  // paths: the per-key gradient rows land in unique order too (a dense apply
+  // read instead of slot-indexed rows the apply had to zero after reading)
+  const bool rows_ok = in.gpu && in.red_pairs && key_bound * in.pstride * in.slice_cap < k32;
+  p.mvmu = rows_ok && p.Sf == 1 && in.kind == kMVM && in.red_rowv;
+  p.fsu = rows_ok && (p.Sf == 1 || p.uqm) && in.kind == kFM && in.fm_math == kFmStandard;
+  p.rowu = p.mvmu || p.fsu;
+  // FTRL with several params per key on the packed apply: the pull stashes
+  // every key's (n, z) in unique order for the first group's apply
+  p.grpst = in.gpu && L.opt == kFTRL && L.P > 1;
+  // the unique-order outputs of a multi-slice step and their slice bits
+  p.uq = p.Sf > 1 && (p.lr16 || p.fmu || p.fsu);
+  p.grad = p.lr16 ? GradPath::kUniqueLR
+           : p.fmu ? GradPath::kUniqueFmBC
+           : p.rowu ? GradPath::kUniqueRows
+           : p.lr16s ? GradPath::kSlotSums
+           : GradPath::kSlotRows;
+  return p;
 }
 
 // Several slices, one pass: dedup -> pull (stash) -> one producer pass over
@@ -707,94 +800,40 @@ void Engine::train_step(const BatchView& b) {
   use_worker_set(0);
   const int S = slices_of(b);
   if (S > cfg_.max_slices) throw std::invalid_argument("batch has more slices than max_slices");
-  {
-    const int sl = csr_slog2(S);
-    if (sl >= 0) {
-      train_step_csr(b, S, sl);
-      return;
-    }
-  }
-  const int ng = slice_groups(S);
-  if (ng > 1 && cfg_.sum_slices)
+  if (cfg_.sum_slices && slice_groups(S) > 1)
     throw std::invalid_argument("sum_slices: at most 32 slices per step (ordered pushes: any count)");
-  // (slice groups always run the masked multi-slice paths: every group has >= 2 slices)
-  const int Sf = ng > 1 ? kSliceGroup : S;
+  // every layout decision, made once (plan_step)
+  const StepPlan P = plan(S);
+  if (P.grad == GradPath::kCsr) {
+    train_step_csr(b, S, P.csr_slog2);
+    return;
+  }
+  const int ng = P.groups;
   const int ps = pstride();
-  const bool masks = Sf > 1 && !cfg_.sum_slices;
+  const bool masks = P.masks;
   const int32_t* srows = slice_rows_dev(b, S);
-  // LR-FTRL on 16-byte slots, bucket reduction: the reduction writes
-  // normalised gradients in unique order (through the compaction's slot ->
-  // unique index map; S > 1: [unique][slice] plus the slice bits) and the
-  // apply takes (n, z) from the pull, so it reads nothing at random and
-  // writes the slot once.
-  const TableLayout& L = table_.L;
-  const bool lr16_layout_ok = be_->is_gpu() && cfg_.model.kind == kLR && L.stride == 4 &&
-                              L.P == 1 && L.opt == kFTRL && !L.has_flag && red_pairs_ &&
-                              (double)scratch_.cap < 4294967295.0;
-  // unique-index positions (see below): decided first, the 32-bit index
-  // bounds of the reductions depend on them
-  const bool upos_path = be_->remaps_positions() && red_pairs_ &&
-                         (Sf > 1 || cfg_.model.kind == kMVM ||
-                          (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard));
-  const bool lr16 = lr16_layout_ok && (Sf == 1 || (masks && reduction_masks(upos_path)));
-  // summed slices: slot-indexed sums (packed apply), still the (n, z) stash
-  const bool lr16s = lr16_layout_ok && Sf > 1 && !lr16;
+  const bool lr16 = P.lr16, lr16s = P.lr16s, uqm = P.uqm, fmu = P.fmu, fm_keep_w = P.fm_keep_w;
+  const bool rowu = P.rowu, fsu = P.fsu, grpst = P.grpst, uq = P.uq, upos = P.upos;
+  // (dest * ps in 32 bits over unique indices or scratch slots, see plan_step)
+  const double key_bound = upos ? (double)cfg_.max_nnz : (double)scratch_.cap;
   if (lr16s && !lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
-  // several slices on the reduction path: unique-order [unique][slice]
-  // gradients plus the slice bits the reduction writes (uq_mask_); the pull
-  // clears the bits, the apply reads only the present slices
-  const bool uqm = masks && reduction_masks(upos_path);
   if (lr16) {
     ensure_inv();
     if (!lr_grad_) lr_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * slice_cap_);
     if (!lr_nz_) lr_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz);
   }
-  // reference FM: the (B, C) sums land in unique order (dense apply read)
-  const bool fmu = fm_vals_ && (Sf == 1 || uqm);
   if (fmu) {
     ensure_inv();
     if (!fm_grad_) fm_grad_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * slice_cap_);
   }
-  // compact reference-FM rows of a grouped step: the (B, C) of later groups
-  // expand with the PULLED weights, not the table's (updated by the earlier
-  // groups), so the pull keeps the per-parameter weights
-  const bool fm_keep_w = fm_vals_ && ng > 1;
   if (fm_keep_w && !fm_w_) fm_w_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps);
-  // MVM (one slice) and standard-math FM (any slices) on their reduction
-  // paths: the per-key gradient rows land in unique order too (a dense apply
-  // read instead of slot-indexed rows the apply had to zero after reading)
-  // (row indices dest * ps in 32 bits: dests are unique indices x slices
-  // with unique-index positions -- at most max_nnz unique keys -- else
-  // scratch slots x slices)
-  const double key_bound = upos_path ? (double)cfg_.max_nnz : (double)scratch_.cap;
-  const bool rows_ok = be_->is_gpu() && red_pairs_ && key_bound * ps * slice_cap_ < 4294967295.0;
-  const bool mvmu = rows_ok && Sf == 1 && cfg_.model.kind == kMVM && red_rowv_;
-  const bool fsu = rows_ok && (Sf == 1 || uqm) && cfg_.model.kind == kFM &&
-                   cfg_.model.fm_math == kFmStandard;
-  const bool rowu = mvmu || fsu;
   if (rowu) {
     ensure_inv();
     const int rs = fsu ? slice_cap_ : 1;
     if (!row_grad_) row_grad_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ps * rs);
   }
-  // FTRL with several params per key (FM / MVM) on the packed apply: the pull
-  // stashes every key's (n, z) in unique order, so the first group's apply
-  // reads them coalesced instead of re-reading the slot's row at random
-  const bool grpst = be_->is_gpu() && L.opt == kFTRL && L.P > 1;
-  if (grpst && !grp_nz_) grp_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * L.P);
-  // the unique-order outputs of a multi-slice step and their slice bits
-  const bool uq = Sf > 1 && (lr16 || fmu || fsu);
+  if (grpst && !grp_nz_) grp_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * table_.L.P);
   if (uq && !lr_mask_) lr_mask_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
-  // unique-index positions (Backend::remap_pos, FwdArgs::red_nuq): pulled
-  // rows, gradient destinations and every gradient / mask buffer in unique
-  // order -- the reductions span the unique keys (S x that with S slices),
-  // not the 4x-headroom scratch slots.  The remap pass costs ~40 us per
-  // 10.2 M occurrences; same-box A/B (profiles/r4_unique_positions_ab.txt):
-  // a win with several slices (FM-8 std S = 8 143 -> 222 M samples/s, FM-8
-  // S = 8 +1.9 %, LR S = 8 +0.8 %), for standard FM (+10.5 %) and -- since
-  // its scaled fixed-point vector sums -- MVM (live +13 %, degenerate +2.3 %),
-  // a loss for one-slice LR (-5.1 %) and reference FM (-1.4 %).
-  const bool upos = upos_path;
   if (upos) ensure_inv();
   dedup_(b, 1, nullptr, upos || lr16 || fmu || rowu);
   inv_valid_ = false;  // (the sharded step's send order is not this one)

@@ -20,6 +20,7 @@
 // atomic per workgroup (single-address atomics serialise), and read
 // device-side element counts so a whole step runs without host syncs.
 #include <cstring>
+#include <type_traits>
 
 #include "kernels.h"
 #include "hip_util.h"
@@ -1150,7 +1151,12 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
                         : *reinterpret_cast<const float2*>(a.table.words + (u64)x.slot * 4 + 2);
     return x;
   };
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // (pass 2: few keys -- the hot ones -- each a long latency-bound chain:
+  // consecutive keys go to consecutive workgroups, so they spread over every
+  // CU and several waves share each SIMD, instead of packing 64 per wave
+  // onto the first few CUs)
+  int64_t i = kLong ? (int64_t)threadIdx.x * gridDim.x + blockIdx.x
+                    : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   In nx;
   if (i < n) nx = load(i);
   for (; i < n; i += stride) {
@@ -1168,21 +1174,28 @@ __global__ void __launch_bounds__(kBlock) k_apply_lr16_csr(ApplyArgs a) {
       ftrl_push_sn(nz.x, nz.y, sn, w, __uint_as_float((u32)(e >> 32)), fp);
     };
     push(x.e0);
-    if (!kLong) {  // (a short chain: a load per entry)
-      for (u32 j = 1; j < x.cnt; ++j) push(ent[x.off + j]);
-    } else {
-      // a hot key's chain (up to one entry per slice): its entries are loaded
-      // kCsrChunk at a time, all in flight together, not one round trip each
-      // (double-buffering the chunks measured 0.8 % slower at S = 256)
-      for (u32 j = 1; j < x.cnt; j += kCsrChunk) {
-        u64 e[kCsrChunk];
+    // the chain's values (the entries' high words) C at a time, all C loads
+    // in flight together: indices past the chain are clamped to its last
+    // entry, not predicated -- a predicated load is a branch around it and
+    // the compiler then waits on each one before the next
+    const u32* __restrict__ hv = reinterpret_cast<const u32*>(ent) + 1;
+    const u32 last = x.off + x.cnt - 1;
+    auto chain = [&](auto cc) {
+      constexpr int C = decltype(cc)::value;
+      for (u32 j = 1; j < x.cnt; j += C) {
+        float e[C];
 #pragma unroll
-        for (int q = 0; q < kCsrChunk; ++q) e[q] = j + q < x.cnt ? ent[x.off + j + q] : 0ull;
+        for (int q = 0; q < C; ++q) e[q] = __uint_as_float(hv[2 * (u64)min(x.off + j + q, last)]);
 #pragma unroll
-        for (int q = 0; q < kCsrChunk; ++q)
-          if (j + q < x.cnt) push(e[q]);
+        for (int q = 0; q < C; ++q)
+          if (j + q < x.cnt) {
+            const float w = ftrl_weight_sn(nz.y, sn, fp);
+            ftrl_push_sn(nz.x, nz.y, sn, w, e[q], fp);
+          }
       }
-    }
+    };
+    if (!kLong) chain(std::integral_constant<int, 4>());
+    else chain(std::integral_constant<int, kCsrChunk>());
     *reinterpret_cast<float2*>(a.table.words + (u64)x.slot * 4 + 2) = nz;
   }
   // (every lane has left the loop: lane 0, the wave's last, saw every defer)
@@ -1497,10 +1510,10 @@ __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
   // (B, C) of entry e: words 3e + 1, 3e + 2 of the uint3 entries
   const float* __restrict__ ebc = static_cast<const float*>(a.csr_ent) + 1;
   const float2* stash = ftrl ? reinterpret_cast<const float2*>(a.nz_stash) : nullptr;
-  auto chunk = [&](u32 off, u32 cnt, u32 c0) {  // the lane's entry of the chunk at c0
-    const u32 e = c0 + (u32)p;
-    if (e >= cnt) return make_float2(0.0f, 0.0f);
-    const float* q = ebc + 3 * (u64)(off + e);
+  // the lane's entry of the chunk at c0 (past the chain: clamped to its last
+  // entry, read but never used -- no branch around the load)
+  auto chunk = [&](u32 off, u32 cnt, u32 c0) {
+    const float* q = ebc + 3 * (u64)(off + min(c0 + (u32)p, cnt - 1u));
     return make_float2(q[0], q[1]);
   };
   struct A {  // stage A: independent loads
@@ -1521,9 +1534,11 @@ __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
   auto stage_b = [&](const A& x) {
     B y;
     y.r = stash ? row_stash(stash, a.keys, x.i, p, L.P) : row_pre(a.table.words, x.slot, p, L);
-    y.c0 = chunk(x.off, x.cnt, 0u);
+    y.c0 = x.cnt ? chunk(x.off, x.cnt, 0u) : make_float2(0.0f, 0.0f);
     return y;
   };
+  // (kLong: packed like pass 1 -- spreading the long chains one key group
+  // per wave, as k_apply_lr16_csr does, measured 10 % slower at S = 256)
   int64_t j = pl.on ? pl.first : n;
   const int64_t st = pl.stride;
   A a0, a1;

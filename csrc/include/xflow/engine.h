@@ -66,6 +66,53 @@ struct EngineConfig {
   bool csr = true;
 };
 
+// What the single-rank step's gradient layout depends on (Engine::step_inputs)
+struct StepInputs {
+  bool gpu = false;        // HIP backend
+  bool remaps = false;     // Backend::remaps_positions (unique-index positions)
+  bool red_pairs = false;  // the bucket reduction's buffers exist
+  bool red_rowv = false;   // ... and its vector records (MVM)
+  bool fm_vals = false;    // reference FM on value rows: compact (B, C) gradients
+  bool csr = true;         // EngineConfig::csr
+  bool sum_slices = false;
+  int kind = kLR;  // ModelKind
+  int fm_math = kFmReference;  // FmMath
+  TableLayout L;
+  double scratch_cap = 0.0, max_nnz = 0.0;
+  int pstride = 1, slice_cap = 1;
+};
+
+// Where a step's gradients land, one per step:
+//   kCsr        CSR entries of the touched (key, slice) pairs (S > 1, LR-FTRL 16-byte
+//               slots or reference FM): one reduction, one chain apply
+//   kUniqueLR   LR-FTRL normalised sums in unique order ([unique][slice] + slice bits)
+//   kUniqueFmBC reference-FM normalised (B, C) in unique order
+//   kUniqueRows full gradient rows in unique order (standard FM any S, MVM S = 1)
+//   kSlotSums   LR-FTRL summed slices, slot-indexed (sum_slices)
+//   kSlotRows   slot- or position-indexed rows the apply gathers and zeroes (CPU, fallbacks)
+enum class GradPath : int { kCsr = 0, kUniqueLR, kUniqueFmBC, kUniqueRows, kSlotSums, kSlotRows };
+const char* grad_path_name(GradPath g);
+
+// The step's layout decisions, made once by plan_step (a pure function of
+// StepInputs and S: unit-tested over the whole input space on the CPU) and
+// only read by Engine::train_step.  Field meanings at their use there.
+struct StepPlan {
+  int S = 1, groups = 1, Sf = 1;  // slices, slice groups, slices per group
+  int csr_slog2 = -1;             // kCsr: log2 of the padded slice count
+  GradPath grad = GradPath::kSlotRows;
+  bool masks = false;     // ordered per-slice pushes read slice bits
+  bool upos = false;      // unique-index positions (Backend::remap_pos)
+  bool lr16 = false;      // kUniqueLR
+  bool lr16s = false;     // kSlotSums
+  bool uqm = false;       // slice bits from the reduction
+  bool fmu = false;       // kUniqueFmBC
+  bool fm_keep_w = false; // the pull keeps per-parameter weights (grouped compact FM)
+  bool mvmu = false, fsu = false, rowu = false;  // kUniqueRows (MVM, standard FM, either)
+  bool grpst = false;     // the pull stashes (n, z) of multi-parameter FTRL keys
+  bool uq = false;        // unique-order slice bits (S > 1 on a unique-order layout)
+};
+StepPlan plan_step(const StepInputs& in, int S);
+
 class Engine {
  public:
   explicit Engine(const EngineConfig& cfg);
@@ -135,7 +182,10 @@ class Engine {
   // ---- the CSR exchange (several slices, GPU: LR-FTRL / reference FM) ----
   // log2 of the padded slice count when a step of S slices runs its gradients
   // as CSR entries (-1: the dense slice-group layout)
-  int csr_slog2(int S) const;
+  int csr_slog2(int S) const { return plan(S).csr_slog2; }
+  // the single-rank step's layout for S slices (plan_step on this engine)
+  StepInputs step_inputs() const;
+  StepPlan plan(int S) const { return plan_step(step_inputs(), S); }
   int csr_entry_bytes() const { return fm_vals_ ? 12 : 8; }
   // worker: forward/backward of every slice of the step at once.  pack:
   // entries packed densely in send order into ent_out (cnt_out: entries per

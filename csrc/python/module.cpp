@@ -83,12 +83,61 @@ OptSpec opt_from(py::dict d) {
   return o;
 }
 
+py::dict plan_dict(const StepPlan& p) {
+  py::dict d;
+  d["S"] = p.S;
+  d["groups"] = p.groups;
+  d["Sf"] = p.Sf;
+  d["csr_slog2"] = p.csr_slog2;
+  d["grad"] = grad_path_name(p.grad);
+  d["masks"] = p.masks;
+  d["upos"] = p.upos;
+  d["lr16"] = p.lr16;
+  d["lr16s"] = p.lr16s;
+  d["uqm"] = p.uqm;
+  d["fmu"] = p.fmu;
+  d["fm_keep_w"] = p.fm_keep_w;
+  d["mvmu"] = p.mvmu;
+  d["fsu"] = p.fsu;
+  d["rowu"] = p.rowu;
+  d["grpst"] = p.grpst;
+  d["uq"] = p.uq;
+  return d;
+}
+
+// {model, opt, gpu, remaps, red_pairs, red_rowv, fm_vals, csr, sum_slices,
+//  scratch_cap, max_nnz, slice_cap}; the table layout and pstride follow
+// from model and opt
+StepInputs inputs_from(py::dict d) {
+  StepInputs in;
+  const ModelSpec m = model_from(d["model"].cast<py::dict>());
+  const OptSpec o = opt_from(d["opt"].cast<py::dict>());
+  in.kind = m.kind;
+  in.fm_math = m.fm_math;
+  in.L = TableLayout::make(m, o);
+  in.pstride = m.pstride();
+  auto flag = [&](const char* k, bool def) { return d.contains(k) ? d[k].cast<bool>() : def; };
+  in.gpu = flag("gpu", true);
+  in.remaps = flag("remaps", in.gpu);
+  in.red_pairs = flag("red_pairs", in.gpu);
+  in.red_rowv = flag("red_rowv", in.gpu && m.kind == kMVM);
+  in.fm_vals = flag("fm_vals", in.gpu && m.kind == kFM && m.fm_math == kFmReference);
+  in.csr = flag("csr", true);
+  in.sum_slices = flag("sum_slices", false);
+  in.max_nnz = d.contains("max_nnz") ? d["max_nnz"].cast<double>() : (double)(1 << 22);
+  in.scratch_cap = d.contains("scratch_cap") ? d["scratch_cap"].cast<double>() : 4.0 * in.max_nnz;
+  in.slice_cap = d.contains("slice_cap") ? d["slice_cap"].cast<int>() : Engine::kSliceGroup;
+  return in;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_xflow_native, m) {
   m.doc() = "xflow-amd native core: HBM hash-table engine, gfx950 kernels, libffm reader";
 
   m.def("hip_available", &hip_backend_available);
+  // the single-rank step's layout decisions for hypothetical inputs (tests)
+  m.def("plan_step", [](py::dict inputs, int S) { return plan_dict(plan_step(inputs_from(inputs), S)); });
   // The reference's pred_<rank>_<block>.txt (lr_worker.cc:65-68: `pctr \t
   // 1-label \t label`, ostream default float format = %g): formatted into one
   // buffer and written with a single fwrite, without the GIL.
@@ -307,6 +356,7 @@ PYBIND11_MODULE(_xflow_native, m) {
            py::arg("csr") = true)
       .def_property_readonly("table_growths", &Engine::table_growths)
       .def_property_readonly("csr_steps", &Engine::csr_steps)
+      .def("step_plan", [](const Engine& e, int S) { return plan_dict(e.plan(S)); })
       .def_property_readonly("table_splits", &Engine::table_splits)
       .def_property_readonly("table_geometry", &Engine::table_geometry)
       .def_property_readonly("table_committed", &Engine::table_committed)
