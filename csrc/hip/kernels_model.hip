@@ -1490,10 +1490,14 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   }
   const int lane = lane_id();
   u32 written = 0, bad = 0;
+  // the next column's position is loaded before this column's barriers, so
+  // the column walk waits on no global load
+  u32 pnext = 0 < len && live ? pos[rs.at(0)] : a.trash_pos;
   for (int j = 0; j < maxlen; ++j) {
     const int t = 0;
     if (threadIdx.x == 0) s_nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
-    const u32 pj = j < len && live ? pos[rs.at(j)] : a.trash_pos;
+    const u32 pj = pnext;
+    pnext = j + 1 < len && live ? pos[rs.at(j + 1)] : a.trash_pos;
     const bool has = pj != a.trash_pos;
     bool claimed = false;
     u32 h = 0;
