@@ -221,7 +221,7 @@ Engine::~Engine() {
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, grp_nz_, own_keys_, fm_grad_,
                   row_grad_,
-                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_,
+                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_, csr_vent_,
                   csr_cnt_, csr_doff_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
@@ -499,8 +499,10 @@ StepInputs Engine::step_inputs() const {
   in.L = table_.L;
   in.scratch_cap = (double)scratch_.cap;
   in.max_nnz = (double)cfg_.max_nnz;
+  in.max_rows = (double)cfg_.max_rows;
   in.pstride = pstride();
   in.slice_cap = slice_cap_;
+  in.kdim = cfg_.model.kernel_dim();
   return in;
 }
 
@@ -514,11 +516,19 @@ StepPlan plan_step(const StepInputs& in, int S) {
   // CSR: several ordered slices of LR-FTRL 16-byte slots or reference FM, on
   // unique-index positions; dests = unique * 2^sl + slice inside one bucket
   // and in 32 bits
-  if (in.csr && S > 1 && !in.sum_slices && in.red_pairs && in.remaps && (lr16_slot || in.fm_vals)) {
+  // standard FM: full-row entries from the vector records' scatter-free
+  // form (k_red_csr_vec), single-rank
+  const bool fm_std = in.kind == kFM && in.fm_math == kFmStandard;
+  const bool std_ok = fm_std && in.gpu && in.red_rowv &&
+                      std::ceil(in.max_rows / fmstd_block(in.kdim)) <= kSegMaxGroups;
+  if (in.csr && S > 1 && !in.sum_slices && in.red_pairs && in.remaps &&
+      (lr16_slot || in.fm_vals || std_ok)) {
     int sl = 0;
     while ((1 << sl) < S) ++sl;
-    if (sl <= red_shift(in.fm_vals ? 2 : 1) && in.max_nnz * (double)(1 << sl) < k32) {
+    const int nv = in.fm_vals ? 2 : (std_ok ? 1 + in.kdim : 1);
+    if (sl <= red_shift(nv) && in.max_nnz * (double)(1 << sl) < k32) {
       p.csr_slog2 = sl;
+      p.csr_rows = std_ok;
       p.grad = GradPath::kCsr;
       return p;
     }
@@ -587,13 +597,17 @@ StepPlan plan_step(const StepInputs& in, int S) {
 void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   const int32_t* srows = slice_rows_dev(b, S);
   const bool fm = fm_vals_;
+  // standard FM: full-row entries (k_red_csr_vec), applied by the packed CSR apply
+  const bool rows = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard;
   ensure_inv();
   if (!csr_off_) {
     csr_off_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
     csr_cnt_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
   }
+  const int ew = rows ? csr_row_words(table_.L.P) : 0;
+  if (rows && !csr_vent_) csr_vent_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ew);
   float* stash;
-  if (fm) {
+  if (fm || rows) {
     if (!grp_nz_) grp_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * table_.L.P);
     stash = grp_nz_;
   } else {
@@ -638,7 +652,8 @@ void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   aa.nz_stash = stash;
   aa.csr_off = csr_off_;
   aa.csr_cnt = csr_cnt_;
-  aa.csr_ent = red_pairs_;
+  aa.csr_ent = rows ? static_cast<const void*>(csr_vent_) : red_pairs_;
+  aa.csr_ew = ew;
   // (a chain has at most S entries: with S <= 16 nothing is ever deferred)
   aa.csr_long = S > 16 ? csr_long_list(b.nnz) : nullptr;
   aa.csr_long_cap = csr_long_cap_;
@@ -672,6 +687,12 @@ void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* 
   fa.red_csr.ent = red_pairs_;
   fa.red_csr.slog2 = slog2;
   fa.red_csr.rows = normalise ? srows : nullptr;
+  if (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard) {  // full-row entries
+    if (!csr_vent_) throw std::logic_error("csr_forward_backward: no full-row entry buffer");
+    fa.red_csr.ent = csr_vent_;
+    fa.red_csr.P = table_.L.P;
+    fa.red_csr.ew = csr_row_words(table_.L.P);
+  }
   be_->forward_backward(fa);
   ++csr_steps_;
 }
@@ -790,9 +811,11 @@ void Engine::csr_debug(std::vector<u32>& off, std::vector<u32>& cnt, std::vector
   be_->copy_d2h(cnt.data(), csr_cnt_, sizeof(u32) * (size_t)n);
   u64 end = 0;
   for (int64_t i = 0; i < n; ++i) end = std::max<u64>(end, (u64)off[i] + cnt[i]);
-  const int w = csr_entry_bytes() / 4;
+  const bool rows = csr_vent_ && cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard;
+  const int w = rows ? csr_row_words(table_.L.P) : csr_entry_bytes() / 4;
   words.resize((size_t)end * w);
-  if (end) be_->copy_d2h(words.data(), red_pairs_, sizeof(u32) * (size_t)end * w);
+  if (end) be_->copy_d2h(words.data(), rows ? static_cast<const void*>(csr_vent_) : red_pairs_,
+                         sizeof(u32) * (size_t)end * w);
 }
 
 void Engine::train_step(const BatchView& b) {

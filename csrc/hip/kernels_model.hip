@@ -1764,6 +1764,175 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
 }
 
 
+// One-workgroup exclusive scan of n u32 counts (n + 1 outputs, the last the
+// total): the CSR entries' base of every bucket from its record total.
+__global__ void __launch_bounds__(kRedBlock) k_scan_small(const u32* __restrict__ in, int nb,
+                                                        u32* __restrict__ out, RedGeom geom,
+                                                        int base) {
+  const int n = geom.active(geom.shift(base), nb);  // (k_red_scan's buckets)
+  u32 carry = 0;
+  for (int c0 = 0; c0 < n; c0 += kRedBlock) {
+    const int i = c0 + (int)threadIdx.x;
+    const u32 v = i < n ? in[i] : 0u;
+    u32 t;
+    const u32 ex = block_exclusive_scan<kRedBlock>(v, &t);
+    if (i < n) out[i] = carry + ex;
+    carry += t;
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+}
+
+// CSR form of the standard-FM vector reduction (several slices, dests =
+// unique * 2^slog2 + slice): only the touched (key, slice) pairs become
+// entries (slice, g_w, g_v_0 .. g_v_{D-1}) -- expanded with the pulled v
+// (g_w = B, g_v = C - v*B, fm_worker.cc:159-202 in Rendle's form) and divided
+// by the slice's rows -- in (key, slice) order, with each key's (off, cnt):
+// the per-key push chains of the reference's per-slice pushes
+// (fm_worker.cc:241-242) in one apply.  Per bucket and window of 2^15 dests:
+// (1) a presence bitmap of the records' dests, (2) its prefix popcounts --
+// the rank of a present dest is its entry index, (3) the keys' (off, cnt)
+// from the bitmap, (4) the records' fixed-point sums accumulated at their
+// rank (1024 ranks at a time, NV int64 each in LDS), then expanded and
+// written.  Only distinct present dests take LDS, so the many-slice dest
+// space (2^slog2 per key) costs one pass over the records, not one per
+// 2^10-dest unit as the dense rows did.
+constexpr int kCsrVecWin = 15;
+template <int D, int G>
+__global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restrict__ recs, RedGeom geom,
+                                                         int nb, SegSrc sg,
+                                                         const u32* __restrict__ estart,
+                                                         CsrOut co, const float* __restrict__ wpull) {
+  constexpr int NV = 1 + D;
+  constexpr int PS = fm_ps(D);
+  constexpr int kShift = red_shift(NV);
+  // ranks per accumulation chunk: NV int64 each in <= 72 KB of LDS
+  constexpr u32 kR = 1u << ilog2c(72 * 1024 / (8 * NV));
+  constexpr u32 kWords = 1u << (kCsrVecWin - 5);
+  static_assert(kWords == kRedBlock, "one bitmap word per thread");
+  constexpr int kFx = FxBits<1>::kFx;
+  using Rec = typename VecRedRec<NV>::T;
+  __shared__ long long acc[kR * NV];
+  __shared__ u32 bits[kWords];
+  __shared__ u32 wscan[kWords];
+  __shared__ u32 rdest[kR];
+  __shared__ u32 s_pre[G];
+  __shared__ u32 s_seg[G];
+  __shared__ u32 s_tot;
+  const Rec* src = static_cast<const Rec*>(recs);
+  const int shift = geom.shift(kShift);
+  const u32 act = (u32)geom.active(shift, nb);
+  const int sl = co.slog2;
+  const u32 smask = (1u << sl) - 1u;
+  const int ew = co.ew, P = co.P;
+  float* ent = static_cast<float*>(co.ent);
+  const int tid = (int)threadIdx.x;
+  for (u32 bk = blockIdx.x; bk < act; bk += gridDim.x) {
+    const u32 nrec = sg.tot[bk];
+    if (nrec == 0) continue;  // (block-uniform)
+    const size_t row0 = (size_t)bk * sg.groups;
+    for (int g = tid; g < sg.groups; g += kRedBlock) {
+      const int64_t r0 = (int64_t)g * sg.rows_per_group;
+      const u32 base = (u32)(sg.b.row_ptr ? sg.b.row_ptr[r0] : r0 * sg.b.nnz_per_row);
+      const u32 pf = sg.hist[row0 + g];
+      s_pre[g] = pf;
+      s_seg[g] = base + sg.subs[row0 + g] - pf;
+    }
+    auto rec_at = [&](u32 i) -> const Rec& {
+      int l0 = 0, l1 = sg.groups;  // first g with s_pre[g] > i
+      while (l0 < l1) {
+        const int m = (l0 + l1) >> 1;
+        if (s_pre[m] <= i) l0 = m + 1;
+        else l1 = m;
+      }
+      return src[s_seg[l0 - 1] + i];
+    };
+    u32 ebase = estart[bk];
+    const u64 blo = (u64)bk << shift;
+    const u64 bhi = blo + (1ull << shift);
+    for (u64 lo = blo; lo < bhi; lo += 1ull << kCsrVecWin) {
+      // (1) presence
+      bits[tid] = 0u;
+      lds_barrier();
+      for (u32 i = tid; i < nrec; i += kRedBlock) {
+        const u64 l = (u64)rec_at(i).q[0].x - lo;
+        if (l < (1ull << kCsrVecWin)) atomicOr(&bits[l >> 5], 1u << (l & 31));
+      }
+      lds_barrier();
+      // (2) ranks
+      u32 tot;
+      const u32 ex = block_exclusive_scan<kRedBlock>((u32)__popc(bits[tid]), &tot);
+      wscan[tid] = ex;
+      if (tid == 0) s_tot = tot;
+      lds_barrier();
+      const u32 ndist = s_tot;
+      if (ndist == 0) continue;  // (block-uniform)
+      auto rank = [&](u32 l) {
+        return wscan[l >> 5] + (u32)__popc(bits[l >> 5] & ((1u << (l & 31)) - 1u));
+      };
+      // (3) the keys' (off, cnt): the window holds 2^(15 - slog2) keys whole
+      for (u32 k = tid; k < (1u << (kCsrVecWin - sl)); k += kRedBlock) {
+        const u32 l0 = k << sl;
+        u32 cnt;
+        if (sl >= 5) {
+          cnt = 0;
+          for (u32 w = l0 >> 5; w < (l0 + (1u << sl)) >> 5; ++w) cnt += (u32)__popc(bits[w]);
+        } else {
+          cnt = (u32)__popc((bits[l0 >> 5] >> (l0 & 31)) & ((1u << (1u << sl)) - 1u));
+        }
+        if (cnt) {
+          const u32 u = (u32)((lo + l0) >> sl);
+          co.off[u] = ebase + rank(l0);
+          co.cnt[u] = cnt;
+        }
+      }
+      // (4) sums at the ranks, kR ranks at a time
+      for (u32 c0 = 0; c0 < ndist; c0 += kR) {
+        for (u32 i = tid; i < kR * NV; i += kRedBlock) acc[i] = 0ll;
+        lds_barrier();
+        for (u32 i = tid; i < nrec; i += kRedBlock) {
+          const Rec& rr = rec_at(i);
+          const u64 l = (u64)rr.q[0].x - lo;
+          if (l >= (1ull << kCsrVecWin)) continue;
+          const u32 r = rank((u32)l) - c0;
+          if (r >= kR) continue;
+          const Rec r4 = rr;
+          u32 wv[vec_rec_words(NV)];
+#pragma unroll
+          for (int q = 0; q < vec_rec_words(NV) / 4; ++q) {
+            wv[4 * q] = r4.q[q].x;
+            wv[4 * q + 1] = r4.q[q].y;
+            wv[4 * q + 2] = r4.q[q].z;
+            wv[4 * q + 3] = r4.q[q].w;
+          }
+          rdest[r] = wv[0];  // (every record of the rank writes the same dest)
+          long long* ap = acc + r * NV;
+#pragma unroll
+          for (int c = 0; c < NV; ++c)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
+                      (unsigned long long)fx_from<kFx>(__uint_as_float(wv[1 + c])));
+        }
+        lds_barrier();
+        const u32 nr = min(kR, ndist - c0);
+        for (u32 t = tid; t < nr; t += kRedBlock) {
+          const u32 d = rdest[t];
+          const u32 u = d >> sl, s = d & smask;
+          const double rows = co.rows ? (double)co.rows[s] : 1.0;
+          const double B = fx_to_double<kFx>(acc[t * NV]);
+          const float* v = wpull + (u64)u * PS;
+          float* e = ent + (u64)(ebase + c0 + t) * (u32)ew;
+          e[0] = __uint_as_float(s);
+          e[1] = (float)(B / rows);
+#pragma unroll
+          for (int c = 1; c < NV; ++c)
+            if (c < P) e[1 + c] = (float)((fx_to_double<kFx>(acc[t * NV + c]) - (double)v[c] * B) / rows);
+        }
+        lds_barrier();  // (the next chunk reinitialises what this one read)
+      }
+      ebase += ndist;
+    }
+  }
+}
+
 // Standard-math FM forward of the split form (k_fm_std_red<.., kSplit>): one
 // lane per row, the same sums in the same order as the fused kernel; writes
 // (loss, loss*vs_0 .. loss*vs_{D-1}, pad) per row to red_rowv.
@@ -1842,9 +2011,36 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   if (a.red_maxb > vec_red_max_buckets(D) || (!seg && a.red_maxb > kRedMaxBuckets))
     throw std::runtime_error("vector reduction: bucket cap beyond the producer's");
   const bool split = a.red_rowv != nullptr;
+  if (a.red_csr.cnt) {  // several slices as CSR entries (Engine::train_step_csr)
+    if (kMvm || !seg || !split || a.red_out || !a.red_nuq || a.S != (1 << a.red_csr.slog2) ||
+        a.red_csr.slog2 > red_shift(NV) || a.red_csr.P > NV || a.red_csr.P < 1 ||
+        a.red_csr.ew < csr_row_words(a.red_csr.P))
+      throw std::runtime_error("CSR vector reduction: standard FM, split scatter-free form, unique "
+                               "positions, S = 2^slog2 <= 2^shift, full-row entries");
+  }
   if (split && !kMvm)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a);
+  if (a.red_csr.cnt) {
+    hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true, false>), dim3(groups), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
+                       a.red_tot, geom, red_shift(NV));
+    u32* estart = a.red_tot + a.red_nb + 1;  // (nb + 1 words: the scatter's starts, unused here)
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kRedBlock), 0, st, a.red_tot, a.red_nb, estart,
+                       geom, red_shift(NV));
+    const SegSrc sg{a.red_hist, a.red_tot, reinterpret_cast<const u32*>(a.red_sorted), a.batch,
+                    BLOCK, groups};
+    const u32 g2 = std::min<u32>((u32)a.red_nb, (u32)device_cus());
+    if (groups <= 512)
+      hipLaunchKernelGGL((k_red_csr_vec<D, 512>), dim3(g2), dim3(kRedBlock), 0, st,
+                         static_cast<const void*>(a.red_pairs), geom, a.red_nb, sg, estart,
+                         a.red_csr, a.wpull);
+    else
+      hipLaunchKernelGGL((k_red_csr_vec<D, kSegMaxGroups>), dim3(g2), dim3(kRedBlock), 0, st,
+                         static_cast<const void*>(a.red_pairs), geom, a.red_nb, sg, estart,
+                         a.red_csr, a.wpull);
+    return;
+  }
   if (seg) {
     if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true, kMvm>), dim3(groups), dim3(BLOCK), 0, st, a);
     else hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true>), dim3(groups), dim3(BLOCK), 0, st, a);

@@ -1491,7 +1491,11 @@ __global__ void __launch_bounds__(kBlock, 7) k_apply_group(ApplyArgs a) {
 // grid-stride loop: slot and (off, cnt) two iterations ahead, the row words
 // and the first chunk one ahead.  kLong: the second launch, over the dense
 // list of the deferred long chains.
-template <bool kLong>
+// kRows (standard FM, ApplyArgs::csr_ew): full-row entries (slice, g_0 ..
+// g_{P-1}) -- lane p reads its own component, kCsrRowChunk entries at a time
+// (clamped, all in flight), the key's lanes together one entry's row.
+constexpr int kCsrRowChunk = 4;
+template <bool kLong, bool kRows = false>
 __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
   if (!kLong) XF_APPLY_SNAPSHOT(a);
   const TableLayout& L = a.table.L;
@@ -1519,9 +1523,17 @@ __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
   struct A {  // stage A: independent loads
     u32 i, slot, off, cnt;
   };
+  // (kRows) the lane's component of entry e
+  const float* __restrict__ eg = static_cast<const float*>(a.csr_ent) + 1 + p;
+  const u32 ew = (u32)a.csr_ew;
+  auto rows_chunk = [&](u32 off, u32 cnt, u32 q0, float (&e)[kCsrRowChunk]) {
+#pragma unroll
+    for (int k = 0; k < kCsrRowChunk; ++k) e[k] = eg[(u64)(off + min(q0 + (u32)k, cnt - 1u)) * ew];
+  };
   struct B {  // stage B: the row words and the first chunk
     RowPre r;
     float2 c0;
+    float r0[kCsrRowChunk];
   };
   auto stage_a = [&](int64_t j) {
     A x;
@@ -1534,7 +1546,11 @@ __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
   auto stage_b = [&](const A& x) {
     B y;
     y.r = stash ? row_stash(stash, a.keys, x.i, p, L.P) : row_pre(a.table.words, x.slot, p, L);
-    y.c0 = x.cnt ? chunk(x.off, x.cnt, 0u) : make_float2(0.0f, 0.0f);
+    if constexpr (kRows) {
+      if (x.cnt) rows_chunk(x.off, x.cnt, 0u, y.r0);
+    } else {
+      y.c0 = x.cnt ? chunk(x.off, x.cnt, 0u) : make_float2(0.0f, 0.0f);
+    }
     return y;
   };
   // (kLong: packed like pass 1 -- spreading the long chains one key group
@@ -1559,9 +1575,34 @@ __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
     }
     float n0 = y.r.s0, z0 = y.r.s1;
     const float w0 = state_weight(y.r.key, y.r.flag != 0u, n0, z0, p, L, a.opt);
-    const float w_pre = a.pulled ? a.pulled[(size_t)x.i * ps + p] : w0;
     float w_next = w0, sn = ftrl ? sqrtf(n0) : 0.0f;
     bool stale = false;
+    auto push = [&](float g) {
+      if (stale) w_next = ftrl ? ftrl_weight_sn(z0, sn, a.opt.ftrl) : n0;
+      if (ftrl) ftrl_push_sn(n0, z0, sn, w_next, g, a.opt.ftrl);
+      else n0 = w_next - a.opt.sgd.lr * g;
+      stale = true;
+    };
+    if constexpr (kRows) {
+      float e[kCsrRowChunk];
+#pragma unroll
+      for (int k = 0; k < kCsrRowChunk; ++k) e[k] = y.r0[k];
+      for (u32 q0 = 0; q0 < x.cnt; q0 += kCsrRowChunk) {
+        float nx[kCsrRowChunk];
+        if (q0 + kCsrRowChunk < x.cnt) rows_chunk(x.off, x.cnt, q0 + kCsrRowChunk, nx);
+#pragma unroll
+        for (int k = 0; k < kCsrRowChunk; ++k)
+          if (q0 + k < x.cnt) push(e[k]);
+#pragma unroll
+        for (int k = 0; k < kCsrRowChunk; ++k) e[k] = nx[k];
+      }
+      u32* sp = a.table.words + (u64)x.slot * L.stride;
+      if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
+      else sp[2 + p] = __float_as_uint(n0);
+      if (L.has_flag && p == 0) sp[L.flag_word] = 1u;
+      continue;
+    }
+    const float w_pre = a.pulled ? a.pulled[(size_t)x.i * ps + p] : w0;
     float2 cur = y.c0;
     float2 nxt = x.cnt > P ? chunk(x.off, x.cnt, P) : make_float2(0.0f, 0.0f);
     u32 r = 0;  // q % P
@@ -1575,11 +1616,7 @@ __global__ void __launch_bounds__(kBlock) k_apply_group_csr(ApplyArgs a) {
       const float Bv = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(cur.x)));
       const float Cv = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(cur.y)));
       ++r;
-      const float g = p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv;
-      if (stale) w_next = ftrl ? ftrl_weight_sn(z0, sn, a.opt.ftrl) : n0;
-      if (ftrl) ftrl_push_sn(n0, z0, sn, w_next, g, a.opt.ftrl);
-      else n0 = w_next - a.opt.sgd.lr * g;
-      stale = true;
+      push(p == 0 ? (float)a.fm_D * Bv : Cv - w_pre * Bv);
     }
     u32* sp = a.table.words + (u64)x.slot * L.stride;
     if (ftrl) *reinterpret_cast<float2*>(sp + 2 + 2 * p) = make_float2(n0, z0);
@@ -1630,14 +1667,20 @@ void launch_table_apply(const ApplyArgs& a, hipStream_t st) {
         dense();
         hipLaunchKernelGGL(k_apply_lr16_csr<true>, dim3(grid), dim3(kBlock), 0, st, a);
       }
-    } else if (a.fm_compact && L.P <= kWave) {
+    } else if (a.fm_compact && L.P <= kWave && !a.csr_ew) {
       hipLaunchKernelGGL(k_apply_group_csr<false>, dim3(g2), dim3(kBlock), 0, st, a);
       if (a.csr_long) {
         dense();
         hipLaunchKernelGGL(k_apply_group_csr<true>, dim3(g2), dim3(kBlock), 0, st, a);
       }
+    } else if (a.csr_ew >= csr_row_words(L.P) && !a.fm_compact && L.P <= kWave) {
+      hipLaunchKernelGGL((k_apply_group_csr<false, true>), dim3(g2), dim3(kBlock), 0, st, a);
+      if (a.csr_long) {
+        dense();
+        hipLaunchKernelGGL((k_apply_group_csr<true, true>), dim3(g2), dim3(kBlock), 0, st, a);
+      }
     } else {
-      throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots or compact reference-FM rows");
+      throw std::runtime_error("CSR apply: LR-FTRL 16-byte slots, compact reference-FM rows or full rows");
     }
   } else if (a.grp.oidx) {
     if (a.zero_after || a.reset_pos) throw std::runtime_error("multi-source apply: bad arguments");

@@ -157,10 +157,15 @@ struct DedupOut {
 struct CsrOut {
   u32* off = nullptr;            // [unique] first entry of the key
   u32* cnt = nullptr;            // [unique] entries of the key (>= 1 for every key of the batch)
-  void* ent = nullptr;           // entries (FwdArgs: the producers' record regions, free by then)
+  // entries (FwdArgs: the producers' record regions, free by then; standard
+  // FM: a buffer of csr_row_words(P) words per entry, >= the step's records)
+  void* ent = nullptr;
   int slog2 = 0;
   const int32_t* rows = nullptr;  // values divided by rows[slice] (null: raw sums)
+  int ew = 0, P = 0;              // full-row entries: words per entry, params per key
 };
+// 32-bit words of a full-row CSR entry (slice, g_0 .. g_{P-1}), 16-B padded
+constexpr int csr_row_words(int P) { return (1 + P + 3) & ~3; }
 
 struct FwdArgs {
   BatchView batch;
@@ -444,6 +449,9 @@ struct ApplyArgs {
   const u32* csr_off = nullptr;
   const u32* csr_cnt = nullptr;
   const void* csr_ent = nullptr;
+  // 0: scalar entries (LR u64, reference-FM (slice, B, C)); else the words of
+  // a full-row entry (slice, g_0 .. g_{P-1}, pad: standard FM, csr_row_words)
+  int csr_ew = 0;
   // (HIP) keys with more than kCsrShortChain entries are deferred to a second
   // launch over the list of them (u32 [n] + a u32 counter): a wave then holds
   // chains of similar length instead of one hot key's slice-long chain and 63

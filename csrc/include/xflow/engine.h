@@ -78,13 +78,15 @@ struct StepInputs {
   int kind = kLR;  // ModelKind
   int fm_math = kFmReference;  // FmMath
   TableLayout L;
-  double scratch_cap = 0.0, max_nnz = 0.0;
+  double scratch_cap = 0.0, max_nnz = 0.0, max_rows = 0.0;
   int pstride = 1, slice_cap = 1;
+  int kdim = 1;  // latent width of the kernels (ModelSpec::kernel_dim)
 };
 
 // Where a step's gradients land, one per step:
 //   kCsr        CSR entries of the touched (key, slice) pairs (S > 1, LR-FTRL 16-byte
-//               slots or reference FM): one reduction, one chain apply
+//               slots, reference FM, or -- single-rank -- standard FM's full rows):
+//               one reduction, one chain apply
 //   kUniqueLR   LR-FTRL normalised sums in unique order ([unique][slice] + slice bits)
 //   kUniqueFmBC reference-FM normalised (B, C) in unique order
 //   kUniqueRows full gradient rows in unique order (standard FM any S, MVM S = 1)
@@ -99,6 +101,7 @@ const char* grad_path_name(GradPath g);
 struct StepPlan {
   int S = 1, groups = 1, Sf = 1;  // slices, slice groups, slices per group
   int csr_slog2 = -1;             // kCsr: log2 of the padded slice count
+  bool csr_rows = false;          // kCsr of full-row entries (standard FM; single-rank only)
   GradPath grad = GradPath::kSlotRows;
   bool masks = false;     // ordered per-slice pushes read slice bits
   bool upos = false;      // unique-index positions (Backend::remap_pos)
@@ -182,7 +185,11 @@ class Engine {
   // ---- the CSR exchange (several slices, GPU: LR-FTRL / reference FM) ----
   // log2 of the padded slice count when a step of S slices runs its gradients
   // as CSR entries (-1: the dense slice-group layout)
-  int csr_slog2(int S) const { return plan(S).csr_slog2; }
+  // (the multi-rank exchange carries scalar entries: LR-FTRL and reference FM)
+  int csr_slog2(int S) const {
+    const StepPlan p = plan(S);
+    return p.csr_rows ? -1 : p.csr_slog2;
+  }
   // the single-rank step's layout for S slices (plan_step on this engine)
   StepInputs step_inputs() const;
   StepPlan plan(int S) const { return plan_step(step_inputs(), S); }
@@ -419,6 +426,7 @@ class Engine {
   // reduction and one apply for any slice count
   u32* csr_off_ = nullptr;      // [max_nnz]
   u32* csr_cnt_ = nullptr;      // [max_nnz]
+  float* csr_vent_ = nullptr;   // standard FM: full-row entries [max_nnz][csr_row_words(P)]
   int64_t csr_steps_ = 0;
   void train_step_csr(const BatchView& b, int S, int slog2);
   u32* csr_doff_ = nullptr;     // [max_nnz + 1] dense offsets (worker pack)

@@ -89,6 +89,7 @@ py::dict plan_dict(const StepPlan& p) {
   d["groups"] = p.groups;
   d["Sf"] = p.Sf;
   d["csr_slog2"] = p.csr_slog2;
+  d["csr_rows"] = p.csr_rows;
   d["grad"] = grad_path_name(p.grad);
   d["masks"] = p.masks;
   d["upos"] = p.upos;
@@ -120,13 +121,15 @@ StepInputs inputs_from(py::dict d) {
   in.gpu = flag("gpu", true);
   in.remaps = flag("remaps", in.gpu);
   in.red_pairs = flag("red_pairs", in.gpu);
-  in.red_rowv = flag("red_rowv", in.gpu && m.kind == kMVM);
+  in.red_rowv = flag("red_rowv", in.gpu && (m.kind == kMVM || (m.kind == kFM && m.fm_math == kFmStandard)));
   in.fm_vals = flag("fm_vals", in.gpu && m.kind == kFM && m.fm_math == kFmReference);
   in.csr = flag("csr", true);
   in.sum_slices = flag("sum_slices", false);
   in.max_nnz = d.contains("max_nnz") ? d["max_nnz"].cast<double>() : (double)(1 << 22);
   in.scratch_cap = d.contains("scratch_cap") ? d["scratch_cap"].cast<double>() : 4.0 * in.max_nnz;
   in.slice_cap = d.contains("slice_cap") ? d["slice_cap"].cast<int>() : Engine::kSliceGroup;
+  in.max_rows = d.contains("max_rows") ? d["max_rows"].cast<double>() : (double)(1 << 16);
+  in.kdim = m.kernel_dim();
   return in;
 }
 

@@ -55,7 +55,8 @@ def test_every_input_picks_one_consistent_layout():
         assert p["rowu"] == (p["mvmu"] or p["fsu"]), tag
         if g == "csr":
             assert S > 1 and csr and not sum_slices and gpu, tag
-            assert (model == "lr" and opt == "ftrl") or model == "fm_ref", tag
+            assert (model == "lr" and opt == "ftrl") or model in ("fm_ref", "fm_std"), tag
+            assert p["csr_rows"] == (model == "fm_std"), tag
             assert (1 << p["csr_slog2"]) >= S > (1 << p["csr_slog2"]) // 2, tag
             continue
         assert p["csr_slog2"] == -1, tag
@@ -84,7 +85,9 @@ def test_every_input_picks_one_consistent_layout():
     ("fm_ref", "ftrl", 64, {"csr": False}, "unique_fm_bc"),
     ("fm_ref", "sgd", 8, {}, "csr"),
     ("fm_std", "ftrl", 1, {}, "unique_rows"),
-    ("fm_std", "ftrl", 64, {}, "unique_rows"),
+    ("fm_std", "ftrl", 64, {}, "csr"),                     # full-row entries
+    ("fm_std", "sgd", 256, {}, "csr"),
+    ("fm_std", "ftrl", 64, {"csr": False}, "unique_rows"),
     ("mvm", "ftrl", 1, {}, "unique_rows"),
     ("mvm", "ftrl", 8, {}, "slot_rows"),
     ("lr", "ftrl", 1, {"gpu": False}, "slot_rows"),
@@ -105,6 +108,12 @@ def test_csr_falls_back_past_its_dest_bounds():
     assert plan("lr", "ftrl", (1 << 14) + 1, **small)["grad"] == "unique_lr"
     assert plan("fm_ref", "ftrl", 1 << 13, **small)["grad"] == "csr"
     assert plan("fm_ref", "ftrl", (1 << 13) + 1, **small)["grad"] == "unique_fm_bc"
+    # standard FM: 2^10 dests per key at most (the vector records' bucket)
+    assert plan("fm_std", "ftrl", 1 << 10, **small)["grad"] == "csr"
+    assert plan("fm_std", "ftrl", (1 << 10) + 1, **small)["grad"] == "unique_rows"
+    # ... and the scatter-free producer form (<= 2048 workgroups of 512 rows)
+    assert plan("fm_std", "ftrl", 8, max_rows=float(1 << 20))["grad"] == "csr"
+    assert plan("fm_std", "ftrl", 8, max_rows=float((1 << 20) + 1))["grad"] == "unique_rows"
 
 
 def test_engine_plan_matches_its_backend():
