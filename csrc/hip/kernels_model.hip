@@ -1718,13 +1718,23 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
           if (u == 0xFFFFFFFFu) continue;
           row = out + ((u64)u * (u64)S + (lo + l - slot * (u64)S)) * PS;
         }
-        const float* w = wpull + slot * PS;
+        // (whole rows as dwordx4: the pulled v, the row's earlier atomics)
+        const float4* w4 = reinterpret_cast<const float4*>(wpull + slot * PS);
+        float4* r4 = reinterpret_cast<float4*>(row);
+        float w[PS], o[PS];
+#pragma unroll
+        for (int q = 0; q < PS / 4; ++q) {
+          const float4 a4 = w4[q], b4 = r4[q];
+          w[4 * q] = a4.x, w[4 * q + 1] = a4.y, w[4 * q + 2] = a4.z, w[4 * q + 3] = a4.w;
+          o[4 * q] = b4.x, o[4 * q + 1] = b4.y, o[4 * q + 2] = b4.z, o[4 * q + 3] = b4.w;
+        }
 #pragma unroll
         for (int c = 0; c < NV; ++c) {
           const long long t = acc[l * NV + c];
-          const float wk = w[c];
-          if (t != 0 && wk != 0.0f) row[c] += (float)(fx_to_double_rt(t, fxs) / (1.0 + (double)wk));
+          if (t != 0 && w[c] != 0.0f) o[c] += (float)(fx_to_double_rt(t, fxs) / (1.0 + (double)w[c]));
         }
+#pragma unroll
+        for (int q = 0; q < PS / 4; ++q) r4[q] = make_float4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
         continue;
       }
       // (B, C_0..C_{D-1}) -> g_w = B, g_v[k] = C_k - v_k*B (k_fm_std_red)
