@@ -1493,6 +1493,22 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   // the next column's position is loaded before this column's barriers, so
   // the column walk waits on no global load
   u32 pnext = 0 < len && live ? pos[rs.at(0)] : a.trash_pos;
+  // the row's fixed-point values, the same for every column: converted once
+  // (factorised: Σ loss*(vs_k - v_k) = C_k - v_k*B with B = Σ loss and C_k =
+  // Σ loss*vs_k -- v_k is the key's pulled value, one per step -- so the
+  // column walk needs no second gather of the pulled row; k_red_sum_vec
+  // expands C - v*B once per dest)
+  long long rowv[NV];
+  if constexpr (kScaled) {  // (kSplit: the row's vector, |.| <= the step's vmax)
+    rowv[0] = fx_from_rt(loss, fxs);
+#pragma unroll
+    for (int k = 0; k < D; ++k) rowv[1 + k] = fx_from_rt(vs[k], fxs);
+  } else {
+    rowv[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+      rowv[1 + k] = fx_from<kFx>(fx_clamp<kFx>(kSplit ? vs[k] : loss * vs[k], bad));
+  }
   for (int j = 0; j < maxlen; ++j) {
     const int t = 0;
     if (threadIdx.x == 0) s_nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
@@ -1501,9 +1517,6 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     const bool has = pj != a.trash_pos;
     bool claimed = false;
     u32 h = 0;
-    long long vals[NV];
-#pragma unroll
-    for (int c = 0; c < NV; ++c) vals[c] = 0ll;
     if (has) {
       const u32 dest = pj * S + sl;
       const u64 key = ((u64)(u32)j << 32) | dest;
@@ -1522,26 +1535,12 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
         }
         h = h + 1 == kSlots ? 0u : h + 1;
       }
-      // factorised: Σ loss*(vs_k - v_k) = C_k - v_k*B with B = Σ loss and
-      // C_k = Σ loss*vs_k (v_k is the key's pulled value, one per step), so the
-      // column walk needs no second gather of the pulled row; k_red_sum_vec
-      // expands C - v*B once per dest
-      if constexpr (kScaled) {  // (kSplit: the row's vector, |.| <= the step's vmax)
-        vals[0] = fx_from_rt(loss, fxs);
-#pragma unroll
-        for (int k = 0; k < D; ++k) vals[1 + k] = fx_from_rt(vs[k], fxs);
-      } else {
-        vals[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-          vals[1 + k] = fx_from<kFx>(fx_clamp<kFx>(kSplit ? vs[k] : loss * vs[k], bad));
-      }
     }
     if (has) {
       long long* acc = &s_acc[t][h * NV];
 #pragma unroll
       for (int c = 0; c < NV; ++c)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)vals[c]);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)rowv[c]);
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
