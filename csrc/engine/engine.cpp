@@ -605,7 +605,6 @@ void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
     csr_cnt_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
   }
   const int ew = rows ? csr_row_words(table_.L.P) : 0;
-  if (rows && !csr_vent_) csr_vent_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ew);
   float* stash;
   if (fm || rows) {
     if (!grp_nz_) grp_nz_ = balloc<float>(*be_, 2 * (size_t)cfg_.max_nnz * table_.L.P);
@@ -687,8 +686,8 @@ void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* 
   fa.red_csr.ent = red_pairs_;
   fa.red_csr.slog2 = slog2;
   fa.red_csr.rows = normalise ? srows : nullptr;
-  if (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard) {  // full-row entries
-    if (!csr_vent_) throw std::logic_error("csr_forward_backward: no full-row entry buffer");
+  if (csr_full_rows()) {  // full-row entries
+    if (!csr_vent_) csr_vent_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * csr_row_words(table_.L.P));
     fa.red_csr.ent = csr_vent_;
     fa.red_csr.P = table_.L.P;
     fa.red_csr.ew = csr_row_words(table_.L.P);
@@ -734,8 +733,8 @@ void Engine::w_forward_backward_csr(const BatchView& b, const float* pulled, int
   if (!pack) return;
   if (!csr_doff_) csr_doff_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz + 1);
   be_->scan_u32(csr_cnt_, csr_doff_, n_uniq_, cfg_.max_nnz);
-  be_->csr_pack(csr_off_, csr_cnt_, red_pairs_, csr_doff_, n_uniq_, cfg_.max_nnz, ent_out,
-                csr_entry_bytes());
+  be_->csr_pack(csr_off_, csr_cnt_, csr_full_rows() ? static_cast<const void*>(csr_vent_) : red_pairs_,
+                csr_doff_, n_uniq_, cfg_.max_nnz, ent_out, csr_entry_bytes());
   be_->copy_d2d(cnt_out, csr_cnt_, sizeof(u32) * (size_t)n_send);
   be_->csr_totals(counts, world, encoded, csr_doff_, totals_out);
 }
@@ -749,7 +748,7 @@ void Engine::s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* 
   stale_stashes();
   const u32* off = csr_off_;
   const u32* cnt = csr_cnt_;
-  const void* ent = red_pairs_;
+  const void* ent = csr_full_rows() ? static_cast<const void*>(csr_vent_) : red_pairs_;
   const int64_t n = src_offsets.empty() ? 0 : src_offsets.back();
   if (n > sb.n) throw std::invalid_argument("s_apply_csr: offsets beyond pull");
   if (recv_cnt) {  // received entries: offsets by a scan of the counts
@@ -781,6 +780,7 @@ void Engine::s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* 
     aa.P = cfg_.model.P();
     aa.fm_compact = fm_vals_;
     aa.fm_D = cfg_.model.v_dim;
+    aa.csr_ew = csr_full_rows() ? csr_row_words(table_.L.P) : 0;
     if (fm_vals_) {
       aa.pulled = pulled_weights(buf, o);
       if (!aa.pulled && src > first_src)
@@ -1143,7 +1143,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
     // owner-partitioned scratch: the slot-ordered unique list is the send
     // order already; counts are range counts (one range at world 1).  inv_
     // (slot -> send index) lets the LR backward write the send buffer directly.
-    if (red_pairs_ && (cfg_.model.kind == kLR || fm_vals_)) ensure_inv();
+    if (red_pairs_ && (cfg_.model.kind == kLR || fm_vals_ || csr_full_rows())) ensure_inv();
     dedup_(b, world, send_keys_out, true, world == 1 ? counts_out : nullptr);
     inv_valid_ = inv_ != nullptr;
     if (world > 1) be_->partition_counts(scratch_, block_counts_, n_uniq_, counts_out, seq);

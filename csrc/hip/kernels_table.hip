@@ -1803,6 +1803,22 @@ __global__ void __launch_bounds__(kBlock) k_csr_pack(const u32* __restrict__ off
   }
 }
 
+// full-row entries (standard FM: m 16-byte words each)
+__global__ void __launch_bounds__(kBlock) k_csr_pack_u4(const u32* __restrict__ off,
+                                                        const u32* __restrict__ cnt,
+                                                        const uint4* __restrict__ src,
+                                                        const u32* __restrict__ doff,
+                                                        const int64_t* __restrict__ n_dev,
+                                                        int64_t n_host, int m,
+                                                        uint4* __restrict__ dst) {
+  const int64_t n = n_dev ? *n_dev : n_host;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const u32 c = cnt[i], o = off[i], d = doff[i];
+    for (u32 j = 0; j < c * (u32)m; ++j) dst[(u64)d * m + j] = src[(u64)o * m + j];
+  }
+}
+
 // per-owner entry totals: owner r's keys are the send-order range of the
 // (decoded) key counts before it
 __global__ void k_csr_totals(const int64_t* __restrict__ counts, int world, int encoded,
@@ -1828,7 +1844,11 @@ void launch_csr_pack(const u32* off, const u32* cnt, const void* src, const u32*
   else if (entry_bytes == 12)
     hipLaunchKernelGGL(k_csr_pack<uint3>, dim3(g), dim3(kBlock), 0, st, off, cnt,
                        static_cast<const uint3*>(src), doff, n_dev, n_max, static_cast<uint3*>(dst));
-  else throw std::runtime_error("csr_pack: entries of 8 or 12 bytes");
+  else if (entry_bytes > 0 && entry_bytes % 16 == 0)
+    hipLaunchKernelGGL(k_csr_pack_u4, dim3(g), dim3(kBlock), 0, st, off, cnt,
+                       static_cast<const uint4*>(src), doff, n_dev, n_max, entry_bytes / 16,
+                       static_cast<uint4*>(dst));
+  else throw std::runtime_error("csr_pack: entries of 8, 12 or 16k bytes");
   XF_HIP_CHECK(hipGetLastError());
 }
 

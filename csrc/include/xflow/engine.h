@@ -85,8 +85,8 @@ struct StepInputs {
 
 // Where a step's gradients land, one per step:
 //   kCsr        CSR entries of the touched (key, slice) pairs (S > 1, LR-FTRL 16-byte
-//               slots, reference FM, or -- single-rank -- standard FM's full rows):
-//               one reduction, one chain apply
+//               slots, reference FM, or standard FM's full rows): one reduction,
+//               one chain apply
 //   kUniqueLR   LR-FTRL normalised sums in unique order ([unique][slice] + slice bits)
 //   kUniqueFmBC reference-FM normalised (B, C) in unique order
 //   kUniqueRows full gradient rows in unique order (standard FM any S, MVM S = 1)
@@ -101,7 +101,7 @@ const char* grad_path_name(GradPath g);
 struct StepPlan {
   int S = 1, groups = 1, Sf = 1;  // slices, slice groups, slices per group
   int csr_slog2 = -1;             // kCsr: log2 of the padded slice count
-  bool csr_rows = false;          // kCsr of full-row entries (standard FM; single-rank only)
+  bool csr_rows = false;          // kCsr of full-row entries (standard FM)
   GradPath grad = GradPath::kSlotRows;
   bool masks = false;     // ordered per-slice pushes read slice bits
   bool upos = false;      // unique-index positions (Backend::remap_pos)
@@ -185,15 +185,16 @@ class Engine {
   // ---- the CSR exchange (several slices, GPU: LR-FTRL / reference FM) ----
   // log2 of the padded slice count when a step of S slices runs its gradients
   // as CSR entries (-1: the dense slice-group layout)
-  // (the multi-rank exchange carries scalar entries: LR-FTRL and reference FM)
-  int csr_slog2(int S) const {
-    const StepPlan p = plan(S);
-    return p.csr_rows ? -1 : p.csr_slog2;
-  }
+  int csr_slog2(int S) const { return plan(S).csr_slog2; }
   // the single-rank step's layout for S slices (plan_step on this engine)
   StepInputs step_inputs() const;
   StepPlan plan(int S) const { return plan_step(step_inputs(), S); }
-  int csr_entry_bytes() const { return fm_vals_ ? 12 : 8; }
+  // bytes of one CSR entry: LR (slice | value) 8, reference FM (slice, B, C)
+  // 12, standard FM a full row (csr_row_words)
+  int csr_entry_bytes() const {
+    return csr_full_rows() ? 4 * csr_row_words(table_.L.P) : (fm_vals_ ? 12 : 8);
+  }
+  bool csr_full_rows() const { return cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard; }
   // worker: forward/backward of every slice of the step at once.  pack:
   // entries packed densely in send order into ent_out (cnt_out: entries per
   // key, u32 [n_send]; totals_out: entries per owner, from the step's owner

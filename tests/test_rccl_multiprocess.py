@@ -183,7 +183,10 @@ def _bs_batches(rank, dev):
 
 
 def _bs_engine(dev, rows, log2_cap, slices=1, kind="lr"):
-    return Engine(ModelConfig(kind=kind, v_dim=4), OptimConfig(),
+    # ("fm_std": standard-math FM, full-row CSR entries)
+    m = (ModelConfig(kind="fm", v_dim=4, fm_math="standard") if kind == "fm_std"
+         else ModelConfig(kind=kind, v_dim=4))
+    return Engine(m, OptimConfig(),
                   EngineConfig(table_log2_cap=log2_cap, max_rows=rows, max_nnz=rows * 39,
                                max_slices=slices), device=dev)
 
@@ -257,7 +260,7 @@ def _csr_worker(rank, world, kind, out_dir):
     np.save(os.path.join(out_dir, f"cb{rank}.npy"), np.array([sh.bytes_moved]))
 
 
-@pytest.mark.parametrize("kind", ["lr", "fm"])
+@pytest.mark.parametrize("kind", ["lr", "fm", "fm_std"])
 def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kind):
     """2 processes x 32 768 Criteo-shaped rows x 64 slices each, 3 pipelined
     steps over RCCL with the CSR gradient exchange == one engine trained on
@@ -280,7 +283,8 @@ def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kin
     v = np.concatenate([np.load(tmp_path / f"cv{r}.npy") for r in range(CSR_W)])
     assert len(np.unique(k)) == len(k) == ref.table_size()
     np.testing.assert_allclose(v, ref.pull(k), rtol=1e-4, atol=1e-6)
-    # dense per-slice blocks would move >= n_keys x 64 x 4 bytes per step
-    dense = CSR_STEPS * len(k) * CSR_S * 4 / CSR_W
+    # dense per-slice blocks would move >= n_keys x 64 x width floats per step
+    width = {"lr": 1, "fm": 2, "fm_std": 8}[kind]
+    dense = CSR_STEPS * len(k) * CSR_S * 4 * width / CSR_W
     for r in range(CSR_W):
         assert np.load(tmp_path / f"cb{r}.npy")[0] < dense / 4
