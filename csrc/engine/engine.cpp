@@ -221,7 +221,7 @@ Engine::~Engine() {
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, grp_nz_, own_keys_, fm_grad_,
                   row_grad_,
-                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_, csr_vent_,
+                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_, csr_vent_, csr_dup_, csr_dup_n_,
                   csr_cnt_, csr_doff_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
@@ -516,16 +516,18 @@ StepPlan plan_step(const StepInputs& in, int S) {
   // CSR: several ordered slices of LR-FTRL 16-byte slots or reference FM, on
   // unique-index positions; dests = unique * 2^sl + slice inside one bucket
   // and in 32 bits
-  // standard FM: full-row entries from the vector records' scatter-free
-  // form (k_red_csr_vec), single-rank
+  // standard FM / MVM: full-row entries from the vector records' scatter-
+  // free form (k_red_csr_vec; MVM's vector is its D-wide T, NV = D)
   const bool fm_std = in.kind == kFM && in.fm_math == kFmStandard;
-  const bool std_ok = fm_std && in.gpu && in.red_rowv &&
-                      std::ceil(in.max_rows / fmstd_block(in.kdim)) <= kSegMaxGroups;
+  const bool mvm = in.kind == kMVM && in.kdim >= 2;
+  const int vnv = fm_std ? 1 + in.kdim : in.kdim;  // (vector records' NV)
+  const bool std_ok = (fm_std || mvm) && in.gpu && in.red_rowv &&
+                      std::ceil(in.max_rows / fmstd_block(vnv - 1)) <= kSegMaxGroups;
   if (in.csr && S > 1 && !in.sum_slices && in.red_pairs && in.remaps &&
       (lr16_slot || in.fm_vals || std_ok)) {
     int sl = 0;
     while ((1 << sl) < S) ++sl;
-    const int nv = in.fm_vals ? 2 : (std_ok ? 1 + in.kdim : 1);
+    const int nv = in.fm_vals ? 2 : (std_ok ? vnv : 1);
     if (sl <= red_shift(nv) && in.max_nnz * (double)(1 << sl) < k32) {
       p.csr_slog2 = sl;
       p.csr_rows = std_ok;
@@ -597,8 +599,8 @@ StepPlan plan_step(const StepInputs& in, int S) {
 void Engine::train_step_csr(const BatchView& b, int S, int slog2) {
   const int32_t* srows = slice_rows_dev(b, S);
   const bool fm = fm_vals_;
-  // standard FM: full-row entries (k_red_csr_vec), applied by the packed CSR apply
-  const bool rows = cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard;
+  // standard FM / MVM: full-row entries (k_red_csr_vec), applied by the packed CSR apply
+  const bool rows = csr_full_rows();
   ensure_inv();
   if (!csr_off_) {
     csr_off_ = balloc<u32>(*be_, (size_t)cfg_.max_nnz);
@@ -687,10 +689,20 @@ void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* 
   fa.red_csr.slog2 = slog2;
   fa.red_csr.rows = normalise ? srows : nullptr;
   if (csr_full_rows()) {  // full-row entries
-    if (!csr_vent_) csr_vent_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * csr_row_words(table_.L.P));
+    const int ew = csr_row_words(table_.L.P);
+    if (!csr_vent_) csr_vent_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ew);
     fa.red_csr.ent = csr_vent_;
     fa.red_csr.P = table_.L.P;
-    fa.red_csr.ew = csr_row_words(table_.L.P);
+    fa.red_csr.ew = ew;
+    if (cfg_.model.kind == kMVM) {  // repeated-field rows' records
+      if (!csr_dup_) {
+        csr_dup_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ew);
+        csr_dup_n_ = balloc<u32>(*be_, 1);
+      }
+      be_->memset(csr_dup_n_, 0, sizeof(u32));
+      fa.red_csr.dup = csr_dup_;
+      fa.red_csr.dup_n = csr_dup_n_;
+    }
   }
   be_->forward_backward(fa);
   ++csr_steps_;

@@ -1806,11 +1806,16 @@ __global__ void __launch_bounds__(kRedBlock) k_scan_small(const u32* __restrict_
 // space (2^slog2 per key) costs one pass over the records, not one per
 // 2^10-dest unit as the dense rows did.
 constexpr int kCsrVecWin = 15;
-template <int D, int G>
+// kMvm: the records are MVM's per-row T = loss*M sums (scaled fixed point,
+// k_red_sum_vec<.., kMvm>) and an entry is g_k = Σ T_k / (1 + v_k), 0 where
+// v_k == 0 (mvm_worker.cc:137-170); rows with a repeated field are added
+// after, by k_csr_dup_add.
+template <int D, int G, bool kMvm = false>
 __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restrict__ recs, RedGeom geom,
                                                          int nb, SegSrc sg,
                                                          const u32* __restrict__ estart,
-                                                         CsrOut co, const float* __restrict__ wpull) {
+                                                         CsrOut co, const float* __restrict__ wpull,
+                                                         const u32* __restrict__ vmax) {
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
@@ -1835,6 +1840,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restric
   const int ew = co.ew, P = co.P;
   float* ent = static_cast<float*>(co.ent);
   const int tid = (int)threadIdx.x;
+  const int fxs = kMvm ? fx_scale_bits(vmax, geom.fx_head) : kFx;
   for (u32 bk = blockIdx.x; bk < act; bk += gridDim.x) {
     const u32 nrec = sg.tot[bk];
     if (nrec == 0) continue;  // (block-uniform)
@@ -1918,7 +1924,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restric
 #pragma unroll
           for (int c = 0; c < NV; ++c)
             atomicAdd(reinterpret_cast<unsigned long long*>(&ap[c]),
-                      (unsigned long long)fx_from<kFx>(__uint_as_float(wv[1 + c])));
+                      (unsigned long long)fx_from_rt(__uint_as_float(wv[1 + c]), fxs));
         }
         lds_barrier();
         const u32 nr = min(kR, ndist - c0);
@@ -1926,19 +1932,52 @@ __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restric
           const u32 d = rdest[t];
           const u32 u = d >> sl, s = d & smask;
           const double rows = co.rows ? (double)co.rows[s] : 1.0;
-          const double B = fx_to_double<kFx>(acc[t * NV]);
           const float* v = wpull + (u64)u * PS;
           float* e = ent + (u64)(ebase + c0 + t) * (u32)ew;
           e[0] = __uint_as_float(s);
-          e[1] = (float)(B / rows);
+          if constexpr (kMvm) {
 #pragma unroll
-          for (int c = 1; c < NV; ++c)
-            if (c < P) e[1 + c] = (float)((fx_to_double<kFx>(acc[t * NV + c]) - (double)v[c] * B) / rows);
+            for (int c = 0; c < NV; ++c) {
+              const long long tc = acc[t * NV + c];
+              if (c < P)
+                e[1 + c] = tc != 0 && v[c] != 0.0f
+                               ? (float)(fx_to_double_rt(tc, fxs) / (1.0 + (double)v[c]) / rows)
+                               : 0.0f;
+            }
+          } else {
+            const double B = fx_to_double_rt(acc[t * NV], fxs);
+            e[1] = (float)(B / rows);
+#pragma unroll
+            for (int c = 1; c < NV; ++c)
+              if (c < P) e[1 + c] = (float)((fx_to_double_rt(acc[t * NV + c], fxs) - (double)v[c] * B) / rows);
+          }
         }
         lds_barrier();  // (the next chunk reinitialises what this one read)
       }
       ebase += ndist;
     }
+  }
+}
+
+// MVM rows with a repeated field (CsrOut::dup): each occurrence's gradient
+// row is added to its (key, slice) entry -- every occurrence left a record,
+// so the entry exists -- divided by the slice's rows, by float atomics (the
+// dense rows took them the same way).
+__global__ void __launch_bounds__(kBlock) k_csr_dup_add(CsrOut co, int max_n) {
+  const u32 n = min(*co.dup_n, (u32)max_n);
+  const int sl = co.slog2;
+  const u32 smask = (1u << sl) - 1u;
+  float* ent = static_cast<float*>(co.ent);
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float* r = co.dup + (size_t)i * co.ew;
+    const u32 d = __float_as_uint(r[0]);
+    const u32 u = d >> sl, s = d & smask;
+    const u32 o = co.off[u], c = co.cnt[u];
+    u32 e = o;
+    while (e < o + c && __float_as_uint(ent[(size_t)e * co.ew]) != s) ++e;
+    if (e == o + c) continue;  // (cannot happen: the occurrence left a record)
+    const float rows = co.rows ? (float)co.rows[s] : 1.0f;
+    for (int k = 0; k < co.P && k + 1 < co.ew; ++k) atomicAdd(&ent[(size_t)e * co.ew + 1 + k], r[1 + k] / rows);
   }
 }
 
@@ -2021,17 +2060,18 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
     throw std::runtime_error("vector reduction: bucket cap beyond the producer's");
   const bool split = a.red_rowv != nullptr;
   if (a.red_csr.cnt) {  // several slices as CSR entries (Engine::train_step_csr)
-    if (kMvm || !seg || !split || a.red_out || !a.red_nuq || a.S != (1 << a.red_csr.slog2) ||
+    if (!seg || !split || a.red_out || !a.red_nuq || a.S != (1 << a.red_csr.slog2) ||
+        (kMvm && (!a.red_csr.dup || !a.red_csr.dup_n)) ||
         a.red_csr.slog2 > red_shift(NV) || a.red_csr.P > NV || a.red_csr.P < 1 ||
         a.red_csr.ew < csr_row_words(a.red_csr.P))
-      throw std::runtime_error("CSR vector reduction: standard FM, split scatter-free form, unique "
-                               "positions, S = 2^slog2 <= 2^shift, full-row entries");
+      throw std::runtime_error("CSR vector reduction: split scatter-free form, unique positions, "
+                               "S = 2^slog2 <= 2^shift, full-row entries (MVM: dup records)");
   }
   if (split && !kMvm)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a);
   if (a.red_csr.cnt) {
-    hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true, false>), dim3(groups), dim3(BLOCK), 0, st, a);
+    hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, true, true, kMvm>), dim3(groups), dim3(BLOCK), 0, st, a);
     hipLaunchKernelGGL(k_red_scan, dim3(a.red_nb), dim3(kBlock), 0, st, a.red_hist, groups,
                        a.red_tot, geom, red_shift(NV));
     u32* estart = a.red_tot + a.red_nb + 1;  // (nb + 1 words: the scatter's starts, unused here)
@@ -2041,13 +2081,16 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
                     BLOCK, groups};
     const u32 g2 = std::min<u32>((u32)a.red_nb, (u32)device_cus());
     if (groups <= 512)
-      hipLaunchKernelGGL((k_red_csr_vec<D, 512>), dim3(g2), dim3(kRedBlock), 0, st,
+      hipLaunchKernelGGL((k_red_csr_vec<D, 512, kMvm>), dim3(g2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), geom, a.red_nb, sg, estart,
-                         a.red_csr, a.wpull);
+                         a.red_csr, a.wpull, a.red_vmax);
     else
-      hipLaunchKernelGGL((k_red_csr_vec<D, kSegMaxGroups>), dim3(g2), dim3(kRedBlock), 0, st,
+      hipLaunchKernelGGL((k_red_csr_vec<D, kSegMaxGroups, kMvm>), dim3(g2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), geom, a.red_nb, sg, estart,
-                         a.red_csr, a.wpull);
+                         a.red_csr, a.wpull, a.red_vmax);
+    if (kMvm)  // (rows with a repeated field: rare; one small grid)
+      hipLaunchKernelGGL(k_csr_dup_add, dim3(std::min<int64_t>(1024, (a.batch.nnz + kBlock - 1) / kBlock + 1)),
+                         dim3(kBlock), 0, st, a.red_csr, (int)a.batch.nnz);
     return;
   }
   if (seg) {
@@ -2537,7 +2580,19 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           if (blockIdx.x == 0) *a.red_vmax_next = 0u;  // (the next step's word)
         }
       }
-      if (active && dup) {
+      if (active && dup && a.red_csr.cnt) {
+        // (CSR entries: the row's occurrences as dup records, k_csr_dup_add)
+        const int ew = a.red_csr.ew;
+        for (int j = 0; j < len; ++j) {
+          float c[D];
+          contrib(j, c);
+          const u32 pj = pos[rs.at(j)];
+          if (pj == a.trash_pos) continue;
+          float* rec = a.red_csr.dup + (size_t)atomicAdd(a.red_csr.dup_n, 1u) * ew;
+          rec[0] = __uint_as_float(pj * S + s);
+          for (int k = 0; k < D && k + 1 < ew; ++k) rec[1 + k] = c[k];
+        }
+      } else if (active && dup) {
         for (int j = 0; j < len; ++j) {
           float c[D];
           contrib(j, c);

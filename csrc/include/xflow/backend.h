@@ -163,6 +163,12 @@ struct CsrOut {
   int slog2 = 0;
   const int32_t* rows = nullptr;  // values divided by rows[slice] (null: raw sums)
   int ew = 0, P = 0;              // full-row entries: words per entry, params per key
+  // MVM: rows with a repeated field (their gradient is not T / (1 + v) of the
+  // key's own v) leave (dest, c_0 .. c_{P-1}) records of ew words here,
+  // counted at dup_n (zeroed before the forward); added to their entries after
+  // the reduction (float atomics, as the dense rows took them)
+  float* dup = nullptr;
+  u32* dup_n = nullptr;
 };
 // 32-bit words of a full-row CSR entry (slice, g_0 .. g_{P-1}), 16-B padded
 constexpr int csr_row_words(int P) { return (1 + P + 3) & ~3; }

@@ -85,8 +85,8 @@ struct StepInputs {
 
 // Where a step's gradients land, one per step:
 //   kCsr        CSR entries of the touched (key, slice) pairs (S > 1, LR-FTRL 16-byte
-//               slots, reference FM, or standard FM's full rows): one reduction,
-//               one chain apply
+//               slots, reference FM, or the full rows of standard FM and MVM): one
+//               reduction, one chain apply
 //   kUniqueLR   LR-FTRL normalised sums in unique order ([unique][slice] + slice bits)
 //   kUniqueFmBC reference-FM normalised (B, C) in unique order
 //   kUniqueRows full gradient rows in unique order (standard FM any S, MVM S = 1)
@@ -101,7 +101,7 @@ const char* grad_path_name(GradPath g);
 struct StepPlan {
   int S = 1, groups = 1, Sf = 1;  // slices, slice groups, slices per group
   int csr_slog2 = -1;             // kCsr: log2 of the padded slice count
-  bool csr_rows = false;          // kCsr of full-row entries (standard FM)
+  bool csr_rows = false;          // kCsr of full-row entries (standard FM, MVM)
   GradPath grad = GradPath::kSlotRows;
   bool masks = false;     // ordered per-slice pushes read slice bits
   bool upos = false;      // unique-index positions (Backend::remap_pos)
@@ -194,7 +194,10 @@ class Engine {
   int csr_entry_bytes() const {
     return csr_full_rows() ? 4 * csr_row_words(table_.L.P) : (fm_vals_ ? 12 : 8);
   }
-  bool csr_full_rows() const { return cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard; }
+  bool csr_full_rows() const {
+    return (cfg_.model.kind == kFM && cfg_.model.fm_math == kFmStandard) ||
+           (cfg_.model.kind == kMVM && cfg_.model.kernel_dim() >= 2);
+  }
   // worker: forward/backward of every slice of the step at once.  pack:
   // entries packed densely in send order into ent_out (cnt_out: entries per
   // key, u32 [n_send]; totals_out: entries per owner, from the step's owner
@@ -427,7 +430,9 @@ class Engine {
   // reduction and one apply for any slice count
   u32* csr_off_ = nullptr;      // [max_nnz]
   u32* csr_cnt_ = nullptr;      // [max_nnz]
-  float* csr_vent_ = nullptr;   // standard FM: full-row entries [max_nnz][csr_row_words(P)]
+  float* csr_vent_ = nullptr;   // standard FM / MVM: full-row entries [max_nnz][csr_row_words(P)]
+  float* csr_dup_ = nullptr;    // MVM: repeated-field rows' records (CsrOut::dup), same shape
+  u32* csr_dup_n_ = nullptr;
   int64_t csr_steps_ = 0;
   void train_step_csr(const BatchView& b, int S, int slog2);
   u32* csr_doff_ = nullptr;     // [max_nnz + 1] dense offsets (worker pack)

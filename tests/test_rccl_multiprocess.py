@@ -260,7 +260,7 @@ def _csr_worker(rank, world, kind, out_dir):
     np.save(os.path.join(out_dir, f"cb{rank}.npy"), np.array([sh.bytes_moved]))
 
 
-@pytest.mark.parametrize("kind", ["lr", "fm", "fm_std"])
+@pytest.mark.parametrize("kind", ["lr", "fm", "fm_std", "mvm"])
 def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kind):
     """2 processes x 32 768 Criteo-shaped rows x 64 slices each, 3 pipelined
     steps over RCCL with the CSR gradient exchange == one engine trained on
@@ -284,7 +284,7 @@ def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kin
     assert len(np.unique(k)) == len(k) == ref.table_size()
     np.testing.assert_allclose(v, ref.pull(k), rtol=1e-4, atol=1e-6)
     # dense per-slice blocks would move >= n_keys x 64 x width floats per step
-    width = {"lr": 1, "fm": 2, "fm_std": 8}[kind]
+    width = {"lr": 1, "fm": 2, "fm_std": 8, "mvm": 4}[kind]
     dense = CSR_STEPS * len(k) * CSR_S * 4 * width / CSR_W
     for r in range(CSR_W):
         assert np.load(tmp_path / f"cb{r}.npy")[0] < dense / 4

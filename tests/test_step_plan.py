@@ -55,8 +55,8 @@ def test_every_input_picks_one_consistent_layout():
         assert p["rowu"] == (p["mvmu"] or p["fsu"]), tag
         if g == "csr":
             assert S > 1 and csr and not sum_slices and gpu, tag
-            assert (model == "lr" and opt == "ftrl") or model in ("fm_ref", "fm_std"), tag
-            assert p["csr_rows"] == (model == "fm_std"), tag
+            assert (model == "lr" and opt == "ftrl") or model in ("fm_ref", "fm_std", "mvm"), tag
+            assert p["csr_rows"] == (model in ("fm_std", "mvm")), tag
             assert (1 << p["csr_slog2"]) >= S > (1 << p["csr_slog2"]) // 2, tag
             continue
         assert p["csr_slog2"] == -1, tag
@@ -89,7 +89,9 @@ def test_every_input_picks_one_consistent_layout():
     ("fm_std", "sgd", 256, {}, "csr"),
     ("fm_std", "ftrl", 64, {"csr": False}, "unique_rows"),
     ("mvm", "ftrl", 1, {}, "unique_rows"),
-    ("mvm", "ftrl", 8, {}, "slot_rows"),
+    ("mvm", "ftrl", 8, {}, "csr"),
+    ("mvm", "sgd", 256, {}, "csr"),
+    ("mvm", "ftrl", 8, {"csr": False}, "slot_rows"),
     ("lr", "ftrl", 1, {"gpu": False}, "slot_rows"),
 ])
 def test_pinned_layouts(model, opt, S, kw, grad):
