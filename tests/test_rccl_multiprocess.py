@@ -167,10 +167,11 @@ def test_rccl_processes_trainer_equals_cpu_gloo(gpu_device, tmp_path):
 BS_ROWS, BS_STEPS, BS_W = 32768, 5, 4
 
 
-def _bs_batches(rank, dev):
+def _bs_batches(rank, dev, kind="lr"):
     from xflow_amd.data.synth import SynthConfig, SyntheticCriteo
 
-    gen_eng = Engine(ModelConfig(), OptimConfig(),
+    # (an MVM generator engine also fills the field ids MVM needs)
+    gen_eng = Engine(ModelConfig(kind="mvm" if kind == "mvm" else "lr"), OptimConfig(),
                      EngineConfig(table_log2_cap=10, max_rows=BS_ROWS, max_nnz=BS_ROWS * 39),
                      device=dev)
     g = SyntheticCriteo(gen_eng, BS_ROWS, SynthConfig(seed=4242), rank=rank)
@@ -186,7 +187,9 @@ def _bs_engine(dev, rows, log2_cap, slices=1, kind="lr"):
     # ("fm_std": standard-math FM, full-row CSR entries)
     m = (ModelConfig(kind="fm", v_dim=4, fm_math="standard") if kind == "fm_std"
          else ModelConfig(kind=kind, v_dim=4))
-    return Engine(m, OptimConfig(),
+    # (MVM live: SGD from v = 0.9, so the 39-field products stay non-zero)
+    o = OptimConfig(kind="sgd", sgd_v_init=0.9) if kind == "mvm" else OptimConfig()
+    return Engine(m, o,
                   EngineConfig(table_log2_cap=log2_cap, max_rows=rows, max_nnz=rows * 39,
                                max_slices=slices), device=dev)
 
@@ -246,7 +249,7 @@ def _csr_worker(rank, world, kind, out_dir):
     eng = _bs_engine(dev, BS_ROWS, 22, slices=CSR_S, kind=kind)
     sh = ShardedEngine(eng)
     assert sh.transport == "rccl", sh.transport
-    bs = _bs_batches(rank, dev)[:CSR_STEPS]
+    bs = _bs_batches(rank, dev, kind)[:CSR_STEPS]
     for b in bs:
         b.slice_rows = BS_ROWS // CSR_S
     for s in range(CSR_STEPS):
@@ -270,13 +273,15 @@ def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kin
     from xflow_amd.engine import Batch
 
     run_world_gpu(_csr_worker, CSR_W, kind, str(tmp_path))
-    data = [_bs_batches(r, gpu_device)[:CSR_STEPS] for r in range(CSR_W)]
+    data = [_bs_batches(r, gpu_device, kind)[:CSR_STEPS] for r in range(CSR_W)]
     ref = _bs_engine(gpu_device, CSR_W * BS_ROWS, 24, slices=CSR_W * CSR_S, kind=kind)
     for s in range(CSR_STEPS):
         keys = torch.cat([data[r][s].keys.view(39, BS_ROWS) for r in range(CSR_W)],
                          dim=1).reshape(-1)
         lab = torch.cat([data[r][s].labels for r in range(CSR_W)])
-        ref.train_step(Batch(keys=keys.contiguous(), labels=lab, nnz_per_row=39,
+        fg = (torch.cat([data[r][s].fgid.view(39, BS_ROWS) for r in range(CSR_W)], dim=1)
+              .reshape(-1).contiguous() if kind == "mvm" else None)
+        ref.train_step(Batch(keys=keys.contiguous(), labels=lab, fgid=fg, nnz_per_row=39,
                              field_major=True, slice_rows=BS_ROWS // CSR_S))
     assert ref.csr_steps == CSR_STEPS
     k = np.concatenate([np.load(tmp_path / f"ck{r}.npy") for r in range(CSR_W)])
