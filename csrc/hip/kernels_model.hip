@@ -1819,8 +1819,11 @@ __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restric
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
-  // ranks per accumulation chunk: NV int64 each in <= 72 KB of LDS
-  constexpr u32 kR = 1u << ilog2c(72 * 1024 / (8 * NV));
+  // ranks per accumulation chunk: NV int64 each in <= 120 KB of LDS (one
+  // workgroup per CU; a bucket holds ~500-1000 distinct dests, so at 1024
+  // ranks one chunk -- one second pass over the records -- covers it: 512
+  // at MVM-10's NV = 10 took a third pass, 332 vs 213 us for FM-8)
+  constexpr u32 kR = 1u << ilog2c(120 * 1024 / (8 * NV) < 2048 ? 120 * 1024 / (8 * NV) : 2048);
   constexpr u32 kWords = 1u << (kCsrVecWin - 5);
   static_assert(kWords == kRedBlock, "one bitmap word per thread");
   constexpr int kFx = FxBits<1>::kFx;
