@@ -32,6 +32,7 @@ __device__ __forceinline__ int slice_of(const BatchView& b, int64_t r, int S) {
 // Bucket geometry of this step's gradient reduction (FwdArgs::red_bcap):
 // the smallest shift >= base that keeps ceil(dests / 2^shift) within
 // kRedMaxBuckets, dests = (batch scratch capacity) * S.
+constexpr int kCsrVecMinShift = 14;
 struct RedGeom {
   const unsigned long long* bcap;
   u64 cap;
@@ -41,6 +42,10 @@ struct RedGeom {
   const int64_t* nuq;
   int maxb;  // bucket cap (FwdArgs::red_maxb)
   int fx_head;  // scaled fixed point (MVM): fx_head_bits of the batch's rows
+  // smallest bucket shift: the CSR vector reduction (k_red_csr_vec) takes
+  // buckets of 2^kCsrVecMinShift dests -- fewer, fuller buckets amortise its
+  // per-bucket phases, and the producer writes fewer per-bucket counts
+  int min_shift;
   __device__ __forceinline__ u64 rows() const {
     return nuq ? (u64)*nuq : (bcap ? (u64)*bcap : cap);
   }
@@ -54,7 +59,7 @@ struct RedGeom {
     // (FM-8 std --slices 8 -1.2 %, --slices 64 +5.5 %: profiles/r4_negative_ab.txt)
     if (maxb > kRedMaxBuckets && sh - base >= 2)
       while (sh > base && ((dests + (1ull << (sh - 1)) - 1) >> (sh - 1)) <= (u64)maxb) --sh;
-    return sh;
+    return sh < min_shift ? min_shift : sh;
   }
   // buckets this step's dests reach (of the nb allocated for the full
   // capacity): producers, scans and sums skip the rest
@@ -68,7 +73,7 @@ struct RedGeom {
 __host__ __device__ inline RedGeom red_geom(const FwdArgs& a) {
   const int S = a.S;
   return RedGeom{a.red_bcap, a.red_cap, S, a.red_nuq, a.red_maxb > 0 ? a.red_maxb : kRedMaxBuckets,
-                 fx_head_bits(a.batch.rows)};
+                 fx_head_bits(a.batch.rows), a.red_csr.cnt && a.red_csr.ew > 0 ? kCsrVecMinShift : 0};
 }
 
 __device__ __forceinline__ int red_active(const FwdArgs& a, int base) {
@@ -1823,7 +1828,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restric
   // workgroup per CU; a bucket holds ~500-1000 distinct dests, so at 1024
   // ranks one chunk -- one second pass over the records -- covers it: 512
   // at MVM-10's NV = 10 took a third pass, 332 vs 213 us for FM-8)
-  constexpr u32 kR = 1u << ilog2c(120 * 1024 / (8 * NV) < 2048 ? 120 * 1024 / (8 * NV) : 2048);
+  constexpr u32 kR = (120 * 1024 / (8 * NV) < 2048 ? 120 * 1024 / (8 * NV) : 2048) & ~63u;
   constexpr u32 kWords = 1u << (kCsrVecWin - 5);
   static_assert(kWords == kRedBlock, "one bitmap word per thread");
   constexpr int kFx = FxBits<1>::kFx;
