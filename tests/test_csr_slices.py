@@ -1,9 +1,9 @@
 """Many-slice steps at bench scale: 32 768 Criteo-shaped rows x 39 fields per
 step, 64 and 256 Hogwild slices (the reference's default slice count is
 hardware_concurrency, lr_worker.h:40-41; each slice pushes only its own keys,
-lr_worker.cc:162-175).  The GPU runs LR-FTRL and reference-math FM on the CSR
-path (Engine::train_step_csr: one reduction and one apply of the touched
-(key, slice) pairs), standard FM and MVM on slice groups; every model is
+lr_worker.cc:162-175).  The GPU runs every model on the CSR path
+(Engine::train_step_csr: one reduction and one apply of the touched (key,
+slice) pairs; full-row entries for standard FM and MVM); every model is
 checked against the native CPU backend on the same (bit-identical) synthetic
 batches -- the producers' narrow workgroups, widened buckets and multi-window
 CSR buckets included."""
@@ -86,3 +86,32 @@ def test_csr_equals_slice_groups_bitwise(gpu_device, kind, fm_math, slices):
     assert a[0].csr_steps == 3 and b[0].csr_steps == 0
     np.testing.assert_array_equal(a[1], b[1])
     np.testing.assert_array_equal(a[2], b[2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,fm_math", [("lr", "reference"), ("fm", "reference"),
+                                          ("fm", "standard"), ("mvm", "reference")])
+def test_csr_steps_with_empty_and_tiny_batches(gpu_device, kind, fm_math):
+    """A many-slice CSR step of 0 rows (a rank out of data), of fewer rows
+    than slices (empty slices) and of one row per slice all run, leave the
+    table consistent with the CPU backend and change nothing for 0 rows."""
+    from helpers import random_csr, to_batch
+
+    m = ModelConfig(kind=kind, v_dim=4, fm_math=fm_math)
+    o = OptimConfig(kind="sgd", sgd_v_init=0.9) if kind == "mvm" else OptimConfig()
+    engs = [Engine(m, o, EngineConfig(table_log2_cap=12, max_rows=256, max_nnz=256 * 16,
+                                      max_slices=64), device=d)
+            for d in (torch.device("cpu"), gpu_device)]
+    assert engs[1].native.step_plan(64)["grad"] == "csr"
+    allk = []
+    for rows, rps, seed in [(128, 2, 1), (0, 2, 2), (64, 1, 3), (40, 2, 4)]:
+        keys, rp, fg, lab = random_csr(rows, fields=5, vocab=30, seed=seed)
+        allk.append(keys)
+        for e in engs:
+            b = to_batch(keys, rp, fg, lab, e.device, slice_rows=rps)
+            e.train_step(b)
+    k = np.unique(np.concatenate(allk))
+    cpu, gpu = engs[0].pull(k), engs[1].pull(k)
+    assert np.abs(cpu).max() > 0
+    np.testing.assert_allclose(gpu, cpu, rtol=2e-4, atol=1e-6)
+    assert engs[0].table_size() == engs[1].table_size()
