@@ -303,6 +303,8 @@ def main():
                        "parallelism": f"dp{world}+table-shard{world}",
                        "rows_per_gpu": a.batch, "nnz_per_row": synth.fields,
                        "slices": a.slices,
+                       # the gradient layout the step planner picked (plan_step)
+                       "grad_layout": engine.native.step_plan(a.slices)["grad"],
                        "hashed_features": a.features, "table_slots_per_gpu": 2 ** log2_cap,
                        "backend": engine.backend_name,
                        "a2a_transport": sharded.transport if sharded is not None else "none",
