@@ -93,6 +93,9 @@ def parse():
                          "the device's ~470: 7 steps of run-ahead (~3 ms) absorb host "
                          "scheduling hiccups; 2, 7 and 32 measured the same throughput "
                          "(profiles/r3s3_monitor_lag.txt)")
+    ap.add_argument("--csr", choices=["on", "off"], default="on",
+                    help="several slices as CSR gradients (EngineConfig.csr); off: the slice-group "
+                         "layouts (A/B)")
     ap.add_argument("--overlap", choices=["on", "off"], default="off",
                     help="generate batch t+1 on a side stream while step t runs (measured on "
                          "one MI355X: 2-4%% slower for the fused and the multi-rank step, the "
@@ -140,7 +143,8 @@ def main():
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
                                        v_init_scale=a.v_init_scale, sgd_v_init=a.sgd_v_init),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
-                                 max_slices=a.slices, monitor_lag=a.monitor_lag),
+                                 max_slices=a.slices, monitor_lag=a.monitor_lag,
+                                 csr=a.csr == "on"),
                     device=device)
     if a.batch % a.slices:
         raise SystemExit("--batch must be a multiple of --slices")

@@ -523,7 +523,11 @@ StepPlan plan_step(const StepInputs& in, int S) {
   const int vnv = fm_std ? 1 + in.kdim : in.kdim;  // (vector records' NV)
   const bool std_ok = (fm_std || mvm) && in.gpu && in.red_rowv &&
                       std::ceil(in.max_rows / fmstd_block(vnv - 1)) <= kSegMaxGroups;
-  if (in.csr && S > 1 && !in.sum_slices && in.red_pairs && in.remaps &&
+  // below these slice counts the slice-group layouts win (same-box A/B at the
+  // bench batch, profiles/r5_ab.txt #27: LR S = 4 499.8 vs 533.7, standard FM
+  // S = 4 266.2 vs 270.4, MVM S = 2 182.9 vs 273.1; reference FM ties at S = 2)
+  const int csr_min = (in.kind == kLR || fm_std) ? 8 : 4;
+  if (in.csr && S >= csr_min && !in.sum_slices && in.red_pairs && in.remaps &&
       (lr16_slot || in.fm_vals || std_ok)) {
     int sl = 0;
     while ((1 << sl) < S) ++sl;

@@ -55,6 +55,7 @@ def test_every_input_picks_one_consistent_layout():
         assert p["rowu"] == (p["mvmu"] or p["fsu"]), tag
         if g == "csr":
             assert S > 1 and csr and not sum_slices and gpu, tag
+            assert S >= (8 if model in ("lr", "fm_std") else 4), tag  # (the A/B thresholds)
             assert (model == "lr" and opt == "ftrl") or model in ("fm_ref", "fm_std", "mvm"), tag
             assert p["csr_rows"] == (model in ("fm_std", "mvm")), tag
             assert (1 << p["csr_slog2"]) >= S > (1 << p["csr_slog2"]) // 2, tag
@@ -73,8 +74,14 @@ def test_every_input_picks_one_consistent_layout():
 
 @pytest.mark.parametrize("model,opt,S,kw,grad", [
     ("lr", "ftrl", 1, {}, "unique_lr"),                     # the headline step
+    ("lr", "ftrl", 4, {}, "unique_lr"),                     # below CSR's slice threshold
     ("lr", "ftrl", 8, {}, "csr"),
     ("lr", "ftrl", 256, {}, "csr"),
+    ("fm_ref", "ftrl", 2, {}, "unique_fm_bc"),
+    ("fm_ref", "ftrl", 4, {}, "csr"),
+    ("fm_std", "ftrl", 4, {}, "unique_rows"),
+    ("mvm", "ftrl", 2, {}, "slot_rows"),
+    ("mvm", "ftrl", 4, {}, "csr"),
     ("lr", "ftrl", 8, {"csr": False}, "unique_lr"),
     ("lr", "ftrl", 64, {"csr": False}, "unique_lr"),         # slice groups
     ("lr", "ftrl", 8, {"sum_slices": True}, "slot_sums"),
