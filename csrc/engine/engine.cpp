@@ -184,8 +184,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       // MVM: T = loss*M per row; standard FM: (loss, loss*vs) per row (k_fm_std_fwd)
       if (mvm || fm_std) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
       if (mvm) {
-        red_vmax_ = balloc<u32>(be, 2);
-        be.memset(red_vmax_, 0, 2 * sizeof(u32));
+        red_vmax_ = balloc<u32>(be, 4);  // (vmax and dup words, two each)
+        be.memset(red_vmax_, 0, 4 * sizeof(u32));
       }
     }
   }
@@ -342,6 +342,8 @@ void Engine::set_reduction(FwdArgs& fa) const {
   if (red_vmax_) {  // (MVM: two alternating words, see FwdArgs::red_vmax)
     fa.red_vmax = red_vmax_ + vmax_parity_;
     fa.red_vmax_next = red_vmax_ + (vmax_parity_ ^ 1);
+    fa.red_dup = red_vmax_ + 2 + vmax_parity_;
+    fa.red_dup_next = red_vmax_ + 2 + (vmax_parity_ ^ 1);
     vmax_parity_ ^= 1;
   }
   fa.red_bcap = bcap_;

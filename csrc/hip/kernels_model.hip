@@ -1634,7 +1634,8 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
                                                            const float* __restrict__ wpull,
                                                            int S, SegSrc sg,
                                                            u32* __restrict__ masks,
-                                                           const u32* __restrict__ vmax) {
+                                                           const u32* __restrict__ vmax,
+                                                           const u32* __restrict__ dup = nullptr) {
   constexpr int NV = 1 + D;
   constexpr int PS = fm_ps(D);
   constexpr int kShift = red_shift(NV);
@@ -1645,6 +1646,9 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
   __shared__ long long acc[kR * NV];
   // MVM: the step's fixed-point scale (k_fm_std_red kScaled)
   const int fxs = kMvm ? fx_scale_bits(vmax, geom.fx_head) : kFx;
+  // MVM: no repeated-field row added to the rows this step -- they hold the
+  // pull's zeros, so the epilogue stores without reading them
+  const bool rows_zero = kMvm && dup && *dup == 0u;
   __shared__ u32 seen[kR / 32];
   __shared__ u32 s_pre[kSeg ? G : 1];
   __shared__ u32 s_seg[kSeg ? G : 1];
@@ -1728,7 +1732,7 @@ __global__ void __launch_bounds__(kRedBlock) k_red_sum_vec(const void* __restric
         float w[PS], o[PS];
 #pragma unroll
         for (int q = 0; q < PS / 4; ++q) {
-          const float4 a4 = w4[q], b4 = r4[q];
+          const float4 a4 = w4[q], b4 = rows_zero ? make_float4(0.f, 0.f, 0.f, 0.f) : r4[q];
           w[4 * q] = a4.x, w[4 * q + 1] = a4.y, w[4 * q + 2] = a4.z, w[4 * q + 3] = a4.w;
           o[4 * q] = b4.x, o[4 * q + 1] = b4.y, o[4 * q + 2] = b4.z, o[4 * q + 3] = b4.w;
         }
@@ -2067,6 +2071,8 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   if (a.red_maxb > vec_red_max_buckets(D) || (!seg && a.red_maxb > kRedMaxBuckets))
     throw std::runtime_error("vector reduction: bucket cap beyond the producer's");
   const bool split = a.red_rowv != nullptr;
+  // (one slice: the rows' only other writer is k_mvm2's repeated-field atomics)
+  const u32* dup = kMvm && a.S == 1 ? a.red_dup : nullptr;
   if (a.red_csr.cnt) {  // several slices as CSR entries (Engine::train_step_csr)
     if (!seg || !split || a.red_out || !a.red_nuq || a.S != (1 << a.red_csr.slog2) ||
         (kMvm && (!a.red_csr.dup || !a.red_csr.dup_n)) ||
@@ -2112,11 +2118,11 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
       const u32 grid2 = std::min<u32>((u32)(a.red_nb * a.red_nsub), 2u * (u32)device_cus());
       hipLaunchKernelGGL((k_red_sum_vec<D, true, 512, kMvm>), dim3(grid2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax);
+                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax, dup);
     } else {
       hipLaunchKernelGGL((k_red_sum_vec<D, true, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
-                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax);
+                         a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax, dup);
     }
     return;
   }
@@ -2131,7 +2137,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
                      geom);
   hipLaunchKernelGGL((k_red_sum_vec<D, false, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
-                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks, a.red_vmax);
+                     a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks, a.red_vmax, dup);
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
@@ -2586,8 +2592,11 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           if (m > 0.0f) atomicMax(a.red_vmax, __float_as_uint(m));  // (>= 0: bits order as values)
           if (!(m <= 3.0e38f)) atomicOr(a.fx_bad, 2u);  // non-finite T: a diverged model
           if (blockIdx.x == 0) *a.red_vmax_next = 0u;  // (the next step's word)
+          if (blockIdx.x == 0 && a.red_dup_next) *a.red_dup_next = 0u;
         }
       }
+      // (one flag write per wave with a repeated-field row: FwdArgs::red_dup)
+      if (a.red_dup && __ballot(active && dup) && lane_id() == 0) atomicOr(a.red_dup, 1u);
       if (active && dup && a.red_csr.cnt) {
         // (CSR entries: the row's occurrences as dup records, k_csr_dup_add)
         const int ew = a.red_csr.ew;

@@ -224,6 +224,12 @@ struct FwdArgs {
   // alternating words); the vector reduction scales its int64 sums by it
   u32* red_vmax = nullptr;
   u32* red_vmax_next = nullptr;
+  // MVM: set (non-zero) by the forward when a row with a repeated field added
+  // its gradients to the rows by atomics; cleared for the next step like
+  // red_vmax_next.  With it zero the reduction's epilogue stores its rows
+  // without reading them back (they hold the pull's zeros)
+  u32* red_dup = nullptr;
+  u32* red_dup_next = nullptr;
   int red_nsub = 1;
   // producer workgroups the reduction buffers hold (red_hist rows, red_count);
   // 0: the model's fixed rows per workgroup.  A smaller batch (a slice group

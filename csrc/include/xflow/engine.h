@@ -523,7 +523,7 @@ class Engine {
   double monitor_wait_s_ = 0.0;
   float* grp_nz_ = nullptr;                   // FM / MVM FTRL: the pull's (n, z) stash [unique][P]
   unsigned long long* rec_count_ = nullptr;  // (count_records) device counter
-  u32* red_vmax_ = nullptr;                   // MVM: per-step fixed-point scale words [2]
+  u32* red_vmax_ = nullptr;                   // MVM: per-step scale words [2], dup words [2]
   u32* text_ws_ = nullptr;                    // parse_text workspace
   int64_t text_ws_words_ = 0;
   long long* text_counts_ = nullptr;          // parse_text counts [7]
