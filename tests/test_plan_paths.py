@@ -80,3 +80,31 @@ def test_cpu_backend_same_weights_as_reference(case):
     plan, got, want = _run(torch.device("cpu"), *args)
     assert plan["grad"] == "slot_rows"
     np.testing.assert_allclose(got, want, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_mvm_batches_alternating_repeated_fields_gpu(gpu_device):
+    """One-slice MVM steps whose batches alternate between rows with a repeated
+    field (their gradients reach the unique-order rows by atomics, and the step
+    raises FwdArgs::red_dup) and none (the reduction then stores its rows
+    without reading them): the same table as the CPU backend, whose MVM is
+    checked against torch_ref above.  The flag words alternate per step, so
+    the pattern dup, none, none, dup, dup, none covers a flag left over from
+    either parity."""
+    m = ModelConfig(kind="mvm", v_dim=4)
+    o = OptimConfig(kind="sgd", sgd_v_init=0.9)
+    engs = [Engine(m, o, EngineConfig(table_log2_cap=12, max_rows=256, max_nnz=256 * 16),
+                   device=d) for d in (torch.device("cpu"), gpu_device)]
+    assert engs[1].native.step_plan(1)["grad"] == "unique_rows"
+    allk = []
+    for step, variable in enumerate([True, False, False, True, True, False]):
+        keys, rp, fg, lab = random_csr(200, fields=5, vocab=30, seed=70 + step, variable=variable)
+        dups = sum(len(set(fg[rp[r]:rp[r + 1]])) < rp[r + 1] - rp[r] for r in range(200))
+        assert (dups > 0) == variable
+        allk.append(keys)
+        for e in engs:
+            e.train_step(to_batch(keys, rp, fg, lab, e.device))
+    k = np.unique(np.concatenate(allk))
+    cpu, gpu = engs[0].pull(k), engs[1].pull(k)
+    assert np.abs(cpu).max() > 0
+    np.testing.assert_allclose(gpu, cpu, rtol=2e-4, atol=1e-6)
