@@ -904,7 +904,10 @@ void Engine::train_step(const BatchView& b) {
     pa.zero_out = fm_grad_;
     pa.zero_width = 2;
   }
-  if (rowu) {
+  // (one-slice standard FM: every unique key's row is written by the
+  // reduction -- each occurrence leaves a record, k_fm_std_red -- so the
+  // pull need not zero them)
+  if (rowu && !(fsu && P.Sf == 1)) {
     pa.zero_out = row_grad_;
     pa.zero_width = ps;
   }

@@ -1405,9 +1405,11 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   const u32 S = (u32)a.S;
   const u32 sl = active ? (u32)slice_of(b, r, a.S) : 0u;
   // kSplit: the row's vector (FM: loss, loss*vs_k; MVM: T_k = loss*M_k); a
-  // one-slice step emits nothing for an all-zero one (a zero contribution --
-  // every unique key is pushed anyway), several slices need every occurrence
-  // (the records' presence gives the slice bits)
+  // one-slice MVM step emits nothing for an all-zero one (a zero contribution
+  // -- every unique key is pushed anyway), several slices need every
+  // occurrence (the records' presence gives the slice bits), and so does
+  // standard FM: every unique key then has a record and the reduction writes
+  // every unique-order row (the pull does not zero them, Engine::train_step)
   float t[PS];
   bool live = active;
   if (kSplit && active) {
@@ -1423,7 +1425,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     bool nz = false;
 #pragma unroll
     for (int c = 0; c < NV; ++c) nz |= t[c] != 0.0f;
-    live = nz || S > 1u;
+    live = nz || S > 1u || !kScaled;
   }
   if constexpr (kSeg) {
     // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (the cursors)
