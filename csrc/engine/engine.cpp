@@ -759,7 +759,7 @@ void Engine::w_forward_backward_csr(const BatchView& b, const float* pulled, int
 
 void Engine::s_apply_csr(const u64* recv_keys, const u32* recv_cnt, const void* recv_ent,
                          const std::vector<int64_t>& src_offsets, int S, int buf) {
-  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, 8)");
+  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, kSrvBufs)");
   SrvBuf& sb = srv_[buf];
   sb.keys = nullptr;  // applied: no slot remap needed after a growth
   bool stash = sb.nz_fresh;
@@ -1190,7 +1190,7 @@ void Engine::w_prepare(const BatchView& b, int world, int64_t* counts_out, u64* 
 }
 
 void Engine::ensure_server_capacity(int64_t n, int buf) {
-  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, 8)");
+  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, kSrvBufs)");
   SrvBuf& sb = srv_[buf];
   if (n <= sb.cap) return;
   be_->synchronize();
@@ -1422,7 +1422,7 @@ void Engine::w_forward_backward(const BatchView& b, const float* pulled, int64_t
 
 void Engine::s_apply(const u64* recv_keys, const float* recv_grads, const u32* recv_masks,
                      const std::vector<int64_t>& src_offsets, int S, int buf) {
-  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, 8)");
+  if (buf < 0 || buf >= kSrvBufs) throw std::invalid_argument("server buffer must be in [0, kSrvBufs)");
   SrvBuf& sb = srv_[buf];
   sb.keys = nullptr;  // applied: no slot remap needed after a growth
   const int ps = pstride();

@@ -188,6 +188,7 @@ class HipBackend final : public Backend {
   // its default current stream.
   void set_stream(void* s) override { stream_ = reinterpret_cast<hipStream_t>(s); }
   void* stream() const override { return stream_; }
+  void bind_thread() override { XF_HIP_CHECK(hipSetDevice(device_)); }
 
   void table_clear(const TableView& t) override { hip::launch_table_clear(t, stream_); }
   void dedup(const u64* keys, int64_t nnz, ScratchView s, DedupOut o) override {

@@ -568,6 +568,9 @@ class Backend {
   virtual void synchronize() = 0;
   virtual void set_stream(void* stream) = 0;
   virtual void* stream() const = 0;
+  // make this backend's device current on the calling thread (a second host
+  // thread driving the backend: the async parameter server's server thread)
+  virtual void bind_thread() {}
   // Bytes of device memory still free (table growth checks it first).
   virtual size_t free_memory() const { return ~(size_t)0; }
   // Write a capacity snapshot {mon: size u64, overflow[2]} with sequence seq

@@ -473,7 +473,8 @@ class Engine {
   // Server buffers: a pipelined step with staleness k applies a buffer's
   // pushes after the next k pulls (parallel/async_p2p.py), so k + 1 are live.
  public:
-  static constexpr int kSrvBufs = 8;
+  // (the asynchronous parameter server keeps one per (source, ring slot))
+  static constexpr int kSrvBufs = 64;
  private:
   struct SrvBuf {
     u32* slots = nullptr;        // table slot of each received key (s_pull)

@@ -17,6 +17,7 @@
 #include <vector>
 #include <string>
 
+#include "../comm/async_ps.h"
 #include "../comm/rccl_comm.h"
 #include "../comm/sharded_step.h"
 #include "xflow/engine.h"
@@ -326,6 +327,62 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def_readonly("last_send", &ShardedStep::last_send)
       .def_readonly("last_recv", &ShardedStep::last_recv);
 
+  py::class_<AsyncPS>(m, "AsyncPS")
+      .def(py::init([](Engine& worker, Engine& server, int world, int rank, int staleness,
+                       int slices, std::string name, double timeout_s, int slow_ms,
+                       double pair_frac, int device) {
+             AsyncPS::Config c;
+             c.world = world;
+             c.rank = rank;
+             c.staleness = staleness;
+             c.slices = slices;
+             c.name = name;
+             c.timeout_s = timeout_s;
+             c.slow_ms = slow_ms;
+             c.pair_frac = pair_frac;
+             c.device = device;
+             return new AsyncPS(worker, server, c);
+           }),
+           py::arg("worker"), py::arg("server"), py::arg("world"), py::arg("rank"),
+           py::arg("staleness"), py::arg("slices"), py::arg("name"), py::arg("timeout_s") = 600.0,
+           py::arg("slow_ms") = 0, py::arg("pair_frac") = 1.0, py::arg("device") = -1,
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>())
+      .def("handle",
+           [](const AsyncPS& a) {
+             auto v = a.handle();
+             return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+           })
+      .def("connect",
+           [](AsyncPS& a, std::vector<py::bytes> hs) {
+             std::vector<std::vector<uint8_t>> v;
+             for (auto& h : hs) {
+               std::string s = h;
+               v.emplace_back(s.begin(), s.end());
+             }
+             a.connect(v);
+           })
+      .def("start", &AsyncPS::start)
+      .def("train_step", &AsyncPS::train_step, py::call_guard<py::gil_scoped_release>())
+      .def("eval_step",
+           [](AsyncPS& a, const BatchView& b, uintptr_t pctr) { return a.eval_step(b, P<float>(pctr)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("finish", &AsyncPS::finish, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &AsyncPS::stop, py::call_guard<py::gil_scoped_release>())
+      .def("log", [](const AsyncPS& a) { return to_np(a.log()); })
+      .def_property_readonly("transport", &AsyncPS::transport)
+      .def_property_readonly("csr", &AsyncPS::csr)
+      .def_readonly("steps", &AsyncPS::steps)
+      .def_readonly("evals", &AsyncPS::evals)
+      .def_readwrite("bytes_moved", &AsyncPS::bytes_moved)
+      .def_readwrite("max_staleness", &AsyncPS::max_staleness)
+      .def_readwrite("max_lead", &AsyncPS::max_lead)
+      .def_readwrite("wait_slot_s", &AsyncPS::wait_slot_s)
+      .def_readwrite("wait_pull_s", &AsyncPS::wait_pull_s)
+      .def_readwrite("sync_s", &AsyncPS::sync_s)
+      .def_readonly("served_pulls", &AsyncPS::served_pulls)
+      .def_readonly("applied_pushes", &AsyncPS::applied_pushes)
+      .def_readonly("server_busy_s", &AsyncPS::server_busy_s);
+
   py::class_<Engine>(m, "Engine")
       .def(py::init([](py::dict model, py::dict opt, int table_log2_cap, int64_t max_rows,
                        int64_t max_nnz, int max_slices, bool sum_slices, double scratch_factor,
@@ -483,6 +540,27 @@ PYBIND11_MODULE(_xflow_native, m) {
            },
            py::arg("keys"), py::arg("grads"), py::arg("masks"), py::arg("offsets"), py::arg("S"),
            py::arg("buf") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("w_forward_backward_csr",
+           [](Engine& e, const BatchView& b, uintptr_t pulled, int64_t n_send, int S, int wb,
+              uintptr_t cnt, uintptr_t ent, uintptr_t counts, int world, uintptr_t totals) {
+             e.w_forward_backward_csr(b, P<const float>(pulled), n_send, S, wb, true, P<u32>(cnt),
+                                      P<void>(ent), P<const int64_t>(counts), world, false,
+                                      P<int64_t>(totals));
+           },
+           py::arg("batch"), py::arg("pulled"), py::arg("n_send"), py::arg("S"), py::arg("wb"),
+           py::arg("cnt"), py::arg("ent"), py::arg("counts"), py::arg("world"), py::arg("totals"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("s_apply_csr",
+           [](Engine& e, uintptr_t keys, uintptr_t cnt, uintptr_t ent, std::vector<int64_t> offsets,
+              int S, int buf) {
+             e.s_apply_csr(P<const u64>(keys), P<const u32>(cnt), P<const void>(ent), offsets, S, buf);
+           },
+           py::arg("keys"), py::arg("cnt"), py::arg("ent"), py::arg("offsets"), py::arg("S"),
+           py::arg("buf") = 0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("csr_entry_bytes", &Engine::csr_entry_bytes)
+      .def("csr_exchange", [](Engine& e, int S) {
+        return e.csr_slog2(S) >= 0 && e.backend().csr_exchange();
+      })
       .def("w_finish", &Engine::w_finish, py::call_guard<py::gil_scoped_release>())
       .def("field_major",
            [](Engine& e, uintptr_t src, uintptr_t dst, int64_t rows, int F, int elem_bytes,

@@ -80,7 +80,7 @@ def _compile_cmd(src: str) -> list[str]:
     out = _obj_path(src)
     if src.endswith(".hip"):
         return [HIPCC, "-c", src, "-o", out] + COMMON_FLAGS + HIP_FLAGS
-    if src.endswith("rccl_comm.cpp"):  # host code against the HIP runtime + RCCL
+    if src.endswith(("rccl_comm.cpp", "peer_window.cpp")):  # host code against the HIP runtime
         return [HIPCC, "-c", src, "-o", out] + COMMON_FLAGS
     flags = list(COMMON_FLAGS)
     if src.endswith("module.cpp"):
@@ -101,9 +101,10 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
     mod_src = os.path.join(CSRC, "python", "module.cpp")
     comm_src = os.path.join(CSRC, "comm", "rccl_comm.cpp")
     step_src = os.path.join(CSRC, "comm", "sharded_step.cpp")
+    aps_srcs = [os.path.join(CSRC, "comm", f) for f in ("async_ps.cpp", "peer_window.cpp")]
     capi_src = os.path.join(CSRC, "capi", "c_api.cpp")
     cli_src = os.path.join(CSRC, "tools", "xflow_lr.cpp")
-    all_srcs = hip_srcs + host_srcs + [mod_src, comm_src, step_src, capi_src, cli_src]
+    all_srcs = hip_srcs + host_srcs + [mod_src, comm_src, step_src, capi_src, cli_src] + aps_srcs
     todo = [s for s in all_srcs if force or _stale(_obj_path(s), [s], hdr)]
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
@@ -129,10 +130,11 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
         torch_lib = None
     rpaths = ([torch_lib] if torch_lib else []) + [rocm_lib]
     mod_out = native_module_path()
-    mod_objs = core_objs + [_obj_path(mod_src), _obj_path(comm_src), _obj_path(step_src)]
+    mod_objs = core_objs + [_obj_path(mod_src), _obj_path(comm_src), _obj_path(step_src)] + \
+        [_obj_path(s) for s in aps_srcs]
     if force or _stale(mod_out, mod_objs, 0.0):
         # librccl.so.1 resolves to the RCCL torch has already loaded (same SONAME)
-        _run(link + mod_objs + ["-o", mod_out, "-L" + rocm_lib, "-lrccl"] +
+        _run(link + mod_objs + ["-o", mod_out, "-L" + rocm_lib, "-lrccl", "-lrt"] +
              [f"-Wl,-rpath,{p}" for p in rpaths], verbose)
     products["module"] = mod_out
 

@@ -9,6 +9,11 @@
 * Fault injection for tests, from the environment (never set in production):
     XFLOW_FAULT=kill:<rank>:<step>      rank exits abruptly before that step
     XFLOW_FAULT=hang:<rank>:<step>      rank stops making progress (sleeps)
+    XFLOW_FAULT=slow_rank:<rank>:<ms>   rank sleeps <ms> before EVERY training step (a
+                                        straggler: the asynchronous parameter server's
+                                        other workers must keep their pace,
+                                        parallel/async_ps.py; the lock-step step
+                                        slows every rank to it)
     XFLOW_FAULT=drop_a2a:<rank>:<step>  rank skips one exchange of that step.  On
                                         the gloo / loopback transports its peers
                                         detect the out-of-step counts at the next
@@ -69,13 +74,19 @@ def watchdog_from_env(name: str = "xflow") -> Optional[Watchdog]:
 class FaultInjector:
     def __init__(self, spec: Optional[str], rank: int):
         self.kind = None
+        self.slow_ms = 0
         if spec:
             kind, r, step = spec.split(":")
             if int(r) == rank:
                 self.kind, self.step = kind, int(step)
+                if kind == "slow_rank":
+                    self.slow_ms = int(step)
 
     def before_step(self, step: int) -> bool:
         """Returns False when this rank must skip an exchange of the step."""
+        if self.kind == "slow_rank":
+            time.sleep(self.slow_ms / 1000.0)
+            return True
         if self.kind is None or step != self.step:
             return True
         if self.kind == "kill":
@@ -89,3 +100,8 @@ class FaultInjector:
 
 def injector_from_env(rank: int) -> FaultInjector:
     return FaultInjector(os.environ.get("XFLOW_FAULT"), rank)
+
+
+def slow_ms_from_env(rank: int) -> int:
+    """XFLOW_FAULT=slow_rank:<rank>:<ms>: this rank's per-step sleep (0: none)."""
+    return FaultInjector(os.environ.get("XFLOW_FAULT"), rank).slow_ms
