@@ -65,10 +65,20 @@ def parse():
     ap.add_argument("--cpu", action="store_true", help="CPU backend (smoke only)")
     ap.add_argument("--sharded", action="store_true",
                     help="force the multi-rank (all-to-all) step even at 1 GPU (overhead probe)")
-    ap.add_argument("--async", dest="async_p2p", action="store_true",
-                    help="config 4: bounded-staleness steps, pushes over RCCL send/recv riding in "
-                         "the next step's key exchange")
-    ap.add_argument("--staleness", type=int, default=1, help="--async: staleness in steps")
+    ap.add_argument("--async", dest="async_ps", action="store_true",
+                    help="config 4: the asynchronous parameter server (parallel/async_ps.py) -- "
+                         "every rank a server thread + a worker that never lock-steps with the "
+                         "others; keys, values and CSR gradient entries through HIP-IPC windows "
+                         "in peer HBM, no collective inside training.  Each rank times its own "
+                         "steps; value = total samples / the slowest rank's time")
+    ap.add_argument("--async-lockstep", dest="async_p2p", action="store_true",
+                    help="the lock-step staleness-k step (pushes over RCCL riding in the next "
+                         "step's key exchange; every rank in every group call)")
+    ap.add_argument("--staleness", type=int, default=1,
+                    help="--async / --async-lockstep: staleness in steps")
+    ap.add_argument("--pair-frac", type=float, default=1.0,
+                    help="--async: inbox capacity per (source, owner) as a fraction of a step's "
+                         "occurrences (1: any key skew fits)")
     ap.add_argument("--sgd-v-init", type=float, default=1e-3,
                     help="SGD latent init (sgd.h:69: the constant 0.001); MVM-SGD with 1.0 keeps "
                          "the field product live (FTRL's first push shrinks v by ~|g|)")
@@ -103,6 +113,123 @@ def parse():
     return ap.parse_args()
 
 
+def run_async(a, world, rank, device, use_gpu, shared_gpu, synth, log2_cap, nnz):
+    """--async: BASELINE config 4 on the asynchronous parameter server.  Every
+    rank warms up, meets the others at one barrier, then runs its --steps
+    without any further meeting; its time ends when its own last pushes are
+    applied.  A straggler (XFLOW_FAULT=slow_rank:<r>:<ms>) slows only itself:
+    the per-rank rates in the JSON show it."""
+    from xflow_amd.parallel.async_ps import AsyncParameterServer
+
+    model = ModelConfig(kind=a.model, v_dim=a.v_dim, fm_math=a.fm_math, fm_mfma=a.fm_mfma)
+    optim = OptimConfig(kind=a.optimizer, lambda1=a.lambda1, v_init_scale=a.v_init_scale,
+                        sgd_v_init=a.sgd_v_init)
+    cfg = EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
+                       max_slices=a.slices, monitor_lag=a.monitor_lag, csr=a.csr == "on")
+    aps = AsyncParameterServer(model, optim, cfg, device, staleness=a.staleness,
+                               slices=a.slices, pair_frac=a.pair_frac, start=False)
+    if a.table_load < 0:
+        n_prefill = a.features // world if use_gpu else 0
+    else:
+        n_prefill = int(a.table_load * 2 ** log2_cap)
+    n_prefill = min(n_prefill, int(0.9 * 2 ** log2_cap))
+    # (the server thread owns the table: prefill before it serves anything)
+    if n_prefill > 0:
+        aps.server.native.prefill(n_prefill, 0x5eed + rank)
+        aps.server.synchronize()
+    prefilled = aps.server.native.table_size()
+    aps.start()
+    gen = SyntheticCriteo(aps.worker, a.batch, synth, rank=rank, slice_rows=a.batch // a.slices)
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize(device)
+
+    for _ in range(a.warmup):
+        aps.train_step(gen.next())
+    sync()
+    aps.native.finish()
+    dist.barrier() if world > 1 else None
+    aps.worker.read_stats(reset=True)
+    p = aps.native
+    s0 = (p.steps, p.bytes_moved, p.wait_slot_s, p.wait_pull_s, p.sync_s)
+    p.max_staleness = 0
+    p.max_lead = 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        aps.train_step(gen.next())
+    aps.native.finish()  # this rank's last pushes applied: part of its timed work
+    sync()
+    elapsed = time.perf_counter() - t0
+    st = aps.worker.read_stats(reset=True)
+    mine = {"rank": rank, "elapsed_s": round(elapsed, 6),
+            "steps_per_s": round(a.steps / elapsed, 3),
+            "wait_slot_ms_per_step": round(1e3 * (p.wait_slot_s - s0[2]) / a.steps, 4),
+            "wait_pull_ms_per_step": round(1e3 * (p.wait_pull_s - s0[3]) / a.steps, 4),
+            "host_sync_ms_per_step": round(1e3 * (p.sync_s - s0[4]) / a.steps, 4),
+            "bytes_moved_per_step": int((p.bytes_moved - s0[1]) // a.steps),
+            "max_staleness": int(p.max_staleness), "max_lead": int(p.max_lead),
+            "slow_ms": aps.slow_ms, "ln_loss": st["ln_loss"], "rows": st["rows"]}
+    aps.close()  # barrier: every worker done; the server threads exit
+    tbl = aps.server.native.table_size()
+    nnzw = aps.server.nonzero_weights()
+    ovf = float(aps.server.overflowed() or aps.worker.overflowed())
+    mine.update(table_keys=int(tbl), nonzero=int(nnzw), ovf=ovf, prefilled=int(prefilled),
+                served_pulls=int(p.served_pulls), applied_pushes=int(p.applied_pushes))
+    if world > 1:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+    if any(r["ovf"] > 0 for r in allr):
+        raise SystemExit("bench: a table or dedup-scratch overflow was flagged: the result is invalid")
+    slowest = max(r["elapsed_s"] for r in allr)
+    samples = a.batch * a.steps * world
+    rows = sum(r["rows"] for r in allr)
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": samples / slowest,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": 1000.0 * slowest / a.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic Criteo-1TB-shaped (%d fields, 1e9 hashed features, planted-logistic "
+                    "labels); table prefilled (untimed) with %d keys no batch touches" % (
+                        synth.fields, sum(r["prefilled"] for r in allr)),
+            "config": {"model": f"{a.model.upper()}-{a.optimizer.upper()}",
+                       "global_batch": a.batch * world, "seq_len": synth.fields,
+                       "parallelism": f"dp{world}+table-shard{world}+async-ps(staleness={a.staleness})",
+                       "rows_per_gpu": a.batch, "nnz_per_row": synth.fields, "slices": a.slices,
+                       "grad_exchange": "csr" if aps.csr else "dense",
+                       "hashed_features": a.features, "table_slots_per_gpu": 2 ** log2_cap,
+                       "backend": aps.server.backend_name, "a2a_transport": aps.transport,
+                       "lambda1": a.lambda1},
+            **({"shared_gpu_rehearsal": True} if shared_gpu else {}),
+            "logloss": sum(r["ln_loss"] for r in allr) / max(rows, 1.0),
+            "table_keys": sum(r["table_keys"] for r in allr),
+            "nonzero_weights": sum(r["nonzero"] for r in allr),
+            "prefilled_keys": sum(r["prefilled"] for r in allr),
+            "table_load": sum(r["table_keys"] for r in allr) / float(world * 2 ** log2_cap),
+            # per-rank: each rank's own rate -- a straggler slows only itself
+            "per_rank": [{k: r[k] for k in ("rank", "steps_per_s", "elapsed_s", "slow_ms",
+                                            "max_staleness", "max_lead", "wait_slot_ms_per_step",
+                                            "wait_pull_ms_per_step", "host_sync_ms_per_step",
+                                            "bytes_moved_per_step")} for r in allr],
+            "bytes_moved_per_step": int(sum(r["bytes_moved_per_step"] for r in allr) / world),
+            "max_staleness": max(r["max_staleness"] for r in allr),
+            "staleness_bound": a.staleness,
+        }
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,7 +252,11 @@ def main():
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world > 1 or a.sharded or a.async_p2p:
+    if a.async_ps and world > 1:
+        # the asynchronous parameter server needs no collective transport:
+        # gloo carries only its start / end handshake
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    elif world > 1 or a.sharded or a.async_p2p:
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
@@ -139,6 +270,10 @@ def main():
     synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed,
                         n_fields=a.fields)
     nnz = a.batch * synth.fields
+    if a.batch % a.slices:
+        raise SystemExit("--batch must be a multiple of --slices")
+    if a.async_ps:
+        return run_async(a, world, rank, device, use_gpu, shared_gpu, synth, log2_cap, nnz)
     model = ModelConfig(kind=a.model, v_dim=a.v_dim, fm_math=a.fm_math, fm_mfma=a.fm_mfma)
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
                                        v_init_scale=a.v_init_scale, sgd_v_init=a.sgd_v_init),

@@ -60,3 +60,27 @@ def run_world_gpu(fn, world: int, *args) -> None:
     real RCCL (socket transport between per-rank host ids): the multi-process
     GPU path on a 1-GPU box."""
     mp.spawn(_entry_gpu, args=(world, free_port(), fn, args), nprocs=world, join=True)
+
+
+def _entry_gpu_gloo(rank, world, port, fn, args):
+    """Rank entry of run_world_gpu_gloo: every rank on GPU 0, gloo for the
+    process group (the asynchronous parameter server needs no collective
+    transport: only its handshake uses the group)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world, *args)
+        torch.cuda.synchronize(dev)
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_world_gpu_gloo(fn, world: int, *args) -> None:
+    mp.spawn(_entry_gpu_gloo, args=(world, free_port(), fn, args), nprocs=world, join=True)

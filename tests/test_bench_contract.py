@@ -39,7 +39,8 @@ def _run(n, extra, cpu=True, env_extra=None):
 
 
 @pytest.mark.parametrize("n,extra", [(1, []), (2, []), (2, ["--model", "fm", "--v-dim", "8"]),
-                                     (2, ["--async"]), (2, ["--slices", "4"])])
+                                     (2, ["--async"]), (2, ["--async-lockstep"]),
+                                     (2, ["--slices", "4"])])
 def test_bench_json_line(n, extra):
     d = _run(n, extra)
     assert KEYS <= set(d)
@@ -55,7 +56,7 @@ def test_bench_json_line(n, extra):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra", [[], ["--sharded"], ["--async"], ["--slices", "8"],
+@pytest.mark.parametrize("extra", [[], ["--sharded"], ["--async"], ["--async-lockstep"], ["--slices", "8"],
                                    ["--model", "fm", "--v-dim", "8"], ["--model", "mvm", "--v-dim", "10"]])
 def test_bench_json_line_on_gpu(gpu_device, extra):
     """The benchmark variants on the HIP backend (1 GPU, prefilled table):
@@ -69,7 +70,8 @@ def test_bench_json_line_on_gpu(gpu_device, extra):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,extra", [(2, []), (2, ["--async"]), (3, ["--model", "fm", "--v-dim", "8"])])
+@pytest.mark.parametrize("n,extra", [(2, []), (2, ["--async"]), (2, ["--async", "--slices", "64"]),
+                                     (3, ["--model", "fm", "--v-dim", "8"])])
 def test_bench_multirank_rccl_on_one_gpu(gpu_device, n, extra):
     """The driver's multi-GPU launch (torch.distributed.run, one process per
     rank, RCCL) with every rank on this box's GPU 0 (XFLOW_SHARED_GPU=1:
@@ -80,8 +82,10 @@ def test_bench_multirank_rccl_on_one_gpu(gpu_device, n, extra):
              cpu=False, env_extra={"XFLOW_SHARED_GPU": "1"})
     assert KEYS <= set(d)
     assert d["n_gpus"] == n and d["shared_gpu_rehearsal"] is True
-    assert d["config"]["a2a_transport"] == "rccl"
+    assert d["config"]["a2a_transport"] == ("ipc" if "--async" in extra else "rccl")
     assert d["config"]["global_batch"] == 16384 * n
     if "--async" not in extra:
         assert d["early_key_exchanges"] >= d["steps"]
+    else:  # one rate per rank, each its own
+        assert len(d["per_rank"]) == n and d["max_staleness"] <= d["staleness_bound"]
     assert 0.0 < d["logloss"] < 1.0 and d["table_keys"] > 0

@@ -77,7 +77,9 @@ class AsyncParameterServer:
                  device: str | torch.device = "cpu", staleness: int = 1, slices: int = 1,
                  group: Optional[dist.ProcessGroup] = None, pair_frac: float = 1.0,
                  timeout_s: Optional[float] = None, name: Optional[str] = None,
-                 slow_ms: Optional[int] = None):
+                 slow_ms: Optional[int] = None, start: bool = True):
+        """start=False: call ``start()`` later (e.g. after preparing the
+        server's table shard, which nothing may touch once it serves)."""
         self.group = group
         on = dist.is_initialized()
         self.world = dist.get_world_size(group) if on else 1
@@ -109,16 +111,26 @@ class AsyncParameterServer:
                                          self.rank, self.staleness, self.slices, name,
                                          timeout_s=timeout, slow_ms=self.slow_ms,
                                          pair_frac=float(pair_frac), device=dev)
+        self.closed = False
+        self.started = False
+        if start:
+            self.start()
+
+    def start(self) -> None:
+        """Handshake (every rank maps every window), barrier, start the server
+        thread.  Collective."""
+        if self.started:
+            return
         h = self._ps.handle()
         if self.world > 1:
             hs = [None] * self.world
-            dist.all_gather_object(hs, h, group=group)
+            dist.all_gather_object(hs, h, group=self.group)
         else:
             hs = [h]
         self._ps.connect(hs)
         self._barrier()
         self._ps.start()
-        self.closed = False
+        self.started = True
 
     def _barrier(self) -> None:
         if self.world > 1:
