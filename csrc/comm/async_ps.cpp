@@ -139,6 +139,11 @@ AsyncPS::AsyncPS(Engine& worker, Engine& server, const Config& c)
   cnt_d_ = static_cast<u32*>(be.alloc(sizeof(u32) * (size_t)nnz));
   pay_d_ = be.alloc(csr_ ? (size_t)eb_ * nnz : 4 * (size_t)S * gw_ * nnz);
   wev_ = be.event_create();
+  srv_stream_ = sv_.backend().stream();
+  served_.assign(W_, -1);
+  applied_.assign(W_, -1);
+  kind_.assign((size_t)W_ * R_, 0);
+  nkeys_.assign((size_t)W_ * R_, 0);
 }
 
 AsyncPS::~AsyncPS() {
@@ -174,6 +179,10 @@ void AsyncPS::connect(const std::vector<std::vector<uint8_t>>& handles) {
 void AsyncPS::start() {
   if (!connected_) throw std::logic_error("AsyncPS: connect() before start()");
   if (running_.load()) return;
+  check_abort();
+  // (the caller may have used the server engine on its own stream meanwhile)
+  sv_.backend().set_stream(srv_stream_);
+  stop_.store(false);
   running_.store(true);
   thr_ = std::thread([this] { server_loop(); });
 }
@@ -271,6 +280,8 @@ bool AsyncPS::step(const BatchView& b, float* pctr, bool train) {
   const int slot = (int)(t % R_);
   Ctl& k = *ctl_;
   Backend& be = wk_.backend();
+  if (train && __atomic_load_n(&k.prog_c(me).a, __ATOMIC_RELAXED))
+    __atomic_store_n(&k.prog_c(me).a, 0, __ATOMIC_RELEASE);  // (training again after finish)
   // 1. bounded staleness / slot reuse: every owner applied (or retired) step t - R
   wait_until(
       [&] {
@@ -404,9 +415,10 @@ void AsyncPS::server_loop() {
     be.bind_thread();
     const int me = c_.rank, S = c_.slices;
     Ctl& k = *ctl_;
-    std::vector<int64_t> served(W_, -1), applied(W_, -1);
-    std::vector<int> kind((size_t)W_ * R_, 0);
-    std::vector<int64_t> nkeys((size_t)W_ * R_, 0);
+    std::vector<int64_t>& served = served_;
+    std::vector<int64_t>& applied = applied_;
+    std::vector<int>& kind = kind_;
+    std::vector<int64_t>& nkeys = nkeys_;
     struct Pend {
       void* ev;
       bool resp;

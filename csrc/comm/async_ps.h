@@ -78,8 +78,11 @@ class AsyncPS {
   bool eval_step(const BatchView& b, float* pctr);
   // worker: wait until every push of this worker is applied; mark it done
   void finish();
-  // server: exit the thread (every rank finished: the caller's barrier)
+  // server: exit the thread (every rank finished: the caller's barrier).
+  // start() again resumes serving where it stopped (e.g. after an epoch's
+  // statistics / checkpoint, which read the server engine from the caller)
   void stop();
+  bool serving() const { return running_.load(); }
 
   // (kind, source, step, count) per owner operation in stream order:
   // kind 0 pull (count keys), 1 push (count entries / keys), 2 eval pull
@@ -133,7 +136,13 @@ class AsyncPS {
   u32* cnt_d_ = nullptr;
   void* pay_d_ = nullptr;
   void* wev_ = nullptr;
-  // server state
+  // server state (kept across stop / start): per source the last step
+  // whose pull was served / whose push was applied, and per (source, slot)
+  // the request kind and key count
+  std::vector<int64_t> served_, applied_;
+  std::vector<int> kind_;
+  std::vector<int64_t> nkeys_;
+  void* srv_stream_ = nullptr;  // the server engine's stream at construction (restored by start)
   std::thread thr_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> running_{false};

@@ -261,7 +261,14 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
   const std::vector<int64_t> offsets = offsets_of(sp.recv);
   const int ngroups = Engine::slice_groups(S);
   float* vals = static_cast<float*>(get(vals_, sizeof(float) * (size_t)(n_recv * ps)));
-  e_.s_pull(recv_keys, n_recv, vals, true, 0, offsets, ngroups > 1);
+  // the CSR exchange applies source by source (s_apply_csr): no owner
+  // grouping, and compact FM rows of a later source expand with the pulled
+  // weights, not the table's (the earlier sources updated it)
+  const bool csr = e_.csr_slog2(S) >= 0 && e_.backend().csr_exchange();
+  if (csr)
+    e_.s_pull(recv_keys, n_recv, vals, true, 0, {}, true);
+  else
+    e_.s_pull(recv_keys, n_recv, vals, true, 0, offsets, ngroups > 1);
   if (prefetch && !prefetched) prefetch();
   const bool alias = self_only();
   float* pulled = alias ? vals : static_cast<float*>(get(pulled_, sizeof(float) * (size_t)(n_send * ps)));
@@ -275,7 +282,7 @@ bool ShardedStep::train_step(const BatchView& b, int64_t id, int S, const BatchV
   a2a_group(ops);
   if (next && !alias) counts_sent(prep_wb_);
 
-  if (e_.csr_slog2(S) >= 0 && e_.backend().csr_exchange()) {
+  if (csr) {
     // several slices as CSR entries: only the touched (key, slice) pairs move
     csr_gradients(b, S, sp, pulled, n_send, n_recv, recv_keys, offsets, next, next_id);
     e_.w_finish();

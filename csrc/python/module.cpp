@@ -369,6 +369,7 @@ PYBIND11_MODULE(_xflow_native, m) {
       .def("finish", &AsyncPS::finish, py::call_guard<py::gil_scoped_release>())
       .def("stop", &AsyncPS::stop, py::call_guard<py::gil_scoped_release>())
       .def("log", [](const AsyncPS& a) { return to_np(a.log()); })
+      .def_property_readonly("serving", &AsyncPS::serving)
       .def_property_readonly("transport", &AsyncPS::transport)
       .def_property_readonly("csr", &AsyncPS::csr)
       .def_readonly("steps", &AsyncPS::steps)

@@ -183,7 +183,7 @@ def _bs_batches(rank, dev, kind="lr"):
     return out
 
 
-def _bs_engine(dev, rows, log2_cap, slices=1, kind="lr"):
+def _bs_engine(dev, rows, log2_cap, slices=1, kind="lr", owner_group=0):
     # ("fm_std": standard-math FM, full-row CSR entries)
     m = (ModelConfig(kind="fm", v_dim=4, fm_math="standard") if kind == "fm_std"
          else ModelConfig(kind=kind, v_dim=4))
@@ -191,7 +191,7 @@ def _bs_engine(dev, rows, log2_cap, slices=1, kind="lr"):
     o = OptimConfig(kind="sgd", sgd_v_init=0.9) if kind == "mvm" else OptimConfig()
     return Engine(m, o,
                   EngineConfig(table_log2_cap=log2_cap, max_rows=rows, max_nnz=rows * 39,
-                               max_slices=slices), device=dev)
+                               max_slices=slices, owner_group=owner_group), device=dev)
 
 
 def _bs_worker(rank, world, kind, out_dir):
@@ -239,14 +239,14 @@ def test_rccl_processes_bench_scale_equals_single_engine(gpu_device, tmp_path, k
 # ---- several Hogwild slices per rank over RCCL: the CSR exchange (only the
 # touched (key, slice) entries move; reference: each slice pushes its own
 # keys, lr_worker.cc:162-175)
-CSR_W, CSR_S, CSR_STEPS = 2, 64, 3
+CSR_S, CSR_STEPS = 64, 3
 
 
-def _csr_worker(rank, world, kind, out_dir):
+def _csr_worker(rank, world, kind, out_dir, owner_group=0):
     from xflow_amd.parallel.sparse_a2a import ShardedEngine
 
     dev = torch.device("cuda", 0)
-    eng = _bs_engine(dev, BS_ROWS, 22, slices=CSR_S, kind=kind)
+    eng = _bs_engine(dev, BS_ROWS, 22, slices=CSR_S, kind=kind, owner_group=owner_group)
     sh = ShardedEngine(eng)
     assert sh.transport == "rccl", sh.transport
     bs = _bs_batches(rank, dev, kind)[:CSR_STEPS]
@@ -263,16 +263,22 @@ def _csr_worker(rank, world, kind, out_dir):
     np.save(os.path.join(out_dir, f"cb{rank}.npy"), np.array([sh.bytes_moved]))
 
 
-@pytest.mark.parametrize("kind", ["lr", "fm", "fm_std", "mvm"])
-def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kind):
-    """2 processes x 32 768 Criteo-shaped rows x 64 slices each, 3 pipelined
+@pytest.mark.parametrize("kind,CSR_W,owner_group", [
+    ("lr", 2, 0), ("fm", 2, 0), ("fm_std", 2, 0), ("mvm", 2, 0),
+    # >= 3 sources: the owners' per-source apply order (s_apply_csr's first
+    # source), and reference FM with the owner grouping configured (the CSR
+    # pull keeps the pulled weights, no grouping)
+    ("lr", 4, 0), ("fm", 4, 1), ("fm_std", 4, 0), ("mvm", 3, 0)])
+def test_rccl_processes_csr_slices_equal_single_engine(gpu_device, tmp_path, kind, CSR_W,
+                                                        owner_group):
+    """W processes x 32 768 Criteo-shaped rows x 64 slices each, 3 pipelined
     steps over RCCL with the CSR gradient exchange == one engine trained on
-    both ranks' rows as 128 ordered slices per step (source 0's slices, then
-    source 1's); the bytes moved are the touched pairs', far below the dense
-    [keys][64 x width] blocks."""
+    every rank's rows as W x 64 ordered slices per step (source 0's slices,
+    then source 1's, ...); the bytes moved are the touched pairs', far below
+    the dense [keys][64 x width] blocks."""
     from xflow_amd.engine import Batch
 
-    run_world_gpu(_csr_worker, CSR_W, kind, str(tmp_path))
+    run_world_gpu(_csr_worker, CSR_W, kind, str(tmp_path), owner_group)
     data = [_bs_batches(r, gpu_device, kind)[:CSR_STEPS] for r in range(CSR_W)]
     ref = _bs_engine(gpu_device, CSR_W * BS_ROWS, 24, slices=CSR_W * CSR_S, kind=kind)
     for s in range(CSR_STEPS):

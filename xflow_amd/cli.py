@@ -46,11 +46,14 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--sum-slices", action="store_true",
                     help="one FTRL push of the summed slice gradients per step")
     ap.add_argument("--no-init-push", action="store_true")
-    ap.add_argument("--async", dest="async_p2p", action="store_true",
-                    help="multi-rank: bounded-staleness steps, pushes over RCCL send/recv riding "
-                         "in the next exchange (BASELINE config 4)")
+    ap.add_argument("--async", dest="async_ps", action="store_true",
+                    help="multi-rank: the asynchronous parameter server (BASELINE config 4) -- a "
+                         "server thread per rank, workers that never wait for each other")
+    ap.add_argument("--async-lockstep", dest="async_p2p", action="store_true",
+                    help="multi-rank: lock-step steps whose pushes ride in the next exchange")
     ap.add_argument("--staleness", type=int, default=1,
-                    help="--async: pulls miss the previous N steps' pushes (1..7)")
+                    help="--async: own pushes in flight (0..7); --async-lockstep: pulls miss "
+                         "the previous N steps' pushes (1..7)")
     ap.add_argument("--log2-cap", type=int, default=22,
                     help="initial table slots per rank = 2^N (the table grows)")
     ap.add_argument("--max-log2-cap", type=int, default=0,
@@ -99,7 +102,8 @@ def config_from_args(a) -> TrainConfig:
         init_push=not a.no_init_push, pred_dir=a.pred_dir, write_pred=not a.no_pred_file,
         checkpoint_dir=a.save,
         save_every=a.save_every, resume_dir=a.resume,
-        metrics_file=a.metrics, async_p2p=a.async_p2p, staleness=a.staleness,
+        metrics_file=a.metrics, async_p2p=a.async_p2p, async_ps=a.async_ps,
+        staleness=a.staleness,
         model=ModelConfig(kind=kind, v_dim=a.v_dim, fm_math=a.fm_math, mvm_math=a.mvm_math,
                           fm_mfma=a.fm_mfma),
         optim=OptimConfig(kind=a.optimizer, alpha=a.alpha, beta=a.beta, lambda1=a.lambda1,

@@ -129,8 +129,11 @@ class TrainConfig:
     save_every: int = 0          # versioned checkpoint every N epochs (checkpoint.publish)
     resume_dir: str = ""         # versioned checkpoint root: resume from LATEST, save there
     metrics_file: str = ""
-    async_p2p: bool = False      # bounded-staleness steps, pushes over RCCL point-to-point
-    staleness: int = 1           # async_p2p: pulls miss the previous N steps' pushes
+    async_p2p: bool = False      # lock-step staleness-k steps, pushes riding the next exchange
+    # the asynchronous parameter server (parallel/async_ps.py): per-rank server
+    # threads, workers that never lock-step, no collective inside an epoch
+    async_ps: bool = False
+    staleness: int = 1           # async_ps: own pushes in flight; async_p2p: pushes missed
     model: ModelConfig = field(default_factory=ModelConfig)
     optim: OptimConfig = field(default_factory=OptimConfig)
     engine: EngineConfig = field(default_factory=EngineConfig)

@@ -175,6 +175,25 @@ class AsyncParameterServer:
         serving until ``close``)."""
         self._ps.finish()
 
+    def pause(self) -> None:
+        """Every rank: finish, barrier, stop serving -- the server engine (the
+        table shard) is then the caller's, e.g. for an epoch's statistics or a
+        checkpoint.  ``resume`` serves again from where it stopped."""
+        self._ps.finish()
+        self._barrier()
+        self._ps.stop()
+
+    def resume(self) -> None:
+        """Serve again after ``pause`` (the first call makes the handshake)."""
+        if not self.started:
+            self.start()
+        else:
+            self._ps.start()
+
+    @property
+    def serving(self) -> bool:
+        return bool(self._ps.serving)
+
     def close(self) -> None:
         """Every rank: finish, barrier (no worker needs a server any more),
         stop the server thread."""

@@ -88,9 +88,26 @@ class Trainer:
                 ecfg.max_rows = max(ecfg.max_rows, rows)
                 ecfg.max_nnz = max(ecfg.max_nnz, nnz)
         ecfg.max_slices = max(ecfg.max_slices, self.S)
-        self.engine = Engine(cfg.model, cfg.optim, ecfg, device=self.device)
         self.sharded = None
-        if self.world > 1 and cfg.async_p2p:
+        self.aps = None
+        if self.world > 1 and cfg.async_ps:
+            # the asynchronous parameter server: this rank's table shard lives
+            # in the server engine (its thread's), batches and forward passes
+            # in the worker engine; served between epochs only when paused
+            from xflow_amd.parallel.async_ps import AsyncParameterServer
+
+            self.aps = AsyncParameterServer(cfg.model, cfg.optim, ecfg, self.device,
+                                            staleness=cfg.staleness, slices=self.S, start=False,
+                                            slow_ms=0)  # (slow_rank: the injector sleeps)
+            self.engine = self.aps.worker
+            self.table = self.aps.server
+        else:
+            self.engine = Engine(cfg.model, cfg.optim, ecfg, device=self.device)
+            # the engine holding this rank's table shard
+            self.table = self.engine
+        if self.aps is not None:
+            pass
+        elif self.world > 1 and cfg.async_p2p:
             from xflow_amd.parallel.async_p2p import AsyncShardedEngine
 
             self.sharded = AsyncShardedEngine(self.engine, staleness=cfg.staleness)
@@ -214,7 +231,7 @@ class Trainer:
         mvm_worker.cc:276-278), applied once by the key's owner."""
         key = 1 if model_kind(self.cfg.model.kind) == 2 else 0
         if int(owner_of(np.array([key], dtype=np.uint64), self.world)[0]) == self.rank:
-            self.engine.push([key], np.zeros(self.engine.params_per_key, dtype=np.float32))
+            self.table.push([key], np.zeros(self.table.params_per_key, dtype=np.float32))
         xdist.barrier()
 
     def train_epochs(self, epochs: int) -> None:
@@ -222,7 +239,10 @@ class Trainer:
         path = shard_path(cfg.train_prefix, self.rank)
         nat = _native.load()
         log_every = int(os.environ.get("XFLOW_LOG_EVERY", "0"))
+        aps = self.aps
         for _ in range(epochs):
+            if aps is not None:
+                aps.resume()
             stream = record = None
             if self._resident is not None:  # batches kept in HBM by the first epoch
                 blocks = iter(self._resident)
@@ -279,7 +299,10 @@ class Trainer:
                 if tl is not None:
                     tl.begin("step")
                 with self.timer.phase("step"):
-                    if sh is not None:
+                    if aps is not None:
+                        if cur.rows > 0:
+                            aps.train_step(cur)
+                    elif sh is not None:
                         if not sh.train_step(cur if cur is not None else empty, S=self.S,
                                              next_batch=nb if nb is not None else empty):
                             break
@@ -302,24 +325,33 @@ class Trainer:
                 self._resident = record
             if hasattr(self.sharded, "flush"):
                 self.sharded.flush()
+            if aps is not None:
+                # every worker's pushes applied, every server idle: the table
+                # shard is this thread's until the next epoch resumes serving
+                aps.pause()
             self.samples += ep_samples
             self.epoch += 1
             if self.epoch % 30 == 0:
                 _say("epoch : %d" % (self.epoch - 1))
             st = self.engine.read_stats(reset=True)
             tot = xdist.all_sum([st["ln_loss"], st["rows"], ep_samples,
-                                 float(self.engine.overflowed())], self.device)
+                                 float(self.engine.overflowed() or self.table.overflowed())],
+                                self.device)
             if tot[3] > 0:
                 raise RuntimeError("table or dedup-scratch overflow during epoch %d: keys were "
                                    "dropped or isolated; grow --log2-cap / max_nnz" % self.epoch)
-            keys = self.engine.table_size()
+            keys = self.table.table_size()
             rec = dict(event="epoch", epoch=self.epoch, steps=self.steps,
                        train_logloss=tot[0] / max(tot[1], 1.0),
                        samples_per_s=tot[2] / max(time.perf_counter() - t0, 1e-9),
-                       table_keys=keys, table_load=keys / float(self.engine.table_capacity),
-                       table_capacity=self.engine.table_capacity,
-                       table_growths=self.engine.table_growths,
-                       monitor_waits=self.engine.monitor_waits)
+                       table_keys=keys, table_load=keys / float(self.table.table_capacity),
+                       table_capacity=self.table.table_capacity,
+                       table_growths=self.table.table_growths,
+                       monitor_waits=self.table.monitor_waits)
+            if aps is not None:
+                rec["async_ps"] = {k: v for k, v in aps.stats().items()
+                                   if k in ("max_staleness", "max_lead", "bytes_moved",
+                                            "wait_pull_s", "wait_slot_s", "transport")}
             if timeline is not None:
                 rec["timeline"] = {k: round(v, 3) for k, v in timeline.items()}
             # host time per step net of the time it sat blocked (monitor
@@ -339,7 +371,7 @@ class Trainer:
                 rec["mid_step_waits"] = sh.mid_step_waits - w0[2]
                 rec["early_key_exchanges"] = getattr(sh, "early_key_exchanges", 0)
             if self.cfg.optim.lambda1 > 0 and os.environ.get("XFLOW_REPORT_NNZ"):
-                rec["nonzero_weights"] = int(xdist.all_sum([self.engine.nonzero_weights()],
+                rec["nonzero_weights"] = int(xdist.all_sum([self.table.nonzero_weights()],
                                                            self.device)[0])
             self.metrics.log(**rec)
             root = cfg.resume_dir or cfg.checkpoint_dir
@@ -375,6 +407,9 @@ class Trainer:
             reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
                       else nat.BlockReader(tpath, cfg.resolved_test_block()))
         compat_mvm = model_kind(cfg.model.kind) == 2 and cfg.mvm_predict_compat
+        aps = self.aps
+        if aps is not None:
+            aps.resume()  # every rank serves; rank 0's worker pulls over all of them
         while True:
             blk, used, sr = None, 0, 0
             while reader is not None:
@@ -390,7 +425,11 @@ class Trainer:
             if self.sharded is None and blk is None:
                 break
             b = self._to_batch(blk, used, sr)
-            if self.sharded is not None:
+            if aps is not None:
+                pctr = aps.eval_step(b) if b.rows > 0 else None
+                if pctr is None:
+                    continue
+            elif self.sharded is not None:
                 # every rank joins; "no test data left anywhere" travels in the
                 # eval exchange's counts (no per-block collective)
                 pctr = self.sharded.eval_step(b)
@@ -407,6 +446,8 @@ class Trainer:
                 p, y = p[keep], y[keep]
             dev_p.append(p.clone())
             dev_y.append(y.clone())
+        if aps is not None:
+            aps.pause()
         if self.rank != 0:
             return None
         dev = self.device
@@ -451,12 +492,12 @@ class Trainer:
     def save(self, ckpt_dir: str) -> None:
         if hasattr(self.sharded, "flush"):
             self.sharded.flush()
-        checkpoint.save(self.engine, ckpt_dir, self.rank, self.world,
+        checkpoint.save(self.table, ckpt_dir, self.rank, self.world,
                         meta={"epoch": self.epoch, "steps": self.steps}, barrier=xdist.barrier)
         xdist.barrier()
 
     def load(self, ckpt_dir: str) -> dict:
-        meta = checkpoint.load(self.engine, ckpt_dir, self.rank, self.world)
+        meta = checkpoint.load(self.table, ckpt_dir, self.rank, self.world)
         self.epoch = int(meta.get("epoch", 0))
         self.steps = int(meta.get("steps", 0))
         xdist.barrier()
@@ -487,6 +528,8 @@ class Trainer:
             self.watchdog.stop()
         if getattr(self, "sharded", None) is not None:
             self.sharded.close()
+        if getattr(self, "aps", None) is not None:
+            self.aps.close()
         xdist.finalize()
 
 
