@@ -301,6 +301,12 @@ def main():
         sharded = (AsyncShardedEngine(engine, staleness=a.staleness) if a.async_p2p
                    else ShardedEngine(engine))
     overlap = a.overlap == "on"
+    # XFLOW_FAULT=slow_rank:<r>:<ms>: rank r sleeps before every step (the
+    # lock-step step then runs every rank at the straggler's pace; --async
+    # applies the same knob inside the async parameter server)
+    from xflow_amd.utils.faults import slow_ms_from_env
+
+    slow_s = slow_ms_from_env(rank) / 1000.0
     if not overlap and sharded is not None:
         # double-buffered batches on the compute stream
         bufs = [gen.alloc_batch(), gen.alloc_batch()]
@@ -311,6 +317,8 @@ def main():
             # pipelined: batch t+1 is generated and prepared (dedup + counts
             # exchange) inside step t, so the host never waits on an in-flight
             # split-size copy (ShardedEngine.prepare)
+            if slow_s:
+                time.sleep(slow_s)
             i = cur[0]
             sharded.train_step(bufs[i], prefetch=lambda: gen.next(out=bufs[i ^ 1]),
                                next_batch=bufs[i ^ 1])
