@@ -246,7 +246,7 @@ void AsyncPS::wait_event(void* ev) {
   const auto t0 = Clock::now();
   Backend& be = wk_.backend();
   be.event_record(ev);
-  be.event_wait(ev);
+  be.event_spin(ev);
   sync_s += since(t0);
 }
 

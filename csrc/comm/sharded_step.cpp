@@ -165,7 +165,7 @@ ShardedStep::Split ShardedStep::take(const BatchView& b, int64_t id, bool mid_st
   if (!be.event_done(counts_ready_[sp.wb])) {
     ++(mid_step ? mid_step_waits : host_waits);
     const auto t0 = std::chrono::steady_clock::now();
-    be.event_wait(counts_ready_[sp.wb]);
+    be.event_spin(counts_ready_[sp.wb]);
     host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   std::vector<int64_t> both(2 * W);
@@ -411,7 +411,7 @@ void ShardedStep::csr_gradients(const BatchView& b, int S, const Split& sp, cons
   if (!be.event_done(csr_tot_ready_)) {
     ++csr_waits;
     const auto t0 = std::chrono::steady_clock::now();
-    be.event_wait(csr_tot_ready_);
+    be.event_spin(csr_tot_ready_);
     csr_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   std::vector<int64_t> es(W), er(W);

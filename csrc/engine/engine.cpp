@@ -184,8 +184,16 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
       // MVM: T = loss*M per row; standard FM: (loss, loss*vs) per row (k_fm_std_fwd)
       if (mvm || fm_std) red_rowv_ = balloc<float>(be, (size_t)cfg_.max_rows * ps);
       if (mvm) {
-        red_vmax_ = balloc<u32>(be, 4);  // (vmax and dup words, two each)
-        be.memset(red_vmax_, 0, 4 * sizeof(u32));
+        // (vmax, dup flag, dup |c| max, dup record count: two alternating words each)
+        red_vmax_ = balloc<u32>(be, 8);
+        be.memset(red_vmax_, 0, 8 * sizeof(u32));
+        // repeated-field rows' records and fixed-point sums (MvmDup, backend.h)
+        const int D = cfg_.model.kernel_dim();
+        mdup_ew_ = csr_row_words(D);
+        mdup_rec_ = balloc<float>(be, (size_t)nnz * mdup_ew_);
+        mdup_acc_ = balloc<long long>(be, (size_t)nnz * D);
+        mdup_claim_ = balloc<u32>(be, (size_t)nnz);
+        mdup_cap_ = nnz;
       }
     }
   }
@@ -221,8 +229,8 @@ Engine::~Engine() {
                   host_slots_dev_, scratch_.ctl, red_pairs_, red_sorted_, red_hist_,
                   red_tot_, red_count_, red_rowv_, lr_grad_, lr_nz_, grp_nz_, own_keys_, fm_grad_,
                   row_grad_,
-                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_, csr_vent_, csr_dup_, csr_dup_n_,
-                  csr_cnt_, csr_doff_};
+                  lr_mask_, fm_w_, rec_count_, red_vmax_, text_ws_, text_counts_, csr_off_, csr_vent_,
+                  csr_cnt_, csr_doff_, mdup_rec_, mdup_acc_, mdup_claim_};
   for (void* p : ptrs) be.free(p);
   for (void* p : stage_io_) be.staging_free(p);
   for (SrvBuf& b : srv_) {
@@ -344,6 +352,17 @@ void Engine::set_reduction(FwdArgs& fa) const {
     fa.red_vmax_next = red_vmax_ + (vmax_parity_ ^ 1);
     fa.red_dup = red_vmax_ + 2 + vmax_parity_;
     fa.red_dup_next = red_vmax_ + 2 + (vmax_parity_ ^ 1);
+    if (mdup_rec_) {
+      fa.mdup.rec = mdup_rec_;
+      fa.mdup.vmax = red_vmax_ + 4 + vmax_parity_;
+      fa.mdup.vmax_next = red_vmax_ + 4 + (vmax_parity_ ^ 1);
+      fa.mdup.n = red_vmax_ + 6 + vmax_parity_;
+      fa.mdup.n_next = red_vmax_ + 6 + (vmax_parity_ ^ 1);
+      fa.mdup.acc = mdup_acc_;
+      fa.mdup.claim = mdup_claim_;
+      fa.mdup.cap = mdup_cap_;
+      fa.mdup.ew = mdup_ew_;
+    }
     vmax_parity_ ^= 1;
   }
   fa.red_bcap = bcap_;
@@ -700,15 +719,6 @@ void Engine::csr_forward_backward(const BatchView& b, int slog2, const int32_t* 
     fa.red_csr.ent = csr_vent_;
     fa.red_csr.P = table_.L.P;
     fa.red_csr.ew = ew;
-    if (cfg_.model.kind == kMVM) {  // repeated-field rows' records
-      if (!csr_dup_) {
-        csr_dup_ = balloc<float>(*be_, (size_t)cfg_.max_nnz * ew);
-        csr_dup_n_ = balloc<u32>(*be_, 1);
-      }
-      be_->memset(csr_dup_n_, 0, sizeof(u32));
-      fa.red_csr.dup = csr_dup_;
-      fa.red_csr.dup_n = csr_dup_n_;
-    }
   }
   be_->forward_backward(fa);
   ++csr_steps_;

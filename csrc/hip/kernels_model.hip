@@ -1820,7 +1820,7 @@ constexpr int kCsrVecWin = 15;
 // kMvm: the records are MVM's per-row T = loss*M sums (scaled fixed point,
 // k_red_sum_vec<.., kMvm>) and an entry is g_k = Σ T_k / (1 + v_k), 0 where
 // v_k == 0 (mvm_worker.cc:137-170); rows with a repeated field are added
-// after, by k_csr_dup_add.
+// after, by the MvmDup passes (k_mdup_*).
 template <int D, int G, bool kMvm = false>
 __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restrict__ recs, RedGeom geom,
                                                          int nb, SegSrc sg,
@@ -1973,26 +1973,82 @@ __global__ void __launch_bounds__(kRedBlock) k_red_csr_vec(const void* __restric
   }
 }
 
-// MVM rows with a repeated field (CsrOut::dup): each occurrence's gradient
-// row is added to its (key, slice) entry -- every occurrence left a record,
-// so the entry exists -- divided by the slice's rows, by float atomics (the
-// dense rows took them the same way).
-__global__ void __launch_bounds__(kBlock) k_csr_dup_add(CsrOut co, int max_n) {
-  const u32 n = min(*co.dup_n, (u32)max_n);
+// MVM rows with a repeated field (MvmDup): three order-free passes after the
+// reduction.  (1) resolve each record's target -- CSR: its (key, slice)
+// entry, found among the key's entries (every occurrence left a record, so
+// it exists) -- and zero the target's accumulators and claim; (2) add the
+// records' components in fixed point at the step's scale (the forward's
+// largest |c|; 2^head of them fit int64); (3) the first record of a target
+// adds the sums to the row / entry once (entries divided by the slice's rows,
+// as the entry itself is).  Integer sums: deterministic in any order.
+__global__ void __launch_bounds__(kBlock) k_mdup_prep(MvmDup m, CsrOut co, int D, int max_n) {
+  const u32 n = min(*m.n, (u32)min<int64_t>(max_n, m.cap));
+  const bool csr = co.cnt != nullptr;
   const int sl = co.slog2;
   const u32 smask = (1u << sl) - 1u;
-  float* ent = static_cast<float*>(co.ent);
+  const float* ent = static_cast<const float*>(co.ent);
   for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float* r = co.dup + (size_t)i * co.ew;
-    const u32 d = __float_as_uint(r[0]);
-    const u32 u = d >> sl, s = d & smask;
-    const u32 o = co.off[u], c = co.cnt[u];
-    u32 e = o;
-    while (e < o + c && __float_as_uint(ent[(size_t)e * co.ew]) != s) ++e;
-    if (e == o + c) continue;  // (cannot happen: the occurrence left a record)
-    const float rows = co.rows ? (float)co.rows[s] : 1.0f;
-    for (int k = 0; k < co.P && k + 1 < co.ew; ++k) atomicAdd(&ent[(size_t)e * co.ew + 1 + k], r[1 + k] / rows);
+    float* r = m.rec + (size_t)i * m.ew;
+    u32 t = __float_as_uint(r[0]);
+    if (csr) {
+      const u32 u = t >> sl, s = t & smask;
+      const u32 o = co.off[u], c = co.cnt[u];
+      u32 e = o;
+      while (e < o + c && __float_as_uint(ent[(size_t)e * co.ew]) != s) ++e;
+      t = e < o + c ? e : 0xFFFFFFFFu;
+      r[0] = __uint_as_float(t);
+    }
+    if (t == 0xFFFFFFFFu || (int64_t)t >= m.cap) continue;
+    for (int k = 0; k < D; ++k) m.acc[(size_t)t * D + k] = 0ll;
+    m.claim[t] = 0u;
   }
+}
+
+__global__ void __launch_bounds__(kBlock) k_mdup_acc(MvmDup m, int D, int head, int max_n) {
+  const u32 n = min(*m.n, (u32)min<int64_t>(max_n, m.cap));
+  const int fxs = fx_scale_bits(m.vmax, head);
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float* r = m.rec + (size_t)i * m.ew;
+    const u32 t = __float_as_uint(r[0]);
+    if (t == 0xFFFFFFFFu || (int64_t)t >= m.cap) continue;
+    for (int k = 0; k < D; ++k)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&m.acc[(size_t)t * D + k]),
+                (unsigned long long)fx_from_rt(r[1 + k], fxs));
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_mdup_fin(MvmDup m, CsrOut co, float* __restrict__ out,
+                                                     int PS, int D, int head, int max_n) {
+  const u32 n = min(*m.n, (u32)min<int64_t>(max_n, m.cap));
+  const int fxs = fx_scale_bits(m.vmax, head);
+  const bool csr = co.cnt != nullptr;
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const u32 t = __float_as_uint(m.rec[(size_t)i * m.ew]);
+    if (t == 0xFFFFFFFFu || (int64_t)t >= m.cap) continue;
+    if (atomicExch(&m.claim[t], 1u) != 0u) continue;  // (one adder per target)
+    const long long* ac = m.acc + (size_t)t * D;
+    if (csr) {
+      float* e = static_cast<float*>(co.ent) + (size_t)t * co.ew;
+      const u32 s = __float_as_uint(e[0]);
+      const double rows = co.rows ? (double)co.rows[s] : 1.0;
+      for (int k = 0; k < co.P && k + 1 < co.ew && k < D; ++k)
+        e[1 + k] += (float)(fx_to_double_rt(ac[k], fxs) / rows);
+    } else {
+      float* row = out + (size_t)t * PS;
+      for (int k = 0; k < D; ++k) row[k] += (float)fx_to_double_rt(ac[k], fxs);
+    }
+  }
+}
+
+static void launch_mdup(const FwdArgs& a, int D, hipStream_t st) {
+  const int64_t nmax = a.batch.nnz < a.mdup.cap ? a.batch.nnz : a.mdup.cap;
+  const int g = (int)std::min<int64_t>(2048, (nmax + kBlock - 1) / kBlock + 1);
+  const int head = fx_head_bits(a.batch.nnz);
+  CsrOut co = a.red_csr.cnt ? a.red_csr : CsrOut();
+  hipLaunchKernelGGL(k_mdup_prep, dim3(g), dim3(kBlock), 0, st, a.mdup, co, D, (int)nmax);
+  hipLaunchKernelGGL(k_mdup_acc, dim3(g), dim3(kBlock), 0, st, a.mdup, D, head, (int)nmax);
+  hipLaunchKernelGGL(k_mdup_fin, dim3(g), dim3(kBlock), 0, st, a.mdup, co, a.red_out,
+                     D == 1 ? 1 : (D + 3) & ~3, D, head, (int)nmax);  // (mvm_ps)
 }
 
 // Standard-math FM forward of the split form (k_fm_std_red<.., kSplit>): one
@@ -2077,7 +2133,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   const u32* dup = kMvm && a.S == 1 ? a.red_dup : nullptr;
   if (a.red_csr.cnt) {  // several slices as CSR entries (Engine::train_step_csr)
     if (!seg || !split || a.red_out || !a.red_nuq || a.S != (1 << a.red_csr.slog2) ||
-        (kMvm && (!a.red_csr.dup || !a.red_csr.dup_n)) ||
+        (kMvm && !a.mdup.rec) ||
         a.red_csr.slog2 > red_shift(NV) || a.red_csr.P > NV || a.red_csr.P < 1 ||
         a.red_csr.ew < csr_row_words(a.red_csr.P))
       throw std::runtime_error("CSR vector reduction: split scatter-free form, unique positions, "
@@ -2104,9 +2160,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((k_red_csr_vec<D, kSegMaxGroups, kMvm>), dim3(g2), dim3(kRedBlock), 0, st,
                          static_cast<const void*>(a.red_pairs), geom, a.red_nb, sg, estart,
                          a.red_csr, a.wpull, a.red_vmax);
-    if (kMvm)  // (rows with a repeated field: rare; one small grid)
-      hipLaunchKernelGGL(k_csr_dup_add, dim3(std::min<int64_t>(1024, (a.batch.nnz + kBlock - 1) / kBlock + 1)),
-                         dim3(kBlock), 0, st, a.red_csr, (int)a.batch.nnz);
+    if (kMvm && a.mdup.rec) launch_mdup(a, NV, st);  // (rows with a repeated field)
     return;
   }
   if (seg) {
@@ -2126,6 +2180,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
                          static_cast<const void*>(a.red_pairs), nullptr, a.grad, geom, a.red_nb,
                          a.red_out, a.red_inv, a.wpull, a.S, sg, masks, a.red_vmax, dup);
     }
+    if (kMvm && a.mdup.rec && a.red_out) launch_mdup(a, NV, st);  // (rows with a repeated field)
     return;
   }
   if (split) hipLaunchKernelGGL((k_fm_std_red<D, BLOCK, false, true, kMvm>), dim3(groups), dim3(BLOCK), 0, st, a);
@@ -2140,6 +2195,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((k_red_sum_vec<D, false, kSegMaxGroups, kMvm>), dim3(grid), dim3(kRedBlock), 0, st,
                      static_cast<const void*>(a.red_sorted), start, a.grad, geom, a.red_nb,
                      a.red_out, a.red_inv, a.wpull, a.S, SegSrc{}, masks, a.red_vmax, dup);
+  if (kMvm && a.mdup.rec && a.red_out) launch_mdup(a, NV, st);  // (rows with a repeated field)
 }
 
 // Reference-math FM on compact value rows (FwdArgs::fm_vals): each feature's
@@ -2595,21 +2651,38 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           if (!(m <= 3.0e38f)) atomicOr(a.fx_bad, 2u);  // non-finite T: a diverged model
           if (blockIdx.x == 0) *a.red_vmax_next = 0u;  // (the next step's word)
           if (blockIdx.x == 0 && a.red_dup_next) *a.red_dup_next = 0u;
+          if (blockIdx.x == 0 && a.mdup.rec) {  // (the next step's record count and max)
+            *a.mdup.n_next = 0u;
+            *a.mdup.vmax_next = 0u;
+          }
         }
       }
-      // (one flag write per wave with a repeated-field row: FwdArgs::red_dup)
-      if (a.red_dup && __ballot(active && dup) && lane_id() == 0) atomicOr(a.red_dup, 1u);
-      if (active && dup && a.red_csr.cnt) {
-        // (CSR entries: the row's occurrences as dup records, k_csr_dup_add)
-        const int ew = a.red_csr.ew;
+      // repeated-field rows on the unique-row / CSR outputs: fixed-point
+      // records for the order-free passes after the reduction (MvmDup)
+      const bool md = a.mdup.rec && (a.red_out || a.red_csr.cnt);
+      // (one flag write per wave with a repeated-field row added by atomics: FwdArgs::red_dup)
+      if (a.red_dup && !md && __ballot(active && dup) && lane_id() == 0) atomicOr(a.red_dup, 1u);
+      float cmax = 0.0f;
+      if (active && dup && md) {
+        const int ew = a.mdup.ew;
         for (int j = 0; j < len; ++j) {
           float c[D];
           contrib(j, c);
           const u32 pj = pos[rs.at(j)];
           if (pj == a.trash_pos) continue;
-          float* rec = a.red_csr.dup + (size_t)atomicAdd(a.red_csr.dup_n, 1u) * ew;
-          rec[0] = __uint_as_float(pj * S + s);
-          for (int k = 0; k < D && k + 1 < ew; ++k) rec[1 + k] = c[k];
+          // target: the (key, slice) dest (CSR; resolved to its entry later)
+          // or the key's unique-order row
+          const u32 tgt = a.red_csr.cnt ? pj * S + s : uix(a.red_inv, pj);
+          if (tgt == 0xFFFFFFFFu) continue;
+          const u32 at = atomicAdd(a.mdup.n, 1u);
+          if (at >= (u32)a.mdup.cap) continue;  // (cannot happen: <= one per occurrence)
+          float* rec = a.mdup.rec + (size_t)at * ew;
+          rec[0] = __uint_as_float(tgt);
+#pragma unroll
+          for (int k = 0; k < D; ++k) {
+            rec[1 + k] = c[k];
+            cmax = fmaxf(cmax, c[k] == c[k] ? fabsf(c[k]) : INFINITY);
+          }
         }
       } else if (active && dup) {
         for (int j = 0; j < len; ++j) {
@@ -2624,6 +2697,13 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           }
 #pragma unroll
           for (int k = 0; k < D; ++k) atomicAdd(&g[k], c[k]);
+        }
+      }
+      if (md) {  // (every lane: the wave's largest |c| sets the step's scale)
+        cmax = wave_max(cmax);
+        if (lane_id() == 0 && cmax > 0.0f) {
+          atomicMax(a.mdup.vmax, __float_as_uint(fminf(cmax, 3.4e38f)));
+          if (!(cmax <= 3.0e38f)) atomicOr(a.fx_bad, 2u);  // non-finite: a diverged model
         }
       }
     } else if constexpr (!kAgg) {

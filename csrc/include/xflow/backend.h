@@ -163,18 +163,36 @@ struct CsrOut {
   int slog2 = 0;
   const int32_t* rows = nullptr;  // values divided by rows[slice] (null: raw sums)
   int ew = 0, P = 0;              // full-row entries: words per entry, params per key
-  // MVM: rows with a repeated field (their gradient is not T / (1 + v) of the
-  // key's own v) leave (dest, c_0 .. c_{P-1}) records of ew words here,
-  // counted at dup_n (zeroed before the forward); added to their entries after
-  // the reduction (float atomics, as the dense rows took them)
-  float* dup = nullptr;
-  u32* dup_n = nullptr;
+  // (MVM rows with a repeated field: FwdArgs::mdup, added to their entries
+  // after the reduction)
 };
 // 32-bit words of a full-row CSR entry (slice, g_0 .. g_{P-1}), 16-B padded
 constexpr int csr_row_words(int P) { return (1 + P + 3) & ~3; }
 
+// MVM rows with a repeated field (HIP reduction paths: one slice into
+// unique-order rows, or CSR entries): their per-occurrence gradients are not
+// T / (1 + v) of the key's own v (the field sum is), so they leave records
+// (target, c_0 .. c_{D-1}) here and three small passes after the reduction add
+// them in fixed point at a per-step scale (the forward's largest |c|): resolve
+// the targets (CSR: the (key, slice) entry) and zero their accumulators, sum,
+// add each target's sum to its row / entry once -- order-free, so
+// deterministic (float atomics were not).  Two alternating count and max
+// words, like red_vmax.
+struct MvmDup {
+  float* rec = nullptr;          // [cap][ew]: target (u32 bits), c_0 .. c_{D-1}
+  u32* n = nullptr;              // records of this step (device)
+  u32* n_next = nullptr;         // the next step's counter (cleared by the forward)
+  u32* vmax = nullptr;           // max |c| (float bits)
+  u32* vmax_next = nullptr;
+  long long* acc = nullptr;      // [cap][D] fixed-point sums per target
+  u32* claim = nullptr;          // [cap] first adder of a target
+  int64_t cap = 0;
+  int ew = 0;
+};
+
 struct FwdArgs {
   BatchView batch;
+  MvmDup mdup;
   const u32* pos = nullptr;        // [nnz]
   // dedup slot of overflowed occurrences (the scratch's trash slot, == cap):
   // read as zero weights, never reduced (none: ~0)
@@ -588,6 +606,13 @@ class Backend {
   virtual void event_record(void* e) { (void)e; }
   virtual bool event_done(void* e) { (void)e; return true; }
   virtual void event_wait(void* e) { (void)e; }
+  // wait by polling (no blocking-sync wake-up latency: a host that must
+  // enqueue the next device work the moment this event fires -- the CSR
+  // exchange's entry totals, the async parameter server's hand-overs)
+  void event_spin(void* e) {
+    while (!event_done(e)) {
+    }
+  }
 
   // Asynchronous double-buffered host -> device staging (the native trainer's
   // input path).  Slot s in {0, 1}: stage_begin(s) waits on the host until

@@ -431,8 +431,12 @@ class Engine {
   u32* csr_off_ = nullptr;      // [max_nnz]
   u32* csr_cnt_ = nullptr;      // [max_nnz]
   float* csr_vent_ = nullptr;   // standard FM / MVM: full-row entries [max_nnz][csr_row_words(P)]
-  float* csr_dup_ = nullptr;    // MVM: repeated-field rows' records (CsrOut::dup), same shape
-  u32* csr_dup_n_ = nullptr;
+  // MVM: repeated-field rows' records and fixed-point sums (MvmDup, backend.h)
+  float* mdup_rec_ = nullptr;
+  long long* mdup_acc_ = nullptr;
+  u32* mdup_claim_ = nullptr;
+  int64_t mdup_cap_ = 0;
+  int mdup_ew_ = 0;
   int64_t csr_steps_ = 0;
   void train_step_csr(const BatchView& b, int S, int slog2);
   u32* csr_doff_ = nullptr;     // [max_nnz + 1] dense offsets (worker pack)

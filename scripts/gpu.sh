@@ -106,6 +106,23 @@ for k, cs in acc.items():
 PY
 }
 
+run_pmcx() {  # "ARGS" "KREGEX" "COUNTERS" -- one extra PMC pass with the given counters
+  local d=$O/px
+  timeout -s KILL 150 rocprofv3 --pmc $3 --kernel-include-regex "${2:-.}" --output-format csv -d $d -o run -- \
+      python3 bench.py --steps 3 --warmup 1 ${1:-} > $d.log 2>&1 || { echo "pmc pass failed"; tail -20 $d.log; exit 1; }
+  python3 - "$d" <<'PY'
+import csv, glob, sys, collections
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        acc[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in acc.items():
+    print("==", k)
+    for c, v in sorted(cs.items()):
+        print(f"   {c:40s} {sum(v)/len(v):16.1f}  (n={len(v)})")
+PY
+}
+
 run_ab() {  # "V1 V2 ..." "ARGS"
   local r v
   for r in $(seq 1 ${ROUNDS:-2}); do
@@ -152,6 +169,7 @@ case $cmd in
   bench) run_bench "${1:-}" ;;
   prof) run_prof "${1:-}" ;;
   pmc) run_pmc "${1:-}" "${2:-.}" ;;
+  pmcx) run_pmcx "${1:-}" "${2:-.}" "${3:?counters}" ;;
   ab) run_ab "${1:?variants}" "${2:-}" ;;
   shared) run_shared "${1:-2}" "${2:-}" ;;
   kbench) run_kbench "${1:-}" ;;

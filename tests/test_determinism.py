@@ -79,3 +79,42 @@ def test_bench_scale_deterministic_and_matches_cpu(gpu_device, kind, rows, small
     np.testing.assert_allclose(w1, wc, rtol=1e-4, atol=1e-6)
     assert st1["rows"] == stc["rows"]
     assert abs(st1["ln_loss"] - stc["ln_loss"]) <= 1e-5 * abs(stc["ln_loss"])
+
+
+def _mvm_dup_train(dev, batches, S, optim):
+    eng = Engine(ModelConfig(kind="mvm", v_dim=10), optim,
+                 EngineConfig(table_log2_cap=20, max_rows=16384, max_nnz=16384 * 24, max_slices=S),
+                 device=dev)
+    for b in batches:
+        if dev.type == "cuda":
+            b = Batch(keys=b.keys.to(dev), labels=b.labels.to(dev), row_ptr=b.row_ptr.to(dev),
+                      fgid=b.fgid.to(dev), slice_rows=b.slice_rows)
+        eng.train_step(b)
+    assert not eng.overflowed()
+    keys, _ = eng.export_table()
+    keys = np.sort(keys)
+    return keys, eng.pull(keys), eng.native.step_plan(S)["grad"]
+
+
+@pytest.mark.parametrize("S", [1, 64])
+def test_mvm_repeated_fields_deterministic(gpu_device, S):
+    """MVM rows with a repeated field (fields 16-17 hold 1-2 features, like
+    the bundled data's multi-valued fields; mvm_worker.cc:137-170: the
+    gradient divides by 1 + the FIELD sum) add their gradients in fixed point
+    after the reduction (MvmDup): two GPU runs are bitwise equal, and equal
+    the CPU backend within rounding -- on the unique-row layout (1 slice) and
+    on CSR entries (64 slices)."""
+    from helpers import random_csr, to_batch
+
+    optim = OptimConfig(kind="sgd", sgd_v_init=0.9)  # (live products: gradients flow)
+    batches = [to_batch(*random_csr(16384, 18, 400, seed=31 + i, variable=True), torch.device("cpu"),
+                        slice_rows=16384 // S) for i in range(4)]
+    assert (np.diff(batches[0].row_ptr.numpy()) > 18).any()  # rows with repeated fields
+    k1, w1, grad = _mvm_dup_train(gpu_device, batches, S, optim)
+    assert grad == ("unique_rows" if S == 1 else "csr"), grad
+    k2, w2, _ = _mvm_dup_train(gpu_device, batches, S, optim)
+    np.testing.assert_array_equal(k1, k2)
+    np.testing.assert_array_equal(w1.view(np.uint32), w2.view(np.uint32))  # bitwise
+    kc, wc, _ = _mvm_dup_train(torch.device("cpu"), batches, S, optim)
+    np.testing.assert_array_equal(k1, kc)
+    np.testing.assert_allclose(w1, wc, rtol=1e-4, atol=1e-6)
