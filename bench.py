@@ -113,6 +113,13 @@ def parse():
     return ap.parse_args()
 
 
+def _entropy(p: float) -> float:
+    """ln-logloss of always predicting the base rate p."""
+    if p <= 0.0 or p >= 1.0:
+        return 0.0
+    return -(p * math.log(p) + (1.0 - p) * math.log(1.0 - p))
+
+
 def run_async(a, world, rank, device, use_gpu, shared_gpu, synth, log2_cap, nnz):
     """--async: BASELINE config 4 on the asynchronous parameter server.  Every
     rank warms up, meets the others at one barrier, then runs its --steps
@@ -404,7 +411,7 @@ def main():
     nnzw = engine.nonzero_weights() if a.async_p2p else 0
     ovf = float(engine.overflowed())  # table probe wrap / dedup scratch overflow
     red = torch.tensor([elapsed, st["ln_loss"], st["rows"], float(tbl), float(nnzw), ovf,
-                        float(prefilled)],
+                        float(prefilled), st["positives"]],
                        dtype=torch.float64, device=device)
     if world > 1:
         mx = red[:1].clone()
@@ -459,6 +466,9 @@ def main():
                        "table_growths": engine.table_growths},
             **({"shared_gpu_rehearsal": True} if shared_gpu else {}),
             "logloss": ln_loss / max(rows, 1.0),
+            # the constant predictor's logloss on the same labels (the base
+            # rate's entropy): a model learns when logloss falls below it
+            "constant_logloss": _entropy(vals[7] / max(rows, 1.0)),
             "table_keys": int(table_keys),
             "reduction_records_per_step": int(records),
             "table_load": table_keys / float(world * 2 ** log2_cap),

@@ -354,10 +354,8 @@ void Engine::set_reduction(FwdArgs& fa) const {
     fa.red_dup_next = red_vmax_ + 2 + (vmax_parity_ ^ 1);
     if (mdup_rec_) {
       fa.mdup.rec = mdup_rec_;
-      fa.mdup.vmax = red_vmax_ + 4 + vmax_parity_;
-      fa.mdup.vmax_next = red_vmax_ + 4 + (vmax_parity_ ^ 1);
-      fa.mdup.n = red_vmax_ + 6 + vmax_parity_;
-      fa.mdup.n_next = red_vmax_ + 6 + (vmax_parity_ ^ 1);
+      fa.mdup.vmax = red_vmax_ + 4;
+      fa.mdup.n = red_vmax_ + 6;
       fa.mdup.acc = mdup_acc_;
       fa.mdup.claim = mdup_claim_;
       fa.mdup.cap = mdup_cap_;

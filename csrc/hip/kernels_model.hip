@@ -1359,8 +1359,18 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   static_assert(BLOCK == fmstd_block(D), "producer block");
   constexpr u32 kSlots = (u32)fmstd_slots(D);  // (not a power of two: 1.5 x BLOCK at D = 8)
   constexpr int kFx = FxBits<1>::kFx;
+  // Column accumulators.  kScaled (MVM): int64 at the step's scale.  Else
+  // int32 at a per-workgroup, per-component scale: a column adds at most one
+  // value per row (BLOCK of them), each below 2^31 / BLOCK once scaled by the
+  // workgroup's largest |value| of that component, so no sum overflows -- and
+  // an int32 LDS atomic touches one bank where an int64 one touched two (the
+  // random-slot atomics were 64 % bank-conflict cycles, profiles/r5_fmstd_pmc.txt).
+  // Order-free integer sums either way: deterministic.
+  using Acc = typename std::conditional<kScaled, long long, int>::type;
   __shared__ u64 s_tag[1][kSlots];
-  __shared__ long long s_acc[1][kSlots * NV];
+  __shared__ Acc s_acc[1][kSlots * NV];
+  __shared__ int s_fxc[NV];
+  __shared__ float s_cmax[NV][BLOCK / kWave];
   const int fxs = kScaled ? fx_scale_bits(a.red_vmax, fx_head_bits(a.batch.rows)) : kFx;
   __shared__ unsigned short s_list[1][BLOCK];
   constexpr int kMaxB = vec_red_max_buckets(D);
@@ -1386,7 +1396,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   for (int i = threadIdx.x; i < kSlots; i += BLOCK) {
     s_tag[0][i] = ~0ull;
 #pragma unroll
-    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = 0ll;
+    for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = (Acc)0;
   }
   for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) s_hist[i] = 0u;
   if (threadIdx.x < 3) s_nlist[threadIdx.x] = 0u;
@@ -1505,16 +1515,41 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   // Σ loss*vs_k -- v_k is the key's pulled value, one per step -- so the
   // column walk needs no second gather of the pulled row; k_red_sum_vec
   // expands C - v*B once per dest)
-  long long rowv[NV];
+  Acc rowv[NV];
   if constexpr (kScaled) {  // (kSplit: the row's vector, |.| <= the step's vmax)
     rowv[0] = fx_from_rt(loss, fxs);
 #pragma unroll
     for (int k = 0; k < D; ++k) rowv[1 + k] = fx_from_rt(vs[k], fxs);
   } else {
-    rowv[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
+    // per-component scale from the workgroup's largest |value| (see s_acc)
+    float f[NV];
+    f[0] = loss;
 #pragma unroll
-    for (int k = 0; k < D; ++k)
-      rowv[1 + k] = fx_from<kFx>(fx_clamp<kFx>(kSplit ? vs[k] : loss * vs[k], bad));
+    for (int k = 0; k < D; ++k) f[1 + k] = kSplit ? vs[k] : loss * vs[k];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      float m = f[c] == f[c] ? fabsf(f[c]) : INFINITY;
+      if (!(m <= 3.0e38f)) bad = 1u;  // non-finite: a diverged model (flagged, read as 0)
+      m = wave_max(m <= 3.0e38f ? m : 0.0f);
+      if (lane_id() == 0) s_cmax[c][threadIdx.x / kWave] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+      float m = 0.0f;
+#pragma unroll
+      for (int w = 0; w < BLOCK / kWave; ++w) m = fmaxf(m, s_cmax[threadIdx.x][w]);
+      int e = 0;
+      if (m > 0.0f) frexpf(m, &e);  // m < 2^e
+      constexpr int kHead = ilog2c(BLOCK) + 1;  // (BLOCK terms, plus rounding slack)
+      const int fx = 31 - kHead - e;
+      s_fxc[threadIdx.x] = fx < -100 ? -100 : (fx > 100 ? 100 : fx);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const double d = ldexp((double)f[c], s_fxc[c]);
+      rowv[c] = (d == d && fabs(d) < 2.1e9) ? (int)__builtin_rint(d) : 0;
+    }
   }
   for (int j = 0; j < maxlen; ++j) {
     const int t = 0;
@@ -1544,10 +1579,14 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       }
     }
     if (has) {
-      long long* acc = &s_acc[t][h * NV];
+      Acc* acc = &s_acc[t][h * NV];
 #pragma unroll
-      for (int c = 0; c < NV; ++c)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)rowv[c]);
+      for (int c = 0; c < NV; ++c) {
+        if constexpr (kScaled)
+          atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)rowv[c]);
+        else
+          atomicAdd(&acc[c], rowv[c]);
+      }
     }
     const unsigned long long m = __ballot(claimed);
     if (m) {
@@ -1566,9 +1605,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       wv[0] = d;
 #pragma unroll
       for (int c = 0; c < NV; ++c) {
-        long long* ap = &s_acc[t][hh * NV + c];
-        wv[1 + c] = __float_as_uint((float)fx_to_double_rt(*ap, fxs));
-        *ap = 0ll;
+        Acc* ap = &s_acc[t][hh * NV + c];
+        wv[1 + c] = __float_as_uint(kScaled ? (float)fx_to_double_rt((long long)*ap, fxs)
+                                            : (float)ldexp((double)*ap, -s_fxc[c]));
+        *ap = (Acc)0;
       }
 #pragma unroll
       for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
@@ -2040,6 +2080,13 @@ __global__ void __launch_bounds__(kBlock) k_mdup_fin(MvmDup m, CsrOut co, float*
   }
 }
 
+// the step's record count and scale back to 0 once the passes read them (a
+// step without a forward -- 0 rows -- must find them 0, whatever the parity)
+__global__ void k_mdup_done(u32* n, u32* vmax) {
+  *n = 0u;
+  *vmax = 0u;
+}
+
 static void launch_mdup(const FwdArgs& a, int D, hipStream_t st) {
   const int64_t nmax = a.batch.nnz < a.mdup.cap ? a.batch.nnz : a.mdup.cap;
   const int g = (int)std::min<int64_t>(2048, (nmax + kBlock - 1) / kBlock + 1);
@@ -2049,6 +2096,7 @@ static void launch_mdup(const FwdArgs& a, int D, hipStream_t st) {
   hipLaunchKernelGGL(k_mdup_acc, dim3(g), dim3(kBlock), 0, st, a.mdup, D, head, (int)nmax);
   hipLaunchKernelGGL(k_mdup_fin, dim3(g), dim3(kBlock), 0, st, a.mdup, co, a.red_out,
                      D == 1 ? 1 : (D + 3) & ~3, D, head, (int)nmax);  // (mvm_ps)
+  hipLaunchKernelGGL(k_mdup_done, dim3(1), dim3(1), 0, st, a.mdup.n, a.mdup.vmax);
 }
 
 // Standard-math FM forward of the split form (k_fm_std_red<.., kSplit>): one
@@ -2651,10 +2699,7 @@ __global__ void __launch_bounds__(mvm_block_for(D, kRed)) k_mvm2(FwdArgs a) {
           if (!(m <= 3.0e38f)) atomicOr(a.fx_bad, 2u);  // non-finite T: a diverged model
           if (blockIdx.x == 0) *a.red_vmax_next = 0u;  // (the next step's word)
           if (blockIdx.x == 0 && a.red_dup_next) *a.red_dup_next = 0u;
-          if (blockIdx.x == 0 && a.mdup.rec) {  // (the next step's record count and max)
-            *a.mdup.n_next = 0u;
-            *a.mdup.vmax_next = 0u;
-          }
+
         }
       }
       // repeated-field rows on the unique-row / CSR outputs: fixed-point

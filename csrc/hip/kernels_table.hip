@@ -19,6 +19,7 @@
 // several independent probes in flight per lane, count bookkeeping with one
 // atomic per workgroup (single-address atomics serialise), and read
 // device-side element counts so a whole step runs without host syncs.
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 
@@ -1778,8 +1779,47 @@ __global__ void __launch_bounds__(kBlock) k_scan_write(const u32* __restrict__ i
   if (blockIdx.x == (unsigned)(nt - 1) && threadIdx.x == kBlock - 1) out[n] = ex;
 }
 
+// small arrays (<= kScanBlock x kScanItems, e.g. the CSR applies' per-wave
+// deferral counts): the whole scan in one launch of one workgroup
+constexpr int64_t kScanOneMax = (int64_t)kScanBlock * kScanItems;
+__global__ void __launch_bounds__(kScanBlock) k_scan_one(const u32* __restrict__ in,
+                                                         const int64_t* __restrict__ n_dev,
+                                                         int64_t n_max, u32* __restrict__ out) {
+  int64_t n = n_dev ? *n_dev : n_max;
+  if (n > n_max) n = n_max;
+  u32 loc[kScanItems], v = 0;
+#pragma unroll
+  for (int q = 0; q < kScanItems; ++q) {
+    const int64_t i = (int64_t)threadIdx.x * kScanItems + q;
+    loc[q] = i < n ? in[i] : 0u;
+    v += loc[q];
+  }
+  u32 tot;
+  u32 ex = block_exclusive_scan<kScanBlock>(v, &tot);
+#pragma unroll
+  for (int q = 0; q < kScanItems; ++q) {
+    const int64_t i = (int64_t)threadIdx.x * kScanItems + q;
+    if (i < n) out[i] = ex;
+    ex += loc[q];
+  }
+  if (threadIdx.x == 0) out[n] = tot;
+}
+
+static bool scan_one_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("XFLOW_SCAN_ONE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void launch_scan_u32(const u32* in, u32* out, const int64_t* n_dev, int64_t n_max, u32* tiles,
                      hipStream_t st) {
+  if (n_max <= kScanOneMax && scan_one_enabled()) {
+    hipLaunchKernelGGL(k_scan_one, dim3(1), dim3(kScanBlock), 0, st, in, n_dev, n_max, out);
+    XF_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int g = (int)((n_max + kScanTile - 1) / kScanTile) + 1;
   hipLaunchKernelGGL(k_scan_tiles, dim3(g), dim3(kBlock), 0, st, in, n_dev, n_max, tiles);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanBlock), 0, st, tiles, n_dev, n_max);

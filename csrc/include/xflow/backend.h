@@ -176,14 +176,12 @@ constexpr int csr_row_words(int P) { return (1 + P + 3) & ~3; }
 // them in fixed point at a per-step scale (the forward's largest |c|): resolve
 // the targets (CSR: the (key, slice) entry) and zero their accumulators, sum,
 // add each target's sum to its row / entry once -- order-free, so
-// deterministic (float atomics were not).  Two alternating count and max
-// words, like red_vmax.
+// deterministic (float atomics were not).  The count and max words are 0
+// at a step's start: the passes' last launch resets them.
 struct MvmDup {
   float* rec = nullptr;          // [cap][ew]: target (u32 bits), c_0 .. c_{D-1}
   u32* n = nullptr;              // records of this step (device)
-  u32* n_next = nullptr;         // the next step's counter (cleared by the forward)
   u32* vmax = nullptr;           // max |c| (float bits)
-  u32* vmax_next = nullptr;
   long long* acc = nullptr;      // [cap][D] fixed-point sums per target
   u32* claim = nullptr;          // [cap] first adder of a target
   int64_t cap = 0;
