@@ -414,6 +414,22 @@ class CpuBackend final : public Backend {
     }
   }
 
+  void unpack_block(const UnpackArgs& a) override {
+    if (a.F > kMaxPackedFields) throw std::invalid_argument("unpack_block: at most 64 fields");
+    for (int f = 0; f < a.F; ++f) {
+      const uint8_t* col = a.block + a.col_off[f];
+      const int w = a.width[f];
+      if (w != 1 && w != 2 && w != 4 && w != 8)
+        throw std::invalid_argument("unpack_block: code widths 1/2/4/8");
+      for (int64_t r = 0; r < a.rows; ++r) {
+        u64 c = 0;
+        std::memcpy(&c, col + r * w, (size_t)w);  // (little endian)
+        a.keys[(int64_t)f * a.rows + r] = a.dict[f] ? a.dict[f][c] : c;
+        if (a.fgid) a.fgid[(int64_t)f * a.rows + r] = a.fgid_col[f];
+      }
+    }
+    for (int64_t r = 0; r < a.rows; ++r) a.labels[r] = (float)a.block[r];
+  }
   void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
                    bool widen) override {
     if (widen) {

@@ -252,6 +252,7 @@ class HipBackend final : public Backend {
     hip::launch_scatter_u32(src, dst, map, n_dev, n_max, stream_);
   }
   void synth_batch(const SynthArgs& a) override { hip::launch_synth(a, stream_); }
+  void unpack_block(const UnpackArgs& a) override { hip::launch_unpack_block(a, stream_); }
   void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
                    bool widen) override {
     hip::launch_field_major(src, dst, rows, F, elem_bytes, widen, stream_);

@@ -53,6 +53,7 @@ void launch_table_nonzero(const TableView& t, const OptSpec& o, unsigned long lo
                           hipStream_t st);
 
 // kernels_layout.hip
+void launch_unpack_block(const UnpackArgs& a, hipStream_t st);
 void launch_field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes, bool widen,
                         hipStream_t st);
 

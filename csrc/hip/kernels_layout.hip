@@ -7,6 +7,8 @@
 // (279 us per 262 144 x 39 block of u64 keys); this kernel stages a tile of
 // kTileRows rows x F fields in LDS with coalesced global reads, then writes
 // each field's kTileRows values as one contiguous run.
+#include <algorithm>
+
 #include "kernels.h"
 #include "hip_util.h"
 
@@ -58,6 +60,49 @@ void launch_field_major(const void* src, void* dst, int64_t rows, int F, int ele
   } else {
     throw std::runtime_error("field_major: 4- or 8-byte elements");
   }
+  XF_HIP_CHECK(hipGetLastError());
+}
+
+// Packed v3 block -> the field-major batch (UnpackArgs).  blockIdx.y = field:
+// one code width and one dictionary per workgroup row, coalesced code reads
+// and key writes; the dictionary gathers hit small tables (a field is
+// dictionary-coded only when it has <= 65536 distinct keys).
+template <typename C>
+__device__ __forceinline__ u64 packed_key(const uint8_t* col, int64_t r, const u64* dict) {
+  const u64 c = (u64)reinterpret_cast<const C*>(col)[r];
+  return dict ? dict[c] : c;
+}
+
+__global__ void __launch_bounds__(kBlock) k_unpack_block(UnpackArgs a) {
+  const int f = blockIdx.y;
+  const uint8_t* col = a.block + a.col_off[f];
+  const u64* dict = a.dict[f];
+  const int w = a.width[f];
+  const int32_t fg = a.fgid_col[f];
+  u64* out = a.keys + (int64_t)f * a.rows;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < a.rows; r += stride) {
+    u64 k;
+    if (w == 1) k = packed_key<uint8_t>(col, r, dict);
+    else if (w == 2) k = packed_key<unsigned short>(col, r, dict);
+    else if (w == 4) k = packed_key<u32>(col, r, dict);
+    else k = packed_key<u64>(col, r, dict);
+    out[r] = k;
+    if (a.fgid) a.fgid[(int64_t)f * a.rows + r] = fg;
+    if (f == 0) a.labels[r] = (float)a.block[r];
+  }
+}
+
+void launch_unpack_block(const UnpackArgs& a, hipStream_t st) {
+  if (a.rows <= 0 || a.F <= 0) return;
+  if (a.F > kMaxPackedFields) throw std::runtime_error("unpack_block: at most 64 fields");
+  for (int f = 0; f < a.F; ++f) {
+    const int w = a.width[f];
+    if ((w != 1 && w != 2 && w != 4 && w != 8) || (a.col_off[f] % w) != 0)
+      throw std::runtime_error("unpack_block: code widths 1/2/4/8, aligned columns");
+  }
+  const int64_t gx = std::min<int64_t>((a.rows + kBlock - 1) / kBlock, 1024);
+  hipLaunchKernelGGL(k_unpack_block, dim3((unsigned)gx, (unsigned)a.F), dim3(kBlock), 0, st, a);
   XF_HIP_CHECK(hipGetLastError());
 }
 

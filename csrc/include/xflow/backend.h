@@ -521,6 +521,26 @@ struct BucketArgs {                // group unique keys by owning rank
   int64_t* scratch = nullptr;      // [2*world] workspace
 };
 
+// A packed block of a v3 .xfb shard (xflow_amd/data/binfmt.py, fixed-width
+// rows): u8 labels, then one column per field of 1/2/4/8-byte codes -- the
+// key itself (direct) or an index into the field's dictionary of u64 keys (a
+// device-resident copy of the shard's dictionaries).  Backend::unpack_block
+// writes the engine's field-major batch from it: half or less of the
+// compact shard's bytes cross the host link, the gathers hit small tables.
+constexpr int kMaxPackedFields = 64;
+struct UnpackArgs {
+  const uint8_t* block = nullptr;          // the block's bytes (backend memory, 16-B aligned)
+  int64_t rows = 0;
+  int F = 0;
+  int width[kMaxPackedFields] = {};        // bytes per code: 1, 2, 4 or 8
+  int64_t col_off[kMaxPackedFields] = {};  // byte offset of field f's column in the block
+  const u64* dict[kMaxPackedFields] = {};  // null: direct keys
+  int32_t fgid_col[kMaxPackedFields] = {}; // the field id of column f
+  u64* keys = nullptr;                     // out [F][rows]
+  float* labels = nullptr;                 // out [rows] (0 / 1)
+  int32_t* fgid = nullptr;                 // out [F][rows], optional
+};
+
 struct SynthArgs {                 // synthetic Criteo-shaped batch generator
   u64* keys = nullptr;
   float* labels = nullptr;
@@ -701,6 +721,8 @@ class Backend {
   // same pass
   virtual void field_major(const void* src, void* dst, int64_t rows, int F, int elem_bytes,
                            bool widen = false) = 0;
+  // packed .xfb block -> field-major keys / labels / fgid (see UnpackArgs)
+  virtual void unpack_block(const UnpackArgs& a) = 0;
   // count occupied slots / dump table rows (checkpointing); returns rows written
   virtual int64_t table_export(const TableView& t, u64* keys_out, u32* words_out,
                                int64_t max_rows) = 0;

@@ -563,6 +563,32 @@ PYBIND11_MODULE(_xflow_native, m) {
         return e.csr_slog2(S) >= 0 && e.backend().csr_exchange();
       })
       .def("w_finish", &Engine::w_finish, py::call_guard<py::gil_scoped_release>())
+      .def("unpack_block",
+           [](Engine& e, uintptr_t block, int64_t rows, std::vector<int> width,
+              std::vector<int64_t> col_off, std::vector<uintptr_t> dict, std::vector<int> fgid_col,
+              uintptr_t keys, uintptr_t labels, uintptr_t fgid) {
+             const size_t F = width.size();
+             if (F == 0 || F > (size_t)kMaxPackedFields || col_off.size() != F || dict.size() != F ||
+                 fgid_col.size() != F)
+               throw std::invalid_argument("unpack_block: one width / offset / dict / fgid per field");
+             UnpackArgs a;
+             a.block = P<const uint8_t>(block);
+             a.rows = rows;
+             a.F = (int)F;
+             for (size_t f = 0; f < F; ++f) {
+               a.width[f] = width[f];
+               a.col_off[f] = col_off[f];
+               a.dict[f] = P<const u64>(dict[f]);
+               a.fgid_col[f] = fgid_col[f];
+             }
+             a.keys = P<u64>(keys);
+             a.labels = P<float>(labels);
+             a.fgid = P<int32_t>(fgid);
+             e.backend().unpack_block(a);
+           },
+           py::arg("block"), py::arg("rows"), py::arg("width"), py::arg("col_off"),
+           py::arg("dict"), py::arg("fgid_col"), py::arg("keys"), py::arg("labels"),
+           py::arg("fgid") = 0, py::call_guard<py::gil_scoped_release>())
       .def("field_major",
            [](Engine& e, uintptr_t src, uintptr_t dst, int64_t rows, int F, int elem_bytes,
               bool widen) {

@@ -39,6 +39,38 @@ def make_shard(path: str, rows: int, fields: int, seed: int, hash_space: int = 0
     binfmt.write(path, labels, np.arange(rows + 1, dtype=np.int64) * fields, keys, fg)
 
 
+def make_criteo_shard(path: str, rows: int, fields: int, seed: int, fmt: str,
+                      block_rows: int) -> dict:
+    """The bench's own synthetic Criteo-1TB-shaped rows (xflow_amd.data.synth:
+    MLPerf cardinalities, 1e9 hashed features) written as an .xfb shard:
+    fmt "v2" (compact u32 keys, CSR) or "packed" (version 3)."""
+    import torch
+
+    from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+    from xflow_amd.data import binfmt
+    from xflow_amd.data.synth import SynthConfig, SyntheticCriteo
+    from xflow_amd.engine import Engine
+
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    chunk = 262144
+    eng = Engine(ModelConfig(), OptimConfig(),
+                 EngineConfig(table_log2_cap=10, max_rows=chunk, max_nnz=chunk * fields), device=dev)
+    gen = SyntheticCriteo(eng, chunk, SynthConfig(seed=seed, n_fields=fields))
+    keys = np.empty((rows, fields), np.uint64)
+    labels = np.empty(rows, np.float32)
+    for r0 in range(0, rows, chunk):
+        n = min(chunk, rows - r0)
+        gen.rows = n
+        b = gen.next(out=SyntheticCriteo(eng, n, gen.cfg).alloc_batch())
+        keys[r0:r0 + n] = b.keys.view(fields, n).t().cpu().numpy().view(np.uint64)
+        labels[r0:r0 + n] = b.labels.cpu().numpy()
+    if fmt == "packed":
+        return binfmt.write_packed(path, labels, keys, block_rows=block_rows)
+    binfmt.write(path, labels, np.arange(rows + 1, dtype=np.int64) * fields, keys.reshape(-1),
+                 np.tile(np.arange(fields, dtype=np.int32), rows), compact="auto")
+    return {"rows": rows, "F": fields, "bytes_per_row": (os.path.getsize(path) / rows)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=4 << 20)
@@ -53,6 +85,12 @@ def main() -> int:
     ap.add_argument("--hash-space", type=int, default=0,
                     help="features hashed into [0, N) (Criteo-1TB: 1e9); N <= 2^32 makes the "
                          "shard compact (u32 keys, half the streamed bytes); 0 = 64-bit keys")
+    ap.add_argument("--data", choices=["zipf", "criteo"], default="zipf",
+                    help="criteo: the bench's synthetic Criteo-1TB shape (data/synth.py; MLPerf "
+                         "cardinalities, 1e9 hashed features)")
+    ap.add_argument("--format", choices=["v2", "packed"], default="v2",
+                    help="--data criteo: the compact CSR shard (v2) or packed field-major "
+                         "blocks with per-field dictionaries (v3)")
     ap.add_argument("--test-rows", type=int, default=65536,
                     help="rows of the test shard rank 0 predicts (pred file + AUC/logloss)")
     a = ap.parse_args()
@@ -68,15 +106,26 @@ def main() -> int:
     t0 = time.perf_counter()
     from xflow_amd.data import binfmt
 
-    want_compact = 0 < a.hash_space <= (1 << 32)
-    if (not os.path.exists(tr) or binfmt.Shard(tr).rows != a.rows
-            or binfmt.Shard(tr).compact != want_compact):
-        make_shard(tr, a.rows, a.fields, 1, a.hash_space)
-    if (not os.path.exists(te) or binfmt.Shard(te).rows != a.test_rows
-            or binfmt.Shard(te).compact != want_compact):
-        make_shard(te, a.test_rows, a.fields, 2, a.hash_space)
+    info = {}
+    if a.data == "criteo":
+        tag = os.path.join(a.dir, "shard.json")
+        want = {"rows": a.rows, "fields": a.fields, "format": a.format, "test_rows": a.test_rows,
+                "block_rows": a.block_rows}
+        if not os.path.exists(tag) or json.load(open(tag)) != want:
+            info = make_criteo_shard(tr, a.rows, a.fields, 1234, a.format, a.block_rows)
+            make_criteo_shard(te, a.test_rows, a.fields, 99, a.format, a.block_rows)
+            json.dump(want, open(tag, "w"))
+    else:
+        want_compact = 0 < a.hash_space <= (1 << 32)
+        if (not os.path.exists(tr) or binfmt.version_of(tr) == binfmt.VERSION_PACKED
+                or binfmt.Shard(tr).rows != a.rows or binfmt.Shard(tr).compact != want_compact):
+            make_shard(tr, a.rows, a.fields, 1, a.hash_space)
+        if (not os.path.exists(te) or binfmt.version_of(te) == binfmt.VERSION_PACKED
+                or binfmt.Shard(te).rows != a.test_rows or binfmt.Shard(te).compact != want_compact):
+            make_shard(te, a.test_rows, a.fields, 2, a.hash_space)
     print(f"shard ready ({time.perf_counter() - t0:.1f}s, "
-          f"{os.path.getsize(tr) / 1e9:.2f} GB)", flush=True)
+          f"{os.path.getsize(tr) / 1e9:.2f} GB, {os.path.getsize(tr) / a.rows:.1f} B/row) {info}",
+          flush=True)
     dev = torch.device("cpu" if a.cpu or not torch.cuda.is_available() else "cuda:0")
     mfile = os.path.join(a.dir, "metrics.jsonl")
     if os.path.exists(mfile):
@@ -96,8 +145,10 @@ def main() -> int:
     wall = t2 - t0
     eps = [json.loads(l) for l in open(mfile) if '"epoch"' in l]
     eps = [e for e in eps if e.get("event") == "epoch"]
-    print(json.dumps({"path": "xfb", "device": str(dev), "rows": a.rows,
-                      "compact_keys": binfmt.Shard(tr).compact,
+    ver = binfmt.version_of(tr)
+    print(json.dumps({"path": "xfb", "device": str(dev), "rows": a.rows, "data": a.data,
+                      "xfb_version": ver, "bytes_per_row": round(os.path.getsize(tr) / a.rows, 1),
+                      "compact_keys": ver == binfmt.VERSION_PACKED or binfmt.Shard(tr).compact,
                       "block_rows": a.block_rows, "resident": a.resident,
                       "fixed_width": not a.csr_only,
                       "samples_per_s_by_epoch": [round(e["samples_per_s"]) for e in eps],

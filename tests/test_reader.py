@@ -336,3 +336,99 @@ def test_compact_xfb_gpu_streamed_equals_wide(gpu_device, tmp_path, csr):
     b = _train_preds(tmp_path / "w", "p", device="cuda", block_rows=512)
     assert len(a) == 1000
     np.testing.assert_array_equal(a, b)
+
+
+def test_packed_xfb_roundtrip_and_training(tmp_path):
+    """Version-3 packed shards (per-field dictionaries as u8 / u16 codes,
+    direct u32 / u64 keys otherwise) expand to exactly the rows written, on
+    the CPU backend's unpack_block, and train bit-identically to the same
+    rows from a v1 shard through the Trainer."""
+    import torch
+
+    from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig, TrainConfig
+    from xflow_amd.data import binfmt
+    from xflow_amd.engine import Engine
+    from xflow_amd.trainer import Trainer
+
+    rng = np.random.default_rng(5)
+    rows, F = 70000, 6
+    keys = np.empty((rows, F), np.uint64)
+    keys[:, 0] = rng.integers(0, 40, rows) * 1000003            # u8 dictionary
+    keys[:, 1] = rng.integers(0, 5000, rows) + (1 << 40)        # u16 dictionary
+    keys[:, 2] = rng.integers(0, 1 << 31, rows)                 # direct u32
+    keys[:, 3] = rng.integers(1 << 40, 1 << 62, rows, dtype=np.uint64)  # direct u64
+    keys[:, 4] = rng.integers(0, 256, rows) * 7919
+    keys[:, 5] = rng.integers(0, 65536, rows) * 31 + 5
+    labels = (rng.random(rows) < 0.3).astype(np.float32)
+    info = binfmt.write_packed(str(tmp_path / "p-00000.xfb"), labels, keys, block_rows=16384)
+    assert info["widths"] == [1, 2, 4, 8, 1, 2], info
+    eng = Engine(ModelConfig(kind="mvm"), OptimConfig(),
+                 EngineConfig(table_log2_cap=12, max_rows=16384, max_nnz=16384 * F))
+    r = binfmt.open_reader(str(tmp_path / "p-00000.xfb"))
+    ks, ls = [], []
+    while True:
+        b = r.next()
+        if b is None:
+            break
+        B = eng.unpack_packed(torch.from_numpy(np.array(b["packed"])), b["rows"], b["shard"],
+                              with_fgid=True)
+        assert B.field_major and B.nnz_per_row == F
+        assert (B.fgid.view(F, -1) == torch.arange(F, dtype=torch.int32).view(F, 1)).all()
+        ks.append(B.keys.view(F, -1).t().numpy().view(np.uint64))
+        ls.append(B.labels.numpy())
+    assert np.array_equal(np.concatenate(ks), keys)
+    assert np.array_equal(np.concatenate(ls), labels)
+    # the same rows as a v1 shard train to the same table
+    binfmt.write(str(tmp_path / "q-00000.xfb"), labels, np.arange(rows + 1) * F, keys.reshape(-1),
+                 np.tile(np.arange(F, dtype=np.int32), rows), compact=False)
+    tables = []
+    for prefix in ("p", "q"):
+        cfg = TrainConfig(train_prefix=str(tmp_path / prefix), test_prefix=str(tmp_path / prefix),
+                          epochs=1, threads=4, block_rows=16384, write_pred=False,
+                          model=ModelConfig(kind="lr"), engine=EngineConfig(table_log2_cap=20))
+        t = Trainer(cfg, device=torch.device("cpu"))
+        t.train_epochs(1)
+        k, w = t.table.export_table()
+        o = np.argsort(k)
+        tables.append((k[o], w.reshape(len(k), -1)[o]))
+        t.close()
+    assert np.array_equal(tables[0][0], tables[1][0])
+    assert np.array_equal(tables[0][1], tables[1][1])
+
+
+@pytest.mark.gpu
+def test_packed_xfb_unpack_on_gpu(gpu_device, tmp_path):
+    """k_unpack_block (csrc/hip/kernels_layout.hip) expands every code width
+    and dictionary mode to the written keys, labels and field ids."""
+    import torch
+
+    from xflow_amd.config import EngineConfig, ModelConfig, OptimConfig
+    from xflow_amd.data import binfmt
+    from xflow_amd.engine import Engine
+
+    rng = np.random.default_rng(9)
+    rows, F = 100000, 5
+    keys = np.empty((rows, F), np.uint64)
+    keys[:, 0] = rng.integers(0, 64, rows) * 77
+    keys[:, 1] = rng.integers(0, 30000, rows) + (1 << 50)
+    keys[:, 2] = rng.integers(0, 1 << 32, rows, dtype=np.uint64)
+    keys[:, 3] = rng.integers(1 << 33, 1 << 63, rows, dtype=np.uint64)
+    keys[:, 4] = rng.integers(0, 3, rows)
+    labels = (rng.random(rows) < 0.25).astype(np.float32)
+    info = binfmt.write_packed(str(tmp_path / "g.xfb"), labels, keys, block_rows=65536)
+    assert info["widths"] == [1, 2, 4, 8, 1]
+    eng = Engine(ModelConfig(kind="mvm"), OptimConfig(),
+                 EngineConfig(table_log2_cap=12, max_rows=65536, max_nnz=65536 * F), device=gpu_device)
+    r = binfmt.open_reader(str(tmp_path / "g.xfb"))
+    ks, ls = [], []
+    while True:
+        b = r.next()
+        if b is None:
+            break
+        B = eng.unpack_packed(torch.from_numpy(np.array(b["packed"])).to(gpu_device), b["rows"],
+                              b["shard"], with_fgid=True)
+        assert (B.fgid.view(F, -1).cpu() == torch.arange(F, dtype=torch.int32).view(F, 1)).all()
+        ks.append(B.keys.view(F, -1).t().cpu().numpy().view(np.uint64))
+        ls.append(B.labels.cpu().numpy())
+    assert np.array_equal(np.concatenate(ks), keys)
+    assert np.array_equal(np.concatenate(ls), labels)

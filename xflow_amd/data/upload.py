@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 _DTYPES = {"keys": torch.int64, "labels": torch.float32, "row_ptr": torch.int32,
-           "fgid": torch.int32}
+           "fgid": torch.int32, "packed": torch.uint8}
 _CHUNK = 4 << 20  # bytes per host-copy task
 
 
@@ -93,7 +93,9 @@ class BlockStream:
                     ev.synchronize()  # the previous H2D from this slot has read it
                 meta = {}
                 t0 = time.perf_counter()
-                for name in self.names:
+                # a packed (v3 .xfb) block is one byte range: one copy, one H2D
+                names = ["packed"] if "packed" in blk else self.names
+                for name in names:
                     a = _np(blk[name])
                     # compact u32 keys travel as int32: half the H2D bytes, widened
                     # on the device (Batch.to_field_major / engine.widen_keys)
@@ -102,10 +104,14 @@ class BlockStream:
                     self._fill(buf.numpy()[:len(a)], a)
                     meta[name] = len(a)
                 self.stage_s += time.perf_counter() - t0
+                if "packed" in blk:
+                    self.ready.put((slot, meta, None, blk["shard"].F,
+                                    {"rows": blk["rows"], "shard": blk["shard"]}))
+                    continue
                 rp = _np(blk["row_ptr"])
                 lens = np.diff(rp) if len(rp) > 1 else np.zeros(0, rp.dtype)
                 F = int(lens[0]) if len(lens) and lens[0] > 0 and np.all(lens == lens[0]) else 0
-                self.ready.put((slot, meta, np.array(rp, copy=True), F))
+                self.ready.put((slot, meta, np.array(rp, copy=True), F, None))
         except BaseException as e:  # surfaced by next()
             self.error = e
         self.ready.put(None)
@@ -118,7 +124,8 @@ class BlockStream:
                 raise self.error
             self.ready.put(None)  # stay exhausted
             return None
-        slot, meta, rp_host, F = item
+        slot, meta, rp_host, F, extra = item
+        names = list(meta)
         compute = torch.cuda.current_stream(self.device)
         # No wait for the compute stream: block t+1's copies run while step t
         # computes.  The pinned slot is reused only after the event behind its
@@ -129,7 +136,7 @@ class BlockStream:
         with torch.cuda.stream(self.copy):
             if self.timeline is not None:
                 self.timeline.begin("h2d", self.copy)
-            for name in self.names:
+            for name in names:
                 out[name] = self.pinned[slot][name][:meta[name]].to(self.device, non_blocking=True)
             if self.timeline is not None:
                 self.timeline.end("h2d", self.copy)
@@ -137,8 +144,12 @@ class BlockStream:
             ev.record(self.copy)
         self.free.put((slot, ev))
         compute.wait_stream(self.copy)
-        for name in self.names:
+        for name in names:
             out[name].record_stream(compute)
+        if extra is not None:  # (packed: expanded by the trainer, Engine.unpack_packed)
+            out.update(extra)
+            out["nnz_per_row"] = F
+            return out
         out["row_ptr_host"] = rp_host
         out["rows"] = len(rp_host) - 1
         out["nnz_per_row"] = F

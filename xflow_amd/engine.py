@@ -375,6 +375,34 @@ class Engine:
             out["row_ptr"].data_ptr(), out["labels"].data_ptr(), int(out["labels"].numel()),
             int(out["keys"].numel()), int(row_mod)))
 
+    def unpack_packed(self, block: torch.Tensor, rows: int, shard, slice_rows: int = 0,
+                      with_fgid: bool = False, used: int = -1) -> Batch:
+        """A packed (version 3) .xfb block -- its raw bytes as a uint8 tensor
+        on this engine's device -- as a field-major Batch (keys expanded from
+        the per-field codes / dictionaries on the device, Backend::unpack_block).
+        used >= 0: only the first `used` rows (the slicing rule's remainder drop)."""
+        if block.device != self.device or block.dtype != torch.uint8:
+            raise ValueError("unpack_packed: uint8 block bytes on the engine's device")
+        F = shard.F
+        dd = shard.device_dicts(self.device)
+        keys = torch.empty(F * rows, dtype=torch.int64, device=self.device)
+        labels = torch.empty(rows, dtype=torch.float32, device=self.device)
+        fgid = torch.empty(F * rows, dtype=torch.int32, device=self.device) if with_fgid else None
+        cols = shard.columns(rows)
+        if block.numel() < cols[-1] + rows * shard.widths[-1]:
+            raise ValueError("unpack_packed: block shorter than its columns")
+        self._sync_stream()
+        self._e.unpack_block(block.data_ptr(), int(rows), list(shard.widths), [int(c) for c in cols],
+                             [dd[f] for f in range(F)], list(shard.fgid_cols), keys.data_ptr(),
+                             labels.data_ptr(), fgid.data_ptr() if fgid is not None else 0)
+        if 0 <= used < rows:  # (field-major: each field's first `used` rows)
+            keys = keys.view(F, rows)[:, :used].contiguous().view(-1)
+            labels = labels[:used]
+            if fgid is not None:
+                fgid = fgid.view(F, rows)[:, :used].contiguous().view(-1)
+        return Batch(keys=keys, labels=labels, fgid=fgid, nnz_per_row=F, slice_rows=slice_rows,
+                     field_major=True)
+
     def count_records(self, on: bool = True) -> None:
         """Count the gradient-reduction records the producers write."""
         self._e.count_records(bool(on))

@@ -129,6 +129,13 @@ class Trainer:
     # ------------------------------------------------------------------ data
     def _to_batch(self, blk: Optional[dict], used: int, slice_rows: int) -> Batch:
         dev = self.device
+        if blk is not None and used > 0 and "packed" in blk:
+            # a packed (v3 .xfb) block: its bytes, expanded on the device
+            p = blk["packed"]
+            if not isinstance(p, torch.Tensor):
+                p = torch.from_numpy(np.array(p)).to(dev)
+            return self.engine.unpack_packed(p, int(blk["rows"]), blk["shard"], slice_rows,
+                                             self._with_fgid, used)
         if blk is not None and used > 0 and isinstance(blk["keys"], torch.Tensor):
             return self._device_batch(blk, used, slice_rows)
         if blk is None or used <= 0:
@@ -206,7 +213,9 @@ class Trainer:
 
     def _slices_of(self, blk: Optional[dict]):
         """Batches of one block: one concurrent step, or one step per slice."""
-        rows = 0 if blk is None else len(blk["labels"])
+        rows = 0 if blk is None else (int(blk["rows"]) if "packed" in blk else len(blk["labels"]))
+        if blk is not None and "packed" in blk and not self.concurrent:
+            raise ValueError("packed .xfb shards train with concurrent slices (not --serial-slices)")
         used, sr = self._split(rows)
         if self.concurrent or blk is None or used <= 0:
             yield self._to_batch(blk, used, sr)
@@ -252,7 +261,7 @@ class Trainer:
                 # (on the CPU backend the same stream parses with reader.cpp's
                 # rules through Engine.parse_text: the multi-rank gloo tests)
                 gpu_text = cfg.gpu_parse and not xfb and self.concurrent
-                reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
+                reader = (binfmt.open_reader(xfb, self.block_rows) if xfb
                           else None if gpu_text
                           else nat.PrefetchReader(path, cfg.train_block_bytes))
                 if gpu_text:
@@ -404,7 +413,7 @@ class Trainer:
         if self.rank == 0:
             tpath = shard_path(cfg.test_prefix, 0)
             xfb = binfmt.shard_file(tpath)
-            reader = (binfmt.ShardReader(xfb, self.block_rows) if xfb
+            reader = (binfmt.open_reader(xfb, self.block_rows) if xfb
                       else nat.BlockReader(tpath, cfg.resolved_test_block()))
         compat_mvm = model_kind(cfg.model.kind) == 2 and cfg.mvm_predict_compat
         aps = self.aps
@@ -419,7 +428,7 @@ class Trainer:
                 blk = reader.next()
                 if blk is None:
                     break
-                used, sr = self._split(len(blk["labels"]))
+                used, sr = self._split(int(blk["rows"]) if "packed" in blk else len(blk["labels"]))
                 if used > 0:
                     break
             if self.sharded is None and blk is None:
