@@ -154,3 +154,24 @@ def test_default_threads_native_cli(tmp_path, hw):
     else:
         assert pred.shape[0] == len(want) == (200 // hw) * hw
         np.testing.assert_allclose(pred[:, 0], [w[1] for w in want], rtol=2e-4, atol=2e-6)
+
+
+def test_mvm_ftrl_liveness_pinned_at_reference_slicing(tmp_path):
+    """MVM-FTRL's liveness, pinned with the oracle at the reference's own
+    slicing (one 2 MB block = the whole 200-row shard, hardware_concurrency = 8
+    slices, mvm_worker.cc:286-296) and init (N(0,1)*1e-2, ftrl.h:114-120):
+    the 17-field product of field sums (~1e-34) is already 0 in float32
+    before any push, so every prediction is exactly 0.5 -- before training
+    and after (the first pushes set v from (z, n), no larger).  The engine
+    reproduces it: the reference's own MVM does not learn on its own data,
+    and bench rows of MVM-FTRL are labelled degenerate for the same reason."""
+    o = oracle.Oracle("mvm", "ftrl", 10, "reference", "compat", 8, v_init)
+    o.init_push()
+    te = oracle.parse_file(TEST + "-00000")
+    assert all(p == 0.5 for _, p in o.predict(te))  # dead at init
+    tr = oracle.parse_file(TRAIN + "-00000")
+    for _ in range(3):
+        o.train_block(tr)
+    assert all(p == 0.5 for _, p in o.predict(te))  # and after three epochs
+    res, pred = run_trainer(tmp_path, "mvm", "ftrl", 3)
+    assert np.all(pred[:, 0] == 0.5)
