@@ -79,3 +79,47 @@ def test_async_ps_gpu_equals_log_replay(tmp_path, kind, fm_math, slices, k, fiel
         keys, words = _table(servers[o])
         assert np.array_equal(keys, live[o]["keys"]), f"owner {o}: key sets differ"
         assert np.array_equal(words, live[o]["words"]), f"owner {o}: state differs from replay"
+
+
+def _trainer_rank(rank, world, data_dir, out_dir):
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
+                      test_prefix=os.path.join(data_dir, "small_test"), epochs=3, threads=4,
+                      pred_dir=out_dir, async_ps=True, staleness=1,
+                      engine=EngineConfig(table_log2_cap=14))
+    t = Trainer(cfg, device=torch.device("cuda", 0))
+    assert t.aps is not None and t.aps.transport.startswith("ipc")
+    res = t.train()
+    np.save(os.path.join(out_dir, f"keys{rank}.npy"), np.sort(t.table.export_table()[0]))
+    if rank == 0:
+        np.save(os.path.join(out_dir, "res.npy"), np.array([res["n"], res["ln_logloss"]]))
+    t.close()
+
+
+def test_async_trainer_two_gpu_processes(tmp_path):
+    """The CLI's --async path (Trainer + asynchronous parameter server) on 2
+    processes sharing GPU 0: both train their shard without meeting, pause at
+    every epoch end, rank 0 predicts over both servers; the two shards hold
+    every key a one-process run holds, each exactly once, and the prediction
+    file is the reference's 200 lines."""
+    from conftest import DATA
+
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    run_world_gpu_gloo(_trainer_rank, 2, DATA, str(tmp_path))
+    k = np.concatenate([np.load(tmp_path / f"keys{r}.npy") for r in range(2)])
+    one = Trainer(TrainConfig(train_prefix=os.path.join(DATA, "small_train"),
+                              test_prefix=os.path.join(DATA, "small_test"), epochs=1,
+                              threads=4, write_pred=False, engine=EngineConfig(table_log2_cap=14)),
+                  device=torch.device("cpu"))
+    one.train()
+    ref = np.sort(one.table.export_table()[0])
+    one.close()
+    assert len(k) == len(np.unique(k)) and np.array_equal(np.sort(k), ref)
+    pred = np.loadtxt(tmp_path / "pred_0_0.txt")
+    assert pred.shape == (200, 3) and np.all((pred[:, 0] > 0) & (pred[:, 0] < 1))
+    n, ll = np.load(tmp_path / "res.npy")
+    assert n == 200 and 0.3 < ll < 1.0
