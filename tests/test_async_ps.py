@@ -83,7 +83,9 @@ def _check_equal(out_dir, world, servers):
 
 
 @pytest.mark.parametrize("kind,slices,k,world", [("lr", 1, 1, 3), ("lr", 4, 0, 2), ("lr", 4, 2, 3),
-                                                 ("fm", 2, 1, 3), ("mvm", 1, 1, 2)])
+                                                 ("fm", 2, 1, 3), ("mvm", 1, 1, 2),
+                                                 # a node's eight ranks: every owner serves 7 peers
+                                                 ("lr", 4, 1, 8)])
 def test_async_tables_equal_log_replay(tmp_path, kind, slices, k, world):
     steps = 5
     run_world(_async_rank, world, kind, slices, k, steps, str(tmp_path), None)
