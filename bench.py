@@ -82,6 +82,15 @@ def parse():
     ap.add_argument("--sgd-v-init", type=float, default=1e-3,
                     help="SGD latent init (sgd.h:69: the constant 0.001); MVM-SGD with 1.0 keeps "
                          "the field product live (FTRL's first push shrinks v by ~|g|)")
+    ap.add_argument("--sgd-lr", type=float, default=1e-3,
+                    help="SGD learning rate (sgd.h:16: 0.001).  The reference's gradient is a "
+                         "mean over the slice's rows, so a 262 144-row slice moves a key by "
+                         "~lr/262144 per occurrence: bench-shape MVM learns at a larger rate")
+    ap.add_argument("--planted-bias", type=float, default=-1.2,
+                    help="synthetic labels' planted logit bias (-1.2: a ~26 %% CTR).  The "
+                         "reference MVM's output sigmoid(sum_k prod_f v_sum) cannot fall "
+                         "below 0.5 once its field sums are positive, so MVM quality rows "
+                         "also run on +1.2 (the same keys, a ~74 %% CTR)")
     ap.add_argument("--fields", type=int, default=39,
                     help="fields (= features) per row: 13 int + (F-13) categorical Criteo fields; "
                          "e.g. 18 like the bundled data (MVM's field product stays live)")
@@ -130,7 +139,7 @@ def run_async(a, world, rank, device, use_gpu, shared_gpu, synth, log2_cap, nnz)
 
     model = ModelConfig(kind=a.model, v_dim=a.v_dim, fm_math=a.fm_math, fm_mfma=a.fm_mfma)
     optim = OptimConfig(kind=a.optimizer, lambda1=a.lambda1, v_init_scale=a.v_init_scale,
-                        sgd_v_init=a.sgd_v_init)
+                        sgd_v_init=a.sgd_v_init, lr=a.sgd_lr)
     cfg = EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
                        max_slices=a.slices, monitor_lag=a.monitor_lag, csr=a.csr == "on")
     aps = AsyncParameterServer(model, optim, cfg, device, staleness=a.staleness,
@@ -275,7 +284,7 @@ def main():
         log2_cap = min(log2_cap, 24)
         a.batch = min(a.batch, 4096)
     synth = SynthConfig(total_features=a.features, hash_space=a.features, seed=a.seed,
-                        n_fields=a.fields)
+                        n_fields=a.fields, planted_bias=a.planted_bias)
     nnz = a.batch * synth.fields
     if a.batch % a.slices:
         raise SystemExit("--batch must be a multiple of --slices")
@@ -283,7 +292,8 @@ def main():
         return run_async(a, world, rank, device, use_gpu, shared_gpu, synth, log2_cap, nnz)
     model = ModelConfig(kind=a.model, v_dim=a.v_dim, fm_math=a.fm_math, fm_mfma=a.fm_mfma)
     engine = Engine(model, OptimConfig(kind=a.optimizer, lambda1=a.lambda1,
-                                       v_init_scale=a.v_init_scale, sgd_v_init=a.sgd_v_init),
+                                       v_init_scale=a.v_init_scale, sgd_v_init=a.sgd_v_init,
+                                       lr=a.sgd_lr),
                     EngineConfig(table_log2_cap=log2_cap, max_rows=a.batch, max_nnz=nnz,
                                  max_slices=a.slices, monitor_lag=a.monitor_lag,
                                  csr=a.csr == "on"),

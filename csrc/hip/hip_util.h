@@ -154,6 +154,12 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ unsigned int wave_sum_u32(unsigned int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // Workgroup-wide sum of a per-lane count, then ONE no-return atomic by lane 0
 // of wave 0.  Bookkeeping counters (table size, dedup claims) are single
 // addresses: per-wave atomics on them serialise at one L2 channel.
