@@ -15,4 +15,5 @@ TAG=r6l_fm2 bash scripts/gpu.sh bench "--model fm --fm-math standard" &&
 TAG=r6l_fm64 bash scripts/gpu.sh bench "--model fm --fm-math standard --slices 64" &&
 TAG=r6l_mvm bash scripts/gpu.sh bench "--model mvm --v-dim 10 --optimizer sgd --sgd-v-init 0.9" &&
 TAG=r6l_prof MARKER=k_synth bash scripts/gpu.sh prof "--model fm --fm-math standard" &&
-bash scripts/r6k.sh
+bash scripts/r6k.sh &&
+bash scripts/r6m.sh
