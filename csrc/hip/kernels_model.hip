@@ -11,6 +11,7 @@
 //   LR   lr_worker.cc:121-143 (loss), :100-119 (gradient)
 //   FM   fm_worker.cc:159-202 (loss), :126-157 (gradient)      [kFmReference]
 //   MVM  mvm_worker.cc:172-218 (loss), :137-170 (gradient)
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 #include "kernels.h"
@@ -205,11 +206,15 @@ struct ColumnAgg {
 
 // Column aggregation for the atomic-free LR backward (PS == 1).  Tags carry
 // the column ((j << 32) | dest), so a table needs no reset between the
-// columns that reuse it; the slots a column claims are appended to a list, so
-// the flush touches only those and writes them densely -- the workgroup's
-// (dest, value) pair region fills column after column without a cursor
-// atomic -- and counts them in the LDS histogram of dest >> kRedShift that
-// drives the reduction kernels below.
+// columns that reuse it.  Per column: every occurrence inserts its dest
+// (claims a slot, or finds it claimed); one that found it claimed adds its
+// values to the slot and marks the slot joined; after the barrier each
+// claimer writes its slot's record -- its own values, plus the slot's sums
+// if joined (then zeroed) -- at an index from the workgroup's running record
+// count, and counts it in the LDS histogram of dest >> kRedShift that drives
+// the reduction kernels below.  A key alone in its column (most of the
+// long-tail occurrences) costs one CAS and one flag read, no accumulator
+// traffic; the flush needs no slot list.
 // NV = values aggregated per key: 1 (LR: Σ loss) or 2 (reference-math FM:
 // Σ loss and Σ loss*vsum, expanded to the 1+D gradient in k_red_sum).
 // Records: NV == 1 -> u64 (dest | value << 32), NV == 2 -> uint3 (dest, v0, v1):
@@ -221,24 +226,30 @@ struct ListAgg {
   static constexpr int kFx = FxBits<NV>::kFx;
   u64 (*tag)[kSlots];
   long long (*acc)[kSlots * NV];  // fixed-point sums (deterministic, see fx_from)
-  unsigned short (*list)[kSlots / 2];
-  u32* nlist;   // [3] list lengths, rotating over columns
+  unsigned short (*list)[kSlots / 2];  // (storage of the joined flags: kSlots bytes per table)
+  u32* nlist;   // [0]: the workgroup's records so far
   u32* hist;    // [red_nb]
   u64* region;  // this workgroup's pair region
-  u32 written;  // pairs written so far (workgroup-uniform)
+  u32 written;  // (unused: total() after the last barrier)
   int shift = kShift;  // bucket = dest >> shift (RedGeom: runtime, >= kShift)
   u32 bad = 0;   // a clamped fixed-point input (see fx_clamp), OR-ed into the stats flag
 
+  __device__ __forceinline__ unsigned char* joined(int t) {
+    return reinterpret_cast<unsigned char*>(&list[t][0]);
+  }
   __device__ __forceinline__ void init(int nb) {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
       tag[0][i] = tag[1][i] = ~0ull;
+      joined(0)[i] = joined(1)[i] = 0;
 #pragma unroll
       for (int v = 0; v < NV; ++v) acc[0][i * NV + v] = acc[1][i * NV + v] = 0ll;
     }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0u;
-    if (threadIdx.x < 3) nlist[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) nlist[0] = 0u;
     written = 0;
   }
+  // records written by the workgroup (after its last column and a barrier)
+  __device__ __forceinline__ u32 total() const { return nlist[0]; }
   // at most kSlots/2 keys per column: the probe terminates
   __device__ __forceinline__ int insert(int t, int j, u32 dest, bool& claimed) {
     const u64 key = ((u64)(u32)j << 32) | dest;
@@ -262,7 +273,6 @@ struct ListAgg {
   __device__ __forceinline__ void column(int j, bool has, u32 dest, float loss,
                                          float loss2 = 0.0f) {
     const int t = j & 1;
-    if (threadIdx.x == 0) nlist[(j + 1) % 3] = 0u;  // last read before the previous barrier
     bool claimed = false;
     int h = 0;
     long long v[NV];
@@ -273,43 +283,86 @@ struct ListAgg {
       v[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
       if constexpr (NV > 1) v[1] = fx_from<kFx>(fx_clamp<kFx>(loss2, bad));
     }
-    if (has) {
+    if (has && !claimed) {
 #pragma unroll
       for (int c = 0; c < NV; ++c)
         atomicAdd(reinterpret_cast<unsigned long long*>(&acc[t][h * NV + c]), (unsigned long long)v[c]);
+      joined(t)[h] = 1;
     }
     const unsigned long long m = __ballot(claimed);
+    u32 idx = 0;
     if (m) {
       const int lane = lane_id();
       const int leader = __ffsll((long long)m) - 1;
       u32 base = 0;
-      if (lane == leader) base = atomicAdd(&nlist[j % 3], (u32)__popcll(m));
-      base = __shfl(base, leader);
-      if (claimed) list[t][base + (u32)__popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)h;
+      if (lane == leader) base = atomicAdd(&nlist[0], (u32)__popcll(m));
+      idx = __shfl(base, leader) + (u32)__popcll(m & ((1ull << lane) - 1ull));
     }
     lds_barrier();
-    const u32 n = nlist[j % 3];
-    for (u32 i = threadIdx.x; i < n; i += blockDim.x) {
-      const int hh = list[t][i];
-      const u32 d = (u32)tag[t][hh];
-      const float v = (float)fx_to_double<kFx>(acc[t][hh * NV]);
-      acc[t][hh * NV] = 0ll;
-      if constexpr (NV == 1) {
-        region[written + i] = (u64)d | ((u64)__float_as_uint(v) << 32);
-      } else {
-        const float v2 = (float)fx_to_double<kFx>(acc[t][hh * NV + 1]);
-        acc[t][hh * NV + 1] = 0ll;
-        reinterpret_cast<uint3*>(region)[written + i] =
-            make_uint3(d, __float_as_uint(v), __float_as_uint(v2));
+    if (claimed) {
+      if (joined(t)[h]) {
+        joined(t)[h] = 0;
+#pragma unroll
+        for (int c = 0; c < NV; ++c) {
+          v[c] += acc[t][h * NV + c];
+          acc[t][h * NV + c] = 0ll;
+        }
       }
-      XF_DASSERT((int)(d >> shift) < kRedMaxBuckets);
-      atomicAdd(&hist[d >> shift], 1u);
+      const float v0 = (float)fx_to_double<kFx>(v[0]);
+      if constexpr (NV == 1) {
+        region[idx] = (u64)dest | ((u64)__float_as_uint(v0) << 32);
+      } else {
+        const float v1 = (float)fx_to_double<kFx>(v[1]);
+        reinterpret_cast<uint3*>(region)[idx] =
+            make_uint3(dest, __float_as_uint(v0), __float_as_uint(v1));
+      }
+      XF_DASSERT((int)(dest >> shift) < kRedMaxBuckets);
+      atomicAdd(&hist[dest >> shift], 1u);
     }
-    written += n;
   }
 };
 
 constexpr int ilog2c(int v) { return v <= 1 ? 0 : 1 + ilog2c(v / 2); }
+
+// A row's dedup positions, column by column, kPosChunk columns per load
+// batch: a chunk's loads are issued together (one memory latency per chunk)
+// and the next chunk's are issued before this chunk's columns run, so the
+// column walks below -- a chain of LDS round trips and barriers per column --
+// never wait on a global load.  (A load issued and consumed inside the walk
+// costs a full memory latency per column: the barriers' memory clobber keeps
+// the compiler from hoisting it, and the records' conditional stores make its
+// vmcnt wait a vmcnt(0).)  Every lane loads from a valid address (pos[0]
+// outside its row) and the row bounds select trash_pos at the use.
+constexpr int kPosChunk = 8;
+struct PosStream {
+  const u32* __restrict__ pos;
+  RowSpan rs;
+  int len;
+  u32 trash;
+  u32 cur[kPosChunk], nxt[kPosChunk];
+  u32 okc = 0, okn = 0;
+  __device__ __forceinline__ PosStream(const u32* p, const RowSpan& r, int n, u32 tr,
+                                       bool prime = true)
+      : pos(p), rs(r), len(n), trash(tr) {
+    if (prime) fetch(cur, okc, 0);
+  }
+  __device__ __forceinline__ void fetch(u32 (&dst)[kPosChunk], u32& ok, int j0) const {
+    ok = 0u;
+#pragma unroll
+    for (int q = 0; q < kPosChunk; ++q) {
+      const bool v = j0 + q < len;
+      dst[q] = pos[v ? rs.at(j0 + q) : 0];
+      ok |= (u32)v << q;
+    }
+  }
+  __device__ __forceinline__ void prefetch(int j0) { fetch(nxt, okn, j0); }
+  __device__ __forceinline__ u32 get(int q) const { return (okc >> q) & 1u ? cur[q] : trash; }
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int q = 0; q < kPosChunk; ++q) cur[q] = nxt[q];
+    okc = okn;
+  }
+};
 
 // Rows of at most kLrRegCols features keep their dedup positions in registers:
 // every pos load of a row is issued before the first use (one memory latency
@@ -443,11 +496,19 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
       if constexpr (!kAgg) {
         for (int j = 0; j < len; ++j) atomicAdd(&a.grad[pos[rs.at(j)] * S + s], loss);
       } else {
-        for (int j = 0; j < maxlen; ++j) {
-          const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
-          const u32 dest = pj * S + s;
-          if constexpr (kRed) lagg.column(j, pj != a.trash_pos, dest, loss);
-          else lr_column<LOG2>(agg, j, j < len, dest, loss, a.grad);
+        PosStream ps(pos, rs, len, a.trash_pos);
+        for (int j0 = 0; j0 < maxlen; j0 += kPosChunk) {
+          ps.prefetch(j0 + kPosChunk);
+#pragma unroll
+          for (int q = 0; q < kPosChunk; ++q) {
+            const int j = j0 + q;
+            if (j >= maxlen) break;
+            const u32 pj = ps.get(q);
+            const u32 dest = pj * S + s;
+            if constexpr (kRed) lagg.column(j, pj != a.trash_pos, dest, loss);
+            else lr_column<LOG2>(agg, j, j < len, dest, loss, a.grad);
+          }
+          ps.advance();
         }
       }
     }
@@ -455,8 +516,8 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   if constexpr (kRed) {
     __syncthreads();
     if (threadIdx.x == 0) {
-      a.red_count[blockIdx.x] = lagg.written;
-      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.written);
+      a.red_count[blockIdx.x] = lagg.total();
+      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.total());
     }
     for (int i = threadIdx.x, n = red_active(a, red_shift(1)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
@@ -1307,14 +1368,21 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
   const u32 S = (u32)a.S;
   const float lv = loss * vsum;
-  for (int j = 0; j < maxlen; ++j) {
-    const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
-    lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
+  PosStream ps(pos, rs, len, a.trash_pos);
+  for (int j0 = 0; j0 < maxlen; j0 += kPosChunk) {
+    ps.prefetch(j0 + kPosChunk);
+#pragma unroll
+    for (int q = 0; q < kPosChunk; ++q) {
+      if (j0 + q >= maxlen) break;
+      const u32 pj = ps.get(q);
+      lagg.column(j0 + q, pj != a.trash_pos, pj * S + s, loss, lv);
+    }
+    ps.advance();
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-      a.red_count[blockIdx.x] = lagg.written;
-      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.written);
+      a.red_count[blockIdx.x] = lagg.total();
+      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.total());
     }
   for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
     a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];
@@ -1353,8 +1421,26 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
 // kScaled (MVM): T = loss*M spans many orders of magnitude (a product over
 // fields), beyond any one static fixed-point scale: the int64 sums use the
 // step's scale (fx_scale_bits of FwdArgs::red_vmax, set by the forward).
+// Diagnostic build only (-DXFLOW_KTIMING): per-phase shader-clock cycles of
+// the standard-FM producer, summed over waves (lane 0 of each wave adds its
+// deltas), printed every 25 launches by launch_fmstd_reduction.
+#ifdef XFLOW_KTIMING
+__device__ unsigned long long g_ktime[16];
+#define XF_KT_DECL unsigned long long kt_ = clock64()
+#define XF_KT(p)                                                          \
+  do {                                                                    \
+    const unsigned long long n_ = clock64();                              \
+    if (lane_id() == 0) atomicAdd(&g_ktime[p], n_ - kt_);                 \
+    kt_ = n_;                                                             \
+  } while (0)
+#else
+#define XF_KT_DECL (void)0
+#define XF_KT(p) (void)0
+#endif
+
 template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kScaled = false>
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
+  XF_KT_DECL;
   constexpr int PS = fm_ps(D);
   constexpr int NV = 1 + D;
   static_assert(BLOCK == fmstd_block(D), "producer block");
@@ -1416,6 +1502,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 #pragma unroll
     for (int w = 0; w < BLOCK / kWave; ++w) maxlen = max(maxlen, s_wmax[w]);
   }
+  XF_KT(0);
   const u32 S = (u32)a.S;
   const u32 sl = active ? (u32)slice_of(b, r, a.S) : 0u;
   // kSplit: the row's vector (FM: loss, loss*vs_k; MVM: T_k = loss*M_k); a
@@ -1443,9 +1530,14 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   }
   if constexpr (kSeg) {
     // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (the cursors)
-    for (int j = 0; j < len && live; ++j) {
-      const u32 pj = pos[rs.at(j)];
-      if (pj != a.trash_pos) atomicAdd(&s_hist[(pj * S + sl) >> shift], 1u);
+    const PosStream pp(pos, rs, live ? len : 0, a.trash_pos, false);
+    for (int j0 = 0; j0 < maxlen; j0 += kPosChunk) {
+      u32 pv[kPosChunk], ok;
+      pp.fetch(pv, ok, j0);
+#pragma unroll
+      for (int q = 0; q < kPosChunk; ++q)
+        if (((ok >> q) & 1u) && pv[q] != a.trash_pos)
+          atomicAdd(&s_hist[(pv[q] * S + sl) >> shift], 1u);
     }
     __syncthreads();
     constexpr int kPer = kMaxB / BLOCK;
@@ -1471,6 +1563,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     }
     __syncthreads();
   }
+  XF_KT(1);
   StatAcc st;
   float loss = 0.0f;
   float vs[D];  // (kSplit: loss*vs_k)
@@ -1511,9 +1604,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   }
   const int lane = lane_id();
   u32 written = 0, bad = 0;
-  // the next column's position is loaded before this column's barriers, so
-  // the column walk waits on no global load
-  u32 pnext = 0 < len && live ? pos[rs.at(0)] : a.trash_pos;
+  // the column walk's positions arrive a chunk ahead (PosStream)
+  PosStream ps(pos, rs, live ? len : 0, a.trash_pos);
   // the row's fixed-point values, the same for every column: converted once
   // (factorised: Σ loss*(vs_k - v_k) = C_k - v_k*B with B = Σ loss and C_k =
   // Σ loss*vs_k -- v_k is the key's pulled value, one per step -- so the
@@ -1561,88 +1653,99 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   // values plus, if joined, the slot's sums (then zeroed for the next column).
   // A key alone in its column (25-35 % of the occurrences at the Criteo
   // shape) costs one CAS and one flag read: no accumulator traffic at all.
-  for (int j = 0; j < maxlen; ++j) {
-    const int t = 0;
-    const u32 pj = pnext;
-    pnext = j + 1 < len && live ? pos[rs.at(j + 1)] : a.trash_pos;
-    const bool has = pj != a.trash_pos;
-    const u32 dest = pj * S + sl;
-    bool claimed = false;
-    u32 h = 0;
-    if (has) {
-      const u64 key = ((u64)(u32)j << 32) | dest;
-      h = (u32)(((u64)(dest * 0x9E3779B1u) * kSlots) >> 32);
-      while (true) {  // <= BLOCK keys per column in > BLOCK slots: terminates
-        const u64 cur = s_tag[t][h];
-        if (cur == key) break;
-        if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
-          const u64 old = atomicCAS((unsigned long long*)&s_tag[t][h], (unsigned long long)cur,
-                                    (unsigned long long)key);
-          if (old == cur) {
-            claimed = true;
-            break;
+  XF_KT(2);
+  for (int j0 = 0; j0 < maxlen; j0 += kPosChunk) {
+    ps.prefetch(j0 + kPosChunk);
+#pragma unroll
+    for (int q = 0; q < kPosChunk; ++q) {
+      if (j0 + q >= maxlen) break;
+      const int j = j0 + q;
+      const int t = 0;
+      const u32 pj = ps.get(q);
+      const bool has = pj != a.trash_pos;
+      const u32 dest = pj * S + sl;
+      bool claimed = false;
+      u32 h = 0;
+      if (has) {
+        const u64 key = ((u64)(u32)j << 32) | dest;
+        h = (u32)(((u64)(dest * 0x9E3779B1u) * kSlots) >> 32);
+        while (true) {  // <= BLOCK keys per column in > BLOCK slots: terminates
+          const u64 cur = s_tag[t][h];
+          if (cur == key) break;
+          if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
+            const u64 old = atomicCAS((unsigned long long*)&s_tag[t][h], (unsigned long long)cur,
+                                      (unsigned long long)key);
+            if (old == cur) {
+              claimed = true;
+              break;
+            }
+            if (old == key) break;
           }
-          if (old == key) break;
+          h = h + 1 == kSlots ? 0u : h + 1;
         }
-        h = h + 1 == kSlots ? 0u : h + 1;
       }
-    }
-    if (has && !claimed) {
-      Acc* acc = &s_acc[t][h * NV];
-#pragma unroll
-      for (int c = 0; c < NV; ++c) {
-        if constexpr (kScaled)
-          atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)rowv[c]);
-        else
-          atomicAdd(&acc[c], rowv[c]);
-      }
-      s_join[h] = 1;
-    }
-    u32 idx = 0;
-    if constexpr (!kSeg) {  // the record's index in the workgroup region
-      const unsigned long long m = __ballot(claimed);
-      if (m) {
-        const int leader = __ffsll((long long)m) - 1;
-        u32 base = 0;
-        if (lane == leader) base = atomicAdd(&s_total, (u32)__popcll(m));
-        idx = __shfl(base, leader) + (u32)__popcll(m & ((1ull << lane) - 1ull));
-      }
-    }
-    lds_barrier();
-    if (claimed) {
-      Acc* acc = &s_acc[t][h * NV];
-      Acc sum[NV];
-#pragma unroll
-      for (int c = 0; c < NV; ++c) sum[c] = rowv[c];
-      if (s_join[h]) {
-        s_join[h] = 0;
+      if (has && !claimed) {
+        Acc* acc = &s_acc[t][h * NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) {
-          sum[c] += acc[c];
-          acc[c] = (Acc)0;
+          if constexpr (kScaled)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&acc[c]), (unsigned long long)rowv[c]);
+          else
+            atomicAdd(&acc[c], rowv[c]);
+        }
+        s_join[h] = 1;
+      }
+      u32 idx = 0;
+      if constexpr (!kSeg) {  // the record's index in the workgroup region
+        const unsigned long long m = __ballot(claimed);
+        if (m) {
+          const int leader = __ffsll((long long)m) - 1;
+          u32 base = 0;
+          if (lane == leader) base = atomicAdd(&s_total, (u32)__popcll(m));
+          idx = __shfl(base, leader) + (u32)__popcll(m & ((1ull << lane) - 1ull));
         }
       }
-      u32 wv[W];
-      wv[0] = dest;
+      XF_KT(3);
+      lds_barrier();
+      XF_KT(4);
+      if (claimed) {
+        Acc* acc = &s_acc[t][h * NV];
+        Acc sum[NV];
 #pragma unroll
-      for (int c = 0; c < NV; ++c)
-        wv[1 + c] = __float_as_uint(kScaled ? (float)fx_to_double_rt((long long)sum[c], fxs)
-                                            : (float)ldexp((double)sum[c], -s_fxc[c]));
+        for (int c = 0; c < NV; ++c) sum[c] = rowv[c];
+        if (s_join[h]) {
+          s_join[h] = 0;
 #pragma unroll
-      for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
-      Rec rec;
+          for (int c = 0; c < NV; ++c) {
+            sum[c] += acc[c];
+            acc[c] = (Acc)0;
+          }
+        }
+        u32 wv[W];
+        wv[0] = dest;
 #pragma unroll
-      for (int q = 0; q < W / 4; ++q)
-        rec.q[q] = make_uint4(wv[4 * q], wv[4 * q + 1], wv[4 * q + 2], wv[4 * q + 3]);
-      if constexpr (kSeg) {
-        region[atomicAdd(&s_hist[dest >> shift], 1u)] = rec;
-        ++written;
-      } else {
-        region[idx] = rec;
-        atomicAdd(&s_hist[dest >> shift], 1u);
+        for (int c = 0; c < NV; ++c)
+          wv[1 + c] = __float_as_uint(kScaled ? (float)fx_to_double_rt((long long)sum[c], fxs)
+                                              : (float)ldexp((double)sum[c], -s_fxc[c]));
+#pragma unroll
+        for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
+        Rec rec;
+#pragma unroll
+        for (int u = 0; u < W / 4; ++u)
+          rec.q[u] = make_uint4(wv[4 * u], wv[4 * u + 1], wv[4 * u + 2], wv[4 * u + 3]);
+        if constexpr (kSeg) {
+          region[atomicAdd(&s_hist[dest >> shift], 1u)] = rec;
+          ++written;
+        } else {
+          region[idx] = rec;
+          atomicAdd(&s_hist[dest >> shift], 1u);
+        }
       }
+      XF_KT(5);
+      lds_barrier();  // (one table: flushed before the next column inserts)
+      XF_KT(6);
     }
-    lds_barrier();  // (one table: flushed before the next column inserts)
+    ps.advance();
   }
   if constexpr (kSeg) {  // (the non-kSeg count is s_total already)
     const u32 wsum = wave_sum_u32(written);
@@ -1662,6 +1765,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   }
   st.bad |= bad;
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
+  XF_KT(7);
+#ifdef XFLOW_KTIMING
+  if (lane_id() == 0) atomicAdd(&g_ktime[15], 1ull);
+#endif
 }
 
 // Sums of a bucket's vector records: units of kR dests (as k_red_sum) with
@@ -2210,6 +2317,20 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
       throw std::runtime_error("CSR vector reduction: split scatter-free form, unique positions, "
                                "S = 2^slog2 <= 2^shift, full-row entries (MVM: dup records)");
   }
+#ifdef XFLOW_KTIMING
+  {
+    static int calls = 0;
+    if (++calls % 25 == 0) {
+      unsigned long long t[16];
+      XF_HIP_CHECK(hipStreamSynchronize(st));
+      XF_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_ktime), sizeof(t)));
+      const double w = (double)(t[15] ? t[15] : 1);
+      std::fprintf(stderr, "[ktime] waves %llu  cycles/wave: init %.0f prepass %.0f rowv %.0f | "
+                   "insert %.0f bar1 %.0f flush %.0f bar2 %.0f | tail %.0f\n", t[15], t[0] / w,
+                   t[1] / w, t[2] / w, t[3] / w, t[4] / w, t[5] / w, t[6] / w, t[7] / w);
+    }
+  }
+#endif
   if (split && !kMvm)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a);
@@ -2345,14 +2466,21 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
     const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
     const u32 S = (u32)a.S;
     const float lv = loss * vsum;
-    for (int j = 0; j < maxlen; ++j) {
-      const u32 pj = j < len ? pos[rs.at(j)] : a.trash_pos;
-      lagg.column(j, pj != a.trash_pos, pj * S + s, loss, lv);
+    PosStream ps(pos, rs, len, a.trash_pos);
+    for (int j0 = 0; j0 < maxlen; j0 += kPosChunk) {
+      ps.prefetch(j0 + kPosChunk);
+#pragma unroll
+      for (int q = 0; q < kPosChunk; ++q) {
+        if (j0 + q >= maxlen) break;
+        const u32 pj = ps.get(q);
+        lagg.column(j0 + q, pj != a.trash_pos, pj * S + s, loss, lv);
+      }
+      ps.advance();
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      a.red_count[blockIdx.x] = lagg.written;
-      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.written);
+      a.red_count[blockIdx.x] = lagg.total();
+      if (a.red_records) atomicAdd(a.red_records, (unsigned long long)lagg.total());
     }
     for (int i = threadIdx.x, n = red_active(a, red_shift(2)); i < n; i += BLOCK)
       a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i];

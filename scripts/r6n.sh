@@ -1,7 +1,7 @@
 #!/bin/bash
-# claimer-flushed ListAgg (LR / reference FM / MVM column producers): GPU
-# tests on the in-tree build, same-box A/B against the previous build, and
-# the LR step's kernel stats
+# claimer-flushed ListAgg (lrcf) and chunk-prefetched column positions (pos,
+# on top of lrcf): GPU tests on the in-tree build (= pos), then same-box A/B
+# against the previous build (base) for LR, reference FM, standard FM, MVM
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -11,6 +11,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method threa
     tests/test_many_slices.py tests/test_plan_paths.py tests/test_parity_reference.py \
     > gpurun_out/r6n/tests.log 2>&1 &&
 tail -2 gpurun_out/r6n/tests.log &&
-TAG=r6n_ab ROUNDS=3 bash scripts/gpu.sh ab "base lrcf" "" &&
-TAG=r6n_abfm ROUNDS=2 bash scripts/gpu.sh ab "base lrcf" "--model fm" &&
-TAG=r6n_prof bash scripts/gpu.sh prof ""
+STEPS=20 TAG=r6n_lr ROUNDS=2 bash scripts/gpu.sh ab "base lrcf pos" "" &&
+STEPS=20 TAG=r6n_fm ROUNDS=2 bash scripts/gpu.sh ab "base lrcf pos" "--model fm" &&
+STEPS=20 TAG=r6n_fms ROUNDS=2 bash scripts/gpu.sh ab "base pos" "--model fm --fm-math standard" &&
+STEPS=20 TAG=r6n_mvm ROUNDS=2 bash scripts/gpu.sh ab "base lrcf pos" "--model mvm --v-dim 10 --optimizer sgd --sgd-v-init 0.9"

@@ -26,7 +26,10 @@ BUILD = os.path.join(ROOT, "build")
 # XFLOW_DEVICE_ASSERT=1: debug build with device-side bounds asserts
 # (XF_DASSERT in csrc/hip/hip_util.h); objects go to their own directory
 DEVICE_ASSERT = os.environ.get("XFLOW_DEVICE_ASSERT", "0") not in ("", "0")
-OBJ = os.path.join(BUILD, "obj-dassert" if DEVICE_ASSERT else "obj")
+# XFLOW_KTIMING=1: diagnostic build with per-phase cycle counters in the
+# standard-FM producer (XF_KT in csrc/hip/kernels_model.hip), own directory
+KTIMING = os.environ.get("XFLOW_KTIMING", "0") not in ("", "0")
+OBJ = os.path.join(BUILD, "obj-dassert" if DEVICE_ASSERT else ("obj-ktime" if KTIMING else "obj"))
 PKG = os.path.join(ROOT, "xflow_amd")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("XFLOW_OFFLOAD_ARCH", "gfx950")
@@ -40,7 +43,8 @@ COMMON_FLAGS = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "
 # backend and the reference (no silent FMA contraction).
 HIP_FLAGS = ["--offload-arch=" + ARCH, "-ffp-contract=off", "-mcode-object-version=5",
              "-I" + os.path.join(CSRC, "hip"), "-Wno-unused-result"] + \
-            (["-DXFLOW_DEVICE_ASSERT=1"] if DEVICE_ASSERT else [])
+            (["-DXFLOW_DEVICE_ASSERT=1"] if DEVICE_ASSERT else []) + \
+            (["-DXFLOW_KTIMING=1"] if KTIMING else [])
 
 HOST_SOURCES = ["io/reader.cpp", "cpu/cpu_backend.cpp", "engine/engine.cpp", "engine/trainer.cpp"]
 
