@@ -204,17 +204,18 @@ struct ColumnAgg {
   }
 };
 
-// Column aggregation for the atomic-free LR backward (PS == 1).  Tags carry
-// the column ((j << 32) | dest), so a table needs no reset between the
-// columns that reuse it.  Per column: every occurrence inserts its dest
-// (claims a slot, or finds it claimed); one that found it claimed adds its
-// values to the slot and marks the slot joined; after the barrier each
-// claimer writes its slot's record -- its own values, plus the slot's sums
-// if joined (then zeroed) -- at an index from the workgroup's running record
-// count, and counts it in the LDS histogram of dest >> kRedShift that drives
-// the reduction kernels below.  A key alone in its column (most of the
-// long-tail occurrences) costs one CAS and one flag read, no accumulator
-// traffic; the flush needs no slot list.
+// Column aggregation for the atomic-free LR backward (PS == 1), double
+// buffered (column j uses table j & 1, one barrier per column).  Per column:
+// every occurrence inserts its dest -- one CAS against kFree per probe step --
+// and so claims a slot or finds it claimed; one that found it claimed adds
+// its values to the slot and marks it joined; a claimer takes its record's
+// index from the workgroup's running count and counts it in the LDS histogram
+// of dest >> kRedShift that drives the reduction kernels below.  After the
+// barrier each claimer frees its slot and writes its record -- its own
+// values, plus the slot's sums if joined (then zeroed) -- so the table is
+// empty again when column j + 2 reuses it.  A key alone in its column (most
+// of the long-tail occurrences) costs one CAS, one flag read and one tag
+// write: no accumulator traffic, no slot list.
 // NV = values aggregated per key: 1 (LR: Σ loss) or 2 (reference-math FM:
 // Σ loss and Σ loss*vsum, expanded to the 1+D gradient in k_red_sum).
 // Records: NV == 1 -> u64 (dest | value << 32), NV == 2 -> uint3 (dest, v0, v1):
@@ -224,7 +225,8 @@ struct ListAgg {
   static constexpr int kSlots = 1 << LOG2;
   static constexpr int kShift = red_shift(NV);
   static constexpr int kFx = FxBits<NV>::kFx;
-  u64 (*tag)[kSlots];
+  static constexpr u32 kFree = 0xffffffffu;  // (no dest: dest < trash_pos * S)
+  u32 (*tag)[kSlots];
   long long (*acc)[kSlots * NV];  // fixed-point sums (deterministic, see fx_from)
   unsigned short (*list)[kSlots / 2];  // (storage of the joined flags: kSlots bytes per table)
   u32* nlist;   // [0]: the workgroup's records so far
@@ -239,7 +241,7 @@ struct ListAgg {
   }
   __device__ __forceinline__ void init(int nb) {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
-      tag[0][i] = tag[1][i] = ~0ull;
+      tag[0][i] = tag[1][i] = kFree;
       joined(0)[i] = joined(1)[i] = 0;
 #pragma unroll
       for (int v = 0; v < NV; ++v) acc[0][i * NV + v] = acc[1][i * NV + v] = 0ll;
@@ -250,22 +252,16 @@ struct ListAgg {
   }
   // records written by the workgroup (after its last column and a barrier)
   __device__ __forceinline__ u32 total() const { return nlist[0]; }
-  // at most kSlots/2 keys per column: the probe terminates
-  __device__ __forceinline__ int insert(int t, int j, u32 dest, bool& claimed) {
-    const u64 key = ((u64)(u32)j << 32) | dest;
+  // at most kSlots/2 keys per column in an empty table: the probe terminates
+  __device__ __forceinline__ int insert(int t, u32 dest, bool& claimed) {
     u32 h = (dest * 0x9E3779B1u) >> (32 - LOG2);
     while (true) {
-      const u64 cur = tag[t][h];
-      if (cur == key) return (int)h;
-      if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
-        const u64 old = atomicCAS((unsigned long long*)&tag[t][h], (unsigned long long)cur,
-                                  (unsigned long long)key);
-        if (old == cur) {
-          claimed = true;
-          return (int)h;
-        }
-        if (old == key) return (int)h;
+      const u32 old = atomicCAS(&tag[t][h], kFree, dest);
+      if (old == kFree) {
+        claimed = true;
+        return (int)h;
       }
+      if (old == dest) return (int)h;
       h = (h + 1) & (kSlots - 1);
     }
   }
@@ -279,7 +275,7 @@ struct ListAgg {
     v[0] = 0ll;
     if constexpr (NV > 1) v[1] = 0ll;
     if (has) {
-      h = insert(t, j, dest, claimed);
+      h = insert(t, dest, claimed);
       v[0] = fx_from<kFx>(fx_clamp<kFx>(loss, bad));
       if constexpr (NV > 1) v[1] = fx_from<kFx>(fx_clamp<kFx>(loss2, bad));
     }
@@ -298,8 +294,13 @@ struct ListAgg {
       if (lane == leader) base = atomicAdd(&nlist[0], (u32)__popcll(m));
       idx = __shfl(base, leader) + (u32)__popcll(m & ((1ull << lane) - 1ull));
     }
+    if (claimed) {
+      XF_DASSERT((int)(dest >> shift) < kRedMaxBuckets);
+      atomicAdd(&hist[dest >> shift], 1u);
+    }
     lds_barrier();
     if (claimed) {
+      tag[t][h] = kFree;
       if (joined(t)[h]) {
         joined(t)[h] = 0;
 #pragma unroll
@@ -316,8 +317,6 @@ struct ListAgg {
         reinterpret_cast<uint3*>(region)[idx] =
             make_uint3(dest, __float_as_uint(v0), __float_as_uint(v1));
       }
-      XF_DASSERT((int)(dest >> shift) < kRedMaxBuckets);
-      atomicAdd(&hist[dest >> shift], 1u);
     }
   }
 };
@@ -394,7 +393,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   __shared__ float s_acc[kCol ? 2 : 1][kCol ? (1 << LOG2) : 1];
   __shared__ long long s_fx[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
   __shared__ int s_wmax[BLOCK / kWave];
-  __shared__ u64 s_tag64[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
+  __shared__ u32 s_tag32[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
   __shared__ unsigned short s_list[kRed ? 2 : 1][kRed ? BLOCK : 1];
   __shared__ u32 s_hist[kRed ? kRedMaxBuckets : 1];
   __shared__ u32 s_nlist[3];
@@ -410,7 +409,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   ColumnAgg<1, LOG2> agg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag[0][0]),
                          reinterpret_cast<float(*)[1 << LOG2]>(&s_acc[0][0])};
   if constexpr (kCol) agg.init();
-  ListAgg<LOG2> lagg{reinterpret_cast<u64(*)[1 << LOG2]>(&s_tag64[0][0]),
+  ListAgg<LOG2> lagg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag32[0][0]),
                      reinterpret_cast<long long(*)[1 << LOG2]>(&s_fx[0][0]),
                      reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
                      s_nlist, s_hist, nullptr, 0u};
@@ -1299,7 +1298,7 @@ template <int D, int BLOCK>
 __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   constexpr int PS = fm_ps(D);
   constexpr int LOG2 = ilog2c(2 * BLOCK);
-  __shared__ u64 s_tag64[2][1 << LOG2];
+  __shared__ u32 s_tag32[2][1 << LOG2];
   __shared__ long long s_acc[2][(1 << LOG2) * 2];
   __shared__ unsigned short s_list[2][BLOCK];
   __shared__ u32 s_hist[kRedMaxBuckets];
@@ -1317,7 +1316,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
   u64* region = reinterpret_cast<u64*>(reinterpret_cast<uint3*>(a.red_pairs) +
                                        (b.row_ptr ? (int64_t)b.row_ptr[r0]
                                                   : r0 * b.nnz_per_row));
-  ListAgg<LOG2, 2> lagg{s_tag64, s_acc, s_list, s_nlist, s_hist, region, 0u};
+  ListAgg<LOG2, 2> lagg{s_tag32, s_acc, s_list, s_nlist, s_hist, region, 0u};
   lagg.init(red_active(a, red_shift(2)));
   lagg.shift = red_geom(a).shift(red_shift(2));
   int maxlen;
@@ -1426,16 +1425,26 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
 // deltas), printed every 25 launches by launch_fmstd_reduction.
 #ifdef XFLOW_KTIMING
 __device__ unsigned long long g_ktime[16];
-#define XF_KT_DECL unsigned long long kt_ = clock64()
-#define XF_KT(p)                                                          \
-  do {                                                                    \
-    const unsigned long long n_ = clock64();                              \
-    if (lane_id() == 0) atomicAdd(&g_ktime[p], n_ - kt_);                 \
-    kt_ = n_;                                                             \
+#define XF_KT_DECL                  \
+  unsigned long long kt_acc_[8] = {}; \
+  unsigned long long kt_ = clock64()
+#define XF_KT(p)                                  \
+  do {                                            \
+    const unsigned long long n_ = clock64();      \
+    kt_acc_[p] += n_ - kt_;                       \
+    kt_ = n_;                                     \
+  } while (0)
+#define XF_KT_FLUSH()                                                    \
+  do {                                                                   \
+    if (lane_id() == 0) {                                                \
+      for (int p_ = 0; p_ < 8; ++p_) atomicAdd(&g_ktime[p_], kt_acc_[p_]); \
+      atomicAdd(&g_ktime[15], 1ull);                                     \
+    }                                                                    \
   } while (0)
 #else
 #define XF_KT_DECL (void)0
 #define XF_KT(p) (void)0
+#define XF_KT_FLUSH() (void)0
 #endif
 
 template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kScaled = false>
@@ -1446,6 +1455,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   static_assert(BLOCK == fmstd_block(D), "producer block");
   // (not a power of two: 2.75 x BLOCK at D = 8 with int32 sums)
   constexpr u32 kSlots = (u32)(kScaled ? fmstd_slots(D) : fmstd_slots32(D));
+  constexpr u32 kFree = 0xffffffffu;  // (no dest: dest < trash_pos * S)
   constexpr int kFx = FxBits<1>::kFx;
   // Column accumulators.  kScaled (MVM): int64 at the step's scale.  Else
   // int32 at a per-workgroup, per-component scale: a column adds at most one
@@ -1455,7 +1465,8 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   // random-slot atomics were 64 % bank-conflict cycles, profiles/r5_fmstd_pmc.txt).
   // Order-free integer sums either way: deterministic.
   using Acc = typename std::conditional<kScaled, long long, int>::type;
-  __shared__ u64 s_tag[1][kSlots];
+  // slot tags: the claiming dest, kFree once its claimer has flushed it
+  __shared__ u32 s_tag[kSlots];
   __shared__ Acc s_acc[1][kSlots * NV];
   __shared__ int s_fxc[NV];
   __shared__ float s_cmax[NV][BLOCK / kWave];
@@ -1483,7 +1494,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   const RedGeom geom = red_geom(a);
   const int shift = geom.shift(red_shift(NV));
   for (int i = threadIdx.x; i < kSlots; i += BLOCK) {
-    s_tag[0][i] = ~0ull;
+    s_tag[i] = kFree;
     s_join[i] = 0;
 #pragma unroll
     for (int c = 0; c < NV; ++c) s_acc[0][i * NV + c] = (Acc)0;
@@ -1647,45 +1658,43 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
       rowv[c] = (d == d && fabs(d) < 2.1e9) ? (int)__builtin_rint(d) : 0;
     }
   }
-  // Per column: insert (claim a slot or find it); an occurrence that found
-  // its (key, slice) already claimed adds its NV values to the slot and marks
-  // it joined; after a barrier each claimer emits its slot's record -- its own
-  // values plus, if joined, the slot's sums (then zeroed for the next column).
-  // A key alone in its column (25-35 % of the occurrences at the Criteo
-  // shape) costs one CAS and one flag read: no accumulator traffic at all.
+  // Per column: insert (claim a free slot, or find the dest's); an occurrence
+  // that found its (key, slice) already claimed adds its NV values to the slot
+  // and marks it joined; a claimer reserves its record's place right away.
+  // After a barrier each claimer frees its slot and writes the record -- its
+  // own values plus, if joined, the slot's sums (then zeroed) -- so the next
+  // column starts on an empty table: the insert is one CAS against kFree per
+  // probe step (no read first, no stale tags), and a key alone in its column
+  // (25-35 % of the occurrences at the Criteo shape) costs one CAS, one flag
+  // read and one tag write -- no accumulator traffic.
+  int fxc[NV];  // (the workgroup's scales, out of LDS once)
+#pragma unroll
+  for (int c = 0; c < NV; ++c) fxc[c] = kScaled ? 0 : s_fxc[c];
   XF_KT(2);
   for (int j0 = 0; j0 < maxlen; j0 += kPosChunk) {
     ps.prefetch(j0 + kPosChunk);
 #pragma unroll
     for (int q = 0; q < kPosChunk; ++q) {
       if (j0 + q >= maxlen) break;
-      const int j = j0 + q;
-      const int t = 0;
       const u32 pj = ps.get(q);
       const bool has = pj != a.trash_pos;
       const u32 dest = pj * S + sl;
       bool claimed = false;
       u32 h = 0;
       if (has) {
-        const u64 key = ((u64)(u32)j << 32) | dest;
         h = (u32)(((u64)(dest * 0x9E3779B1u) * kSlots) >> 32);
-        while (true) {  // <= BLOCK keys per column in > BLOCK slots: terminates
-          const u64 cur = s_tag[t][h];
-          if (cur == key) break;
-          if ((u32)(cur >> 32) != (u32)j) {  // free for this column (empty or stale)
-            const u64 old = atomicCAS((unsigned long long*)&s_tag[t][h], (unsigned long long)cur,
-                                      (unsigned long long)key);
-            if (old == cur) {
-              claimed = true;
-              break;
-            }
-            if (old == key) break;
+        while (true) {  // <= BLOCK keys per column in > BLOCK free slots: terminates
+          const u32 old = atomicCAS(&s_tag[h], kFree, dest);
+          if (old == kFree) {
+            claimed = true;
+            break;
           }
+          if (old == dest) break;
           h = h + 1 == kSlots ? 0u : h + 1;
         }
       }
       if (has && !claimed) {
-        Acc* acc = &s_acc[t][h * NV];
+        Acc* acc = &s_acc[0][h * NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) {
           if constexpr (kScaled)
@@ -1696,7 +1705,9 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
         s_join[h] = 1;
       }
       u32 idx = 0;
-      if constexpr (!kSeg) {  // the record's index in the workgroup region
+      if constexpr (kSeg) {  // the record's place in its bucket's sub-range
+        if (claimed) idx = atomicAdd(&s_hist[dest >> shift], 1u);
+      } else {  // the record's index in the workgroup region
         const unsigned long long m = __ballot(claimed);
         if (m) {
           const int leader = __ffsll((long long)m) - 1;
@@ -1704,12 +1715,14 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
           if (lane == leader) base = atomicAdd(&s_total, (u32)__popcll(m));
           idx = __shfl(base, leader) + (u32)__popcll(m & ((1ull << lane) - 1ull));
         }
+        if (claimed) atomicAdd(&s_hist[dest >> shift], 1u);
       }
       XF_KT(3);
       lds_barrier();
       XF_KT(4);
       if (claimed) {
-        Acc* acc = &s_acc[t][h * NV];
+        s_tag[h] = kFree;
+        Acc* acc = &s_acc[0][h * NV];
         Acc sum[NV];
 #pragma unroll
         for (int c = 0; c < NV; ++c) sum[c] = rowv[c];
@@ -1726,23 +1739,18 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
 #pragma unroll
         for (int c = 0; c < NV; ++c)
           wv[1 + c] = __float_as_uint(kScaled ? (float)fx_to_double_rt((long long)sum[c], fxs)
-                                              : (float)ldexp((double)sum[c], -s_fxc[c]));
+                                              : (float)ldexp((double)sum[c], -fxc[c]));
 #pragma unroll
         for (int c = 1 + NV; c < W; ++c) wv[c] = 0u;
         Rec rec;
 #pragma unroll
         for (int u = 0; u < W / 4; ++u)
           rec.q[u] = make_uint4(wv[4 * u], wv[4 * u + 1], wv[4 * u + 2], wv[4 * u + 3]);
-        if constexpr (kSeg) {
-          region[atomicAdd(&s_hist[dest >> shift], 1u)] = rec;
-          ++written;
-        } else {
-          region[idx] = rec;
-          atomicAdd(&s_hist[dest >> shift], 1u);
-        }
+        region[idx] = rec;
+        if constexpr (kSeg) ++written;
       }
       XF_KT(5);
-      lds_barrier();  // (one table: flushed before the next column inserts)
+      lds_barrier();  // (one table: freed before the next column inserts)
       XF_KT(6);
     }
     ps.advance();
@@ -1766,9 +1774,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
   st.bad |= bad;
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
   XF_KT(7);
-#ifdef XFLOW_KTIMING
-  if (lane_id() == 0) atomicAdd(&g_ktime[15], 1ull);
-#endif
+  XF_KT_FLUSH();
 }
 
 // Sums of a bucket's vector records: units of kR dests (as k_red_sum) with
@@ -2398,7 +2404,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
 template <int BLOCK, bool kGrad>
 __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
   constexpr int LOG2 = ilog2c(2 * BLOCK);
-  __shared__ u64 s_tag64[kGrad ? 2 : 1][kGrad ? (1 << LOG2) : 1];
+  __shared__ u32 s_tag32[kGrad ? 2 : 1][kGrad ? (1 << LOG2) : 1];
   __shared__ long long s_acc[kGrad ? 2 : 1][kGrad ? (1 << LOG2) * 2 : 1];
   __shared__ unsigned short s_list[kGrad ? 2 : 1][kGrad ? BLOCK : 1];
   __shared__ u32 s_hist[kGrad ? kRedMaxBuckets : 1];
@@ -2413,7 +2419,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
   if (active) rs = row_span(b, r);
   const int len = rs.len;
   const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
-  ListAgg<LOG2, 2> lagg{reinterpret_cast<u64(*)[1 << LOG2]>(&s_tag64[0][0]),
+  ListAgg<LOG2, 2> lagg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag32[0][0]),
                         reinterpret_cast<long long(*)[(1 << LOG2) * 2]>(&s_acc[0][0]),
                         reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
                         s_nlist, s_hist, nullptr, 0u};

@@ -320,14 +320,14 @@ constexpr int vec_red_max_buckets(int D) {
              ? 2 * kRedMaxBuckets
              : kRedMaxBuckets;
 }
-// Column-table slots of the int32-accumulator producer (standard FM: tag,
-// 1 + D int32 sums and a joined flag per slot): the same LDS as the int64
-// table buys ~1.8x the slots, i.e. a column load <= 0.36 instead of 0.67 --
-// the insert's linear probe is a chain of dependent LDS round trips (a read,
-// then a CAS, per step), and a wave waits for its longest chain
+// Column-table slots of the int32-accumulator producer (standard FM: a u32
+// tag, 1 + D int32 sums and a joined flag per slot): the LDS of the int64
+// table buys 2x the slots, i.e. a column load <= 0.33 instead of 0.67 -- the
+// insert's linear probe is a chain of dependent LDS round trips, and a wave
+// waits for its longest chain
 constexpr int fmstd_slots32(int D) {
   for (int q = 16; q >= 5; --q)
-    if ((int64_t)(fmstd_block(D) * q / 4) * (8 + 4 * (1 + D) + 1) +
+    if ((int64_t)(fmstd_block(D) * q / 4) * (4 + 4 * (1 + D) + 1) +
             (int64_t)vec_red_max_buckets(D) * 4 + 2048 <= 80 * 1024)
       return fmstd_block(D) * q / 4;
   return fmstd_slots(D);
