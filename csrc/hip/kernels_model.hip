@@ -2307,7 +2307,12 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
     throw std::runtime_error("vector-record red_out with several slices needs the slice bits");
   u32* masks = a.S > 1 ? a.red_masks : nullptr;
   // scatter-free form: the sub-range starts ([nb][groups] u32) live in red_sorted
-  const bool seg = groups <= kSegMaxGroups &&
+  // (XFLOW_FMSTD_SEG=0: the dense producer region + k_red_scatter instead, an A/B switch)
+  static const bool seg_on = [] {
+    const char* e = std::getenv("XFLOW_FMSTD_SEG");
+    return !(e && e[0] == '0');
+  }();
+  const bool seg = seg_on && groups <= kSegMaxGroups &&
                    (int64_t)a.red_nb * groups <= 2 * a.red_sorted_words &&
                    a.red_sorted_words * 8 / (vec_rec_words(NV) * 4) < (1ll << 32);
   if (a.red_maxb > vec_red_max_buckets(D) || (!seg && a.red_maxb > kRedMaxBuckets))
