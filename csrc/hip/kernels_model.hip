@@ -20,6 +20,47 @@
 namespace xflow {
 namespace hip {
 
+// Diagnostic build only (-DXFLOW_KTIMING): per-phase shader-clock cycles of
+// the column-walk producers (k_fm_std_red, k_lr), summed over waves (each
+// wave accumulates in registers, lane 0 adds them once), printed every 25
+// launches (ktime_dump).
+#ifdef XFLOW_KTIMING
+__device__ unsigned long long g_ktime[16];
+#define XF_KT_DECL                  \
+  unsigned long long kt_acc_[8] = {}; \
+  unsigned long long kt_ = clock64()
+#define XF_KT(p)                                  \
+  do {                                            \
+    const unsigned long long n_ = clock64();      \
+    kt_acc_[p] += n_ - kt_;                       \
+    kt_ = n_;                                     \
+  } while (0)
+#define XF_KT_FLUSH()                                                    \
+  do {                                                                   \
+    if (lane_id() == 0) {                                                \
+      for (int p_ = 0; p_ < 8; ++p_) atomicAdd(&g_ktime[p_], kt_acc_[p_]); \
+      atomicAdd(&g_ktime[15], 1ull);                                     \
+    }                                                                    \
+  } while (0)
+#else
+#define XF_KT_DECL (void)0
+#define XF_KT(p) (void)0
+#define XF_KT_FLUSH() (void)0
+#endif
+#ifdef XFLOW_KTIMING
+static void ktime_dump(const char* what, int nphase, hipStream_t st) {
+  static int calls = 0;
+  if (++calls % 25) return;
+  unsigned long long t[16];
+  XF_HIP_CHECK(hipStreamSynchronize(st));
+  XF_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_ktime), sizeof(t)));
+  const double w = (double)(t[15] ? t[15] : 1);
+  std::fprintf(stderr, "[ktime] %s waves %llu  cycles/wave:", what, t[15]);
+  for (int p = 0; p < nphase; ++p) std::fprintf(stderr, " p%d %.0f", p, t[p] / w);
+  std::fprintf(stderr, "\n");
+}
+#endif
+
 // unique index of a gradient row: through the slot -> unique map, or the row
 // itself when the positions already are unique indices (inv == null)
 __device__ __forceinline__ u32 uix(const u32* inv, u64 x) { return inv ? inv[x] : (u32)x; }
@@ -235,6 +276,20 @@ struct ListAgg {
   u32 written;  // (unused: total() after the last barrier)
   int shift = kShift;  // bucket = dest >> shift (RedGeom: runtime, >= kShift)
   u32 bad = 0;   // a clamped fixed-point input (see fx_clamp), OR-ed into the stats flag
+#ifdef XFLOW_KTIMING
+  unsigned long long* kt_acc_ = nullptr;  // (the kernel's phase counters: 4 insert, 5 barrier, 6 flush)
+  unsigned long long* kt_cur_ = nullptr;
+#define XF_KTL(p)                                  \
+  do {                                             \
+    if (kt_acc_) {                                 \
+      const unsigned long long n_ = clock64();     \
+      kt_acc_[p] += n_ - *kt_cur_;                 \
+      *kt_cur_ = n_;                               \
+    }                                              \
+  } while (0)
+#else
+#define XF_KTL(p) (void)0
+#endif
 
   __device__ __forceinline__ unsigned char* joined(int t) {
     return reinterpret_cast<unsigned char*>(&list[t][0]);
@@ -298,7 +353,9 @@ struct ListAgg {
       XF_DASSERT((int)(dest >> shift) < kRedMaxBuckets);
       atomicAdd(&hist[dest >> shift], 1u);
     }
+    XF_KTL(4);
     lds_barrier();
+    XF_KTL(5);
     if (claimed) {
       tag[t][h] = kFree;
       if (joined(t)[h]) {
@@ -318,6 +375,7 @@ struct ListAgg {
             make_uint3(dest, __float_as_uint(v0), __float_as_uint(v1));
       }
     }
+    XF_KTL(6);
   }
 };
 
@@ -386,6 +444,7 @@ __device__ __forceinline__ void lr_column(ColumnAgg<1, LOG2>& agg, int j, bool h
 // atomics at 256 rows, 2.95 M at 1024 rows, for 10.2 M occurrences).
 template <bool kGrad, bool kAgg, int BLOCK, bool kRed = false>
 __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
+  XF_KT_DECL;
   constexpr int LOG2 = ilog2c(2 * BLOCK);
   constexpr int C = kLrRegCols;
   constexpr bool kCol = kAgg && !kRed;  // column tables with global atomics
@@ -420,6 +479,10 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
     lagg.region = a.red_pairs + (b.row_ptr ? (int64_t)b.row_ptr[r0] : r0 * b.nnz_per_row);
     lagg.init(red_active(a, red_shift(1)));
     lagg.shift = red_geom(a).shift(red_shift(1));
+#ifdef XFLOW_KTIMING
+    lagg.kt_acc_ = kt_acc_;
+    lagg.kt_cur_ = &kt_;
+#endif
   }
   // block-uniform longest row: selects the register path and bounds the
   // backward column walk
@@ -439,6 +502,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   float loss = 0.0f;
   const u32 s = active ? (u32)slice_of(b, r, a.S) : 0u;
   const u32 S = (u32)a.S;
+  XF_KT(0);
   if (maxlen <= C) {
     u32 pv[C];
 #pragma unroll
@@ -457,6 +521,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
       if (a.pctr) a.pctr[r] = p;
       st.add(p, y);
     }
+    XF_KT(1);
     if constexpr (kGrad) {
       if constexpr (!kAgg) {
 #pragma unroll
@@ -471,6 +536,7 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
         }
       }
     }
+    XF_KT(2);
   } else {
     if (active) {
       float wx = 0.0f;
@@ -523,6 +589,8 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   }
   st.bad |= lagg.bad;
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
+  XF_KT(3);
+  XF_KT_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -1420,32 +1488,6 @@ __global__ void __launch_bounds__(BLOCK) k_fm_red(FwdArgs a) {
 // kScaled (MVM): T = loss*M spans many orders of magnitude (a product over
 // fields), beyond any one static fixed-point scale: the int64 sums use the
 // step's scale (fx_scale_bits of FwdArgs::red_vmax, set by the forward).
-// Diagnostic build only (-DXFLOW_KTIMING): per-phase shader-clock cycles of
-// the standard-FM producer, summed over waves (lane 0 of each wave adds its
-// deltas), printed every 25 launches by launch_fmstd_reduction.
-#ifdef XFLOW_KTIMING
-__device__ unsigned long long g_ktime[16];
-#define XF_KT_DECL                  \
-  unsigned long long kt_acc_[8] = {}; \
-  unsigned long long kt_ = clock64()
-#define XF_KT(p)                                  \
-  do {                                            \
-    const unsigned long long n_ = clock64();      \
-    kt_acc_[p] += n_ - kt_;                       \
-    kt_ = n_;                                     \
-  } while (0)
-#define XF_KT_FLUSH()                                                    \
-  do {                                                                   \
-    if (lane_id() == 0) {                                                \
-      for (int p_ = 0; p_ < 8; ++p_) atomicAdd(&g_ktime[p_], kt_acc_[p_]); \
-      atomicAdd(&g_ktime[15], 1ull);                                     \
-    }                                                                    \
-  } while (0)
-#else
-#define XF_KT_DECL (void)0
-#define XF_KT(p) (void)0
-#define XF_KT_FLUSH() (void)0
-#endif
 
 template <int D, int BLOCK, bool kSeg = false, bool kSplit = false, bool kScaled = false>
 __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
@@ -2329,18 +2371,7 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
                                "S = 2^slog2 <= 2^shift, full-row entries (MVM: dup records)");
   }
 #ifdef XFLOW_KTIMING
-  {
-    static int calls = 0;
-    if (++calls % 25 == 0) {
-      unsigned long long t[16];
-      XF_HIP_CHECK(hipStreamSynchronize(st));
-      XF_HIP_CHECK(hipMemcpyFromSymbol(t, HIP_SYMBOL(g_ktime), sizeof(t)));
-      const double w = (double)(t[15] ? t[15] : 1);
-      std::fprintf(stderr, "[ktime] waves %llu  cycles/wave: init %.0f prepass %.0f rowv %.0f | "
-                   "insert %.0f bar1 %.0f flush %.0f bar2 %.0f | tail %.0f\n", t[15], t[0] / w,
-                   t[1] / w, t[2] / w, t[3] / w, t[4] / w, t[5] / w, t[6] / w, t[7] / w);
-    }
-  }
+  ktime_dump("fmstd (init prepass rowv insert bar1 flush bar2 tail)", 8, st);
 #endif
   if (split && !kMvm)
     hipLaunchKernelGGL(k_fm_std_fwd<D>, dim3((int)((a.batch.rows + kBlock - 1) / kBlock)),
@@ -3005,6 +3036,9 @@ void launch_forward_backward(const FwdArgs& a, hipStream_t st) {
           case 256: hipLaunchKernelGGL((k_lr<true, true, 256, true>), dim3(gr), dim3(R), 0, st, a); break;
           default: hipLaunchKernelGGL((k_lr<true, true, 128, true>), dim3(gr), dim3(R), 0, st, a); break;
         }
+#ifdef XFLOW_KTIMING
+        ktime_dump("lr (init forward walk-other tail insert barrier flush)", 7, st);
+#endif
         launch_reduction<1>(a, gr, R, st);
       } else if (grad && a.agg_ok)
         hipLaunchKernelGGL((k_lr<true, true, kLrBlock>), dim3(g), dim3(kLrBlock), 0, st, a);
