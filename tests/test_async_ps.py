@@ -144,3 +144,44 @@ def test_async_single_rank_and_eval(tmp_path):
     ref.import_table(*aps.server.export_table())
     q = ref.eval_step(_batch(0, 99, 2))
     np.testing.assert_array_equal(p.numpy(), q.numpy())
+
+
+def _ckpt_rank(rank, world, data_dir, root, out_dir, resume):
+    from xflow_amd.config import TrainConfig
+    from xflow_amd.trainer import Trainer
+
+    cfg = TrainConfig(train_prefix=os.path.join(data_dir, "small_train"),
+                      test_prefix=os.path.join(data_dir, "small_test"), epochs=3, threads=4,
+                      async_ps=True, staleness=1, write_pred=False, save_every=1,
+                      engine=EngineConfig(table_log2_cap=14))
+    t = Trainer(cfg, device=torch.device("cpu"))
+    if resume:
+        meta = t.resume(root)
+        assert meta is not None and t.epoch == int(meta["epoch"])
+        # the resumed server shard is the saved one, bit for bit
+        saved = np.load(os.path.join(out_dir, f"ep{t.epoch}_r{rank}.npz"))
+        keys, words = _table(t.table)
+        assert np.array_equal(keys, saved["keys"]) and np.array_equal(words, saved["words"])
+        t.train()
+        np.save(os.path.join(out_dir, f"resumed_epoch_r{rank}.npy"), np.array([t.epoch]))
+    else:
+        cfg.checkpoint_dir = root
+        t.train_epochs(2)
+        keys, words = _table(t.table)
+        np.savez(os.path.join(out_dir, f"ep{t.epoch}_r{rank}.npz"), keys=keys, words=words)
+    t.close()
+
+
+def test_async_trainer_checkpoint_resume(tmp_path):
+    """Config 4 through the Trainer with versioned checkpoints: every epoch
+    end pauses the servers (all pushes applied), each rank saves its shard;
+    a new 2-rank job resumes from LATEST with each shard restored bit for
+    bit and trains the remaining epoch."""
+    from conftest import DATA
+
+    root = str(tmp_path / "ckpt")
+    run_world(_ckpt_rank, 2, DATA, root, str(tmp_path), False)
+    assert os.path.exists(os.path.join(root, "LATEST"))
+    run_world(_ckpt_rank, 2, DATA, root, str(tmp_path), True)
+    for r in range(2):
+        assert int(np.load(tmp_path / f"resumed_epoch_r{r}.npy")[0]) == 3
