@@ -398,7 +398,7 @@ class CpuBackend final : public Backend {
   void synth_batch(const SynthArgs& a) override {
     if (a.fields > kSynthMaxFields) throw std::runtime_error("synth: at most 64 fields");
     std::vector<SynthField> F(a.fields);
-    for (int f = 0; f < a.fields; ++f) F[f] = synth_field(a.vocab[f], (double)a.zipf_s[f]);
+    for (int f = 0; f < a.fields; ++f) F[f] = synth_field(a.vocab[f], (double)a.zipf_s[f], f);
     for (int64_t r = 0; r < a.rows; ++r) {
       const u64 rs = synth_row_seed(a.seed, a.step, r);
       float logit = a.planted_bias;

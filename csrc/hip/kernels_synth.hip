@@ -62,7 +62,7 @@ void launch_synth(const SynthArgs& a, hipStream_t st) {
   if (a.rows <= 0) return;
   if (a.fields > kSynthMaxFields) throw std::runtime_error("synth: at most 64 fields");
   SynthConsts c;
-  for (int f = 0; f < a.fields; ++f) c.f[f] = synth_field(a.vocab[f], (double)a.zipf_s[f]);
+  for (int f = 0; f < a.fields; ++f) c.f[f] = synth_field(a.vocab[f], (double)a.zipf_s[f], f);
   const dim3 grid((int)((a.rows + kSynthRows - 1) / kSynthRows));
   if (synth_small_ok(a.vocab, a.fields, a.hash_space))
     hipLaunchKernelGGL(k_synth<true>, grid, dim3(kBlock), 0, st, a, c);

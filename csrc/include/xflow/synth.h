@@ -102,15 +102,17 @@ XF_HD u64 synth_row_seed(u64 seed, u64 step, int64_t r) {
 // double on the host and rounded to float for the per-element recipe.
 struct SynthField {
   u64 vocab;
+  u64 fseed;     // (f + 1) * 0x94d049bb133111eb: the field's term of the element hash
   float A;       // (V+1)^(1-s) - 1
   float inv_e;   // 1/(1-s)
   float log2v1;  // log2(V+1), for s == 1
   int unit_s;
 };
 
-inline SynthField synth_field(u64 vocab, double s) {
+inline SynthField synth_field(u64 vocab, double s, int f) {
   SynthField F;
   F.vocab = vocab ? vocab : 1;
+  F.fseed = (u64)(f + 1) * 0x94d049bb133111ebull;
   const double V = (double)F.vocab;
   F.unit_s = fabs(s - 1.0) < 1e-9;
   F.log2v1 = (float)log2(V + 1.0);
@@ -138,7 +140,7 @@ XF_HD u64 mulhi64_u32(u64 a, u32 b) {
 template <bool kSmall = false>
 XF_HD u64 synth_sample(u64 rowseed, int f, const SynthField& F, u64 hash_space, float scale,
                        float& weight) {
-  const u64 h = fmix64(rowseed + (u64)(f + 1) * 0x94d049bb133111ebull);
+  const u64 h = fmix64(rowseed + F.fseed);  // (a 64-bit multiply per element saved)
   const float u = synth_unit_f(h);
   const float y = F.unit_s ? u * F.log2v1 : synth_log2(F.A * u + 1.0f) * F.inv_e;
   u64 rank;
