@@ -25,6 +25,7 @@ __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
   __shared__ float pw[kSynthRows * kSynthMaxFields];
   __shared__ u64 rseed[kSynthRows];
   __shared__ SynthField fc[kSynthMaxFields];
+  __shared__ int64_t fofs[kSynthMaxFields];  // field-major: f * col_stride (no 64-bit multiply per key)
   const int F = a.fields;
   const int64_t r0 = (int64_t)blockIdx.x * kSynthRows;
   const int rows = (int)min((int64_t)kSynthRows, a.rows - r0);
@@ -32,7 +33,10 @@ __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
   const bool field_major = a.col_stride > 0;
   if ((int)threadIdx.x < rows)
     rseed[threadIdx.x] = synth_row_seed_mixed(a.seed, synth_step_mix(a.step), r0 + threadIdx.x);
-  if ((int)threadIdx.x < F) fc[threadIdx.x] = c.f[threadIdx.x];
+  if ((int)threadIdx.x < F) {
+    fc[threadIdx.x] = c.f[threadIdx.x];
+    fofs[threadIdx.x] = (int64_t)threadIdx.x * a.col_stride;
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
     int rl, f;
@@ -45,7 +49,7 @@ __global__ void __launch_bounds__(kBlock) k_synth(SynthArgs a, SynthConsts c) {
     }
     float w;
     const u64 key = synth_sample<kSmall>(rseed[rl], f, fc[f], a.hash_space, a.planted_scale, w);
-    const int64_t o = field_major ? (int64_t)f * a.col_stride + r0 + rl : r0 * F + e;
+    const int64_t o = field_major ? fofs[f] + r0 + rl : r0 * F + e;
     a.keys[o] = key;
     if (a.fgid) a.fgid[o] = f;
     pw[rl * F + f] = w;
