@@ -149,18 +149,14 @@ __global__ void __launch_bounds__(kBlock) k_dedup_insert(const u64* __restrict__
   for (int j = 0; j < kDedupItems; ++j) {
     if (base + (int64_t)j * kBlock >= nnz) continue;
     u32 x = h[j];
-    while (true) {
-      const u64 c = t_key[x];
-      if (c == k[j]) break;
-      if (c == kEmptyKey) {
-        const u64 prev = atomicCAS((unsigned long long*)&t_key[x], (unsigned long long)kEmptyKey,
-                                   (unsigned long long)k[j]);
-        if (prev == kEmptyKey) {
-          lead |= 1u << j;
-          break;
-        }
-        if (prev == k[j]) break;
+    while (true) {  // (one CAS against an empty slot per probe step, no read first)
+      const u64 prev = atomicCAS((unsigned long long*)&t_key[x], (unsigned long long)kEmptyKey,
+                                 (unsigned long long)k[j]);
+      if (prev == kEmptyKey) {
+        lead |= 1u << j;
+        break;
       }
+      if (prev == k[j]) break;
       x = (x + 1) & (kL - 1);  // <= kDedupChunk keys in kL slots: terminates
     }
     h[j] = x;
