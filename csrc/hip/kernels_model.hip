@@ -203,13 +203,9 @@ struct ColumnAgg {
   // kSlots/2 keys, so the probe always terminates
   __device__ __forceinline__ int insert(int t, u32 dest) {
     u32 h = (dest * 0x9E3779B1u) >> (32 - LOG2);
-    while (true) {
-      u32 cur = tag[t][h];
-      if (cur == dest) return (int)h;
-      if (cur == kColEmpty) {
-        u32 old = atomicCAS(&tag[t][h], kColEmpty, dest);
-        if (old == kColEmpty || old == dest) return (int)h;
-      }
+    while (true) {  // (one CAS against an empty slot per probe step, no read first)
+      const u32 old = atomicCAS(&tag[t][h], kColEmpty, dest);
+      if (old == kColEmpty || old == dest) return (int)h;
       h = (h + 1) & (kSlots - 1);
     }
   }
@@ -1269,13 +1265,9 @@ __global__ void __launch_bounds__(kCsrBlock) k_red_csr(const void* __restrict__ 
       lds_barrier();
       auto insert = [&](u32 d, const T& r) {
         u32 h = (d * 0x9E3779B1u) >> (32 - ilog2c(kCsrHash));
-        while (true) {
-          const u32 cur = tag[h];
-          if (cur == d) break;
-          if (cur == ~0u) {
-            const u32 old = atomicCAS(&tag[h], ~0u, d);
-            if (old == ~0u || old == d) break;
-          }
+        while (true) {  // (one CAS against an empty slot per probe step)
+          const u32 old = atomicCAS(&tag[h], ~0u, d);
+          if (old == ~0u || old == d) break;
           h = (h + 1) & (kCsrHash - 1);
         }
         add(h, r);
