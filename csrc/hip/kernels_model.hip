@@ -1573,6 +1573,11 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     for (int c = 0; c < NV; ++c) nz |= t[c] != 0.0f;
     live = nz || S > 1u || !kScaled;
   }
+  constexpr int kPer = kMaxB / BLOCK;
+  // kSeg: this thread's buckets' sub-range starts kept for the tail (when
+  // they fit a few registers; else re-read from red_sorted)
+  constexpr bool kRegStart = kSeg && kPer <= 8;
+  u32 sstart[kRegStart ? kPer : 1];
   if constexpr (kSeg) {
     // occurrences per bucket (s_hist, zeroed above) -> sub-range starts (the cursors)
     const PosStream pp(pos, rs, live ? len : 0, a.trash_pos, false);
@@ -1585,7 +1590,6 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
           atomicAdd(&s_hist[(pv[q] * S + sl) >> shift], 1u);
     }
     __syncthreads();
-    constexpr int kPer = kMaxB / BLOCK;
     const int nb = geom.active(shift, a.red_nb);
     u32 c[kPer], sum = 0;
 #pragma unroll
@@ -1604,6 +1608,7 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
         sub_out[(size_t)i * gridDim.x + blockIdx.x] = ex;
         s_hist[i] = ex;  // now the record cursor
       }
+      if constexpr (kRegStart) sstart[q] = ex;
       ex += c[q];
     }
     __syncthreads();
@@ -1799,11 +1804,21 @@ __global__ void __launch_bounds__(BLOCK) k_fm_std_red(FwdArgs a) {
     a.red_count[blockIdx.x] = written;
     if (a.red_records) atomicAdd(a.red_records, (unsigned long long)written);
   }
-  // (kSeg: the cursor ends at the bucket's start in the region + its records)
-  const u32* sub_start = reinterpret_cast<const u32*>(a.red_sorted);
-  for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) {
-    const size_t at = (size_t)i * gridDim.x + blockIdx.x;
-    a.red_hist[at] = kSeg ? s_hist[i] - sub_start[at] : s_hist[i];
+  // (kSeg: the cursor ends at the bucket's start in the region + its records;
+  // the starts are still in the registers of the pre-pass's bucket mapping)
+  if constexpr (kRegStart) {
+    const int nb = geom.active(shift, a.red_nb);
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int i = (int)threadIdx.x * kPer + q;
+      if (i < nb) a.red_hist[(size_t)i * gridDim.x + blockIdx.x] = s_hist[i] - sstart[q];
+    }
+  } else {
+    const u32* sub_start = reinterpret_cast<const u32*>(a.red_sorted);
+    for (int i = threadIdx.x, n = geom.active(shift, a.red_nb); i < n; i += BLOCK) {
+      const size_t at = (size_t)i * gridDim.x + blockIdx.x;
+      a.red_hist[at] = kSeg ? s_hist[i] - sub_start[at] : s_hist[i];
+    }
   }
   st.bad |= bad;
   flush_stats<BLOCK>(st, a.stats, a.fx_bad);
