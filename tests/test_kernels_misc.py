@@ -334,10 +334,10 @@ int main() {
   const u64 spaces[] = {1, 7, 1000000000ull, (1ull << 32) - 1};
   long bad = 0, n = 0;
   for (u64 V : vocabs) for (double s : ss) for (u64 hs : spaces) {
-    const SynthField F = synth_field(V, s);
     for (u64 r = 0; r < 20000; ++r) {
       const u64 seed = fmix64(r * 0x9e3779b97f4a7c15ull + V + hs);
       for (int f = 0; f < 39; f += 7) {
+        const SynthField F = synth_field(V, s, f);
         float w0, w1;
         const u64 k0 = synth_sample<false>(seed, f, F, hs, 0.3f, w0);
         const u64 k1 = synth_sample<true>(seed, f, F, hs, 0.3f, w1);
