@@ -442,14 +442,18 @@ template <bool kGrad, bool kAgg, int BLOCK, bool kRed = false>
 __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   XF_KT_DECL;
   constexpr int LOG2 = ilog2c(2 * BLOCK);
+  // the reduction's column tables: 4 x BLOCK slots (a column's load <= 1/4:
+  // short probe chains -- the insert is a chain of dependent LDS CASes, and
+  // the barrier waits for the longest); the workgroup owns its CU anyway
+  constexpr int LOG2R = ilog2c(4 * BLOCK);
   constexpr int C = kLrRegCols;
   constexpr bool kCol = kAgg && !kRed;  // column tables with global atomics
   __shared__ u32 s_tag[kCol ? 2 : 1][kCol ? (1 << LOG2) : 1];
   __shared__ float s_acc[kCol ? 2 : 1][kCol ? (1 << LOG2) : 1];
-  __shared__ long long s_fx[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
+  __shared__ long long s_fx[kRed ? 2 : 1][kRed ? (1 << LOG2R) : 1];
   __shared__ int s_wmax[BLOCK / kWave];
-  __shared__ u32 s_tag32[kRed ? 2 : 1][kRed ? (1 << LOG2) : 1];
-  __shared__ unsigned short s_list[kRed ? 2 : 1][kRed ? BLOCK : 1];
+  __shared__ u32 s_tag32[kRed ? 2 : 1][kRed ? (1 << LOG2R) : 1];
+  __shared__ unsigned short s_list[kRed ? 2 : 1][kRed ? (1 << LOG2R) / 2 : 1];
   __shared__ u32 s_hist[kRed ? kRedMaxBuckets : 1];
   __shared__ u32 s_nlist[3];
   const BatchView& b = a.batch;
@@ -464,9 +468,9 @@ __global__ void __launch_bounds__(BLOCK) k_lr(FwdArgs a) {
   ColumnAgg<1, LOG2> agg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag[0][0]),
                          reinterpret_cast<float(*)[1 << LOG2]>(&s_acc[0][0])};
   if constexpr (kCol) agg.init();
-  ListAgg<LOG2> lagg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag32[0][0]),
-                     reinterpret_cast<long long(*)[1 << LOG2]>(&s_fx[0][0]),
-                     reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
+  ListAgg<LOG2R> lagg{reinterpret_cast<u32(*)[1 << LOG2R]>(&s_tag32[0][0]),
+                      reinterpret_cast<long long(*)[1 << LOG2R]>(&s_fx[0][0]),
+                      reinterpret_cast<unsigned short(*)[(1 << LOG2R) / 2]>(&s_list[0][0]),
                      s_nlist, s_hist, nullptr, 0u};
   if constexpr (kRed) {
     // the workgroup's pair region starts at its first row's first occurrence
