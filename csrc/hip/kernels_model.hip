@@ -257,7 +257,9 @@ struct ColumnAgg {
 // Σ loss and Σ loss*vsum, expanded to the 1+D gradient in k_red_sum).
 // Records: NV == 1 -> u64 (dest | value << 32), NV == 2 -> uint3 (dest, v0, v1):
 // 12 bytes, dwordx3 accesses (a quarter less traffic than padded uint4 records).
-template <int LOG2, int NV = 1>
+// kTabs = 1: one table, freed before the next column inserts (a second
+// barrier per column) -- twice the slots in the same LDS.
+template <int LOG2, int NV = 1, int kTabs = 2>
 struct ListAgg {
   static constexpr int kSlots = 1 << LOG2;
   static constexpr int kShift = red_shift(NV);
@@ -292,10 +294,13 @@ struct ListAgg {
   }
   __device__ __forceinline__ void init(int nb) {
     for (int i = threadIdx.x; i < kSlots; i += blockDim.x) {
-      tag[0][i] = tag[1][i] = kFree;
-      joined(0)[i] = joined(1)[i] = 0;
 #pragma unroll
-      for (int v = 0; v < NV; ++v) acc[0][i * NV + v] = acc[1][i * NV + v] = 0ll;
+      for (int tt = 0; tt < kTabs; ++tt) {
+        tag[tt][i] = kFree;
+        joined(tt)[i] = 0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) acc[tt][i * NV + v] = 0ll;
+      }
     }
     for (int i = threadIdx.x; i < nb; i += blockDim.x) hist[i] = 0u;
     if (threadIdx.x == 0) nlist[0] = 0u;
@@ -319,7 +324,7 @@ struct ListAgg {
   // called by every lane of the workgroup (wave-uniform control flow)
   __device__ __forceinline__ void column(int j, bool has, u32 dest, float loss,
                                          float loss2 = 0.0f) {
-    const int t = j & 1;
+    const int t = kTabs == 2 ? (j & 1) : 0;
     bool claimed = false;
     int h = 0;
     long long v[NV];
@@ -372,6 +377,7 @@ struct ListAgg {
       }
     }
     XF_KTL(6);
+    if constexpr (kTabs == 1) lds_barrier();  // (freed before the next column inserts)
   }
 };
 
@@ -2450,10 +2456,12 @@ static void launch_vec_reduction(const FwdArgs& a, hipStream_t st) {
 // A third of the gather traffic of the full-row kernel, independent of D.
 template <int BLOCK, bool kGrad>
 __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
-  constexpr int LOG2 = ilog2c(2 * BLOCK);
-  __shared__ u32 s_tag32[kGrad ? 2 : 1][kGrad ? (1 << LOG2) : 1];
-  __shared__ long long s_acc[kGrad ? 2 : 1][kGrad ? (1 << LOG2) * 2 : 1];
-  __shared__ unsigned short s_list[kGrad ? 2 : 1][kGrad ? BLOCK : 1];
+  // one column table of 4 x BLOCK slots (load <= 1/4: short probe chains) in
+  // the LDS of two alternating 2 x BLOCK ones, at one more barrier per column
+  constexpr int LOG2 = ilog2c(4 * BLOCK);
+  __shared__ u32 s_tag32[1][kGrad ? (1 << LOG2) : 1];
+  __shared__ long long s_acc[1][kGrad ? (1 << LOG2) * 2 : 1];
+  __shared__ unsigned short s_list[1][kGrad ? (1 << LOG2) / 2 : 1];
   __shared__ u32 s_hist[kGrad ? kRedMaxBuckets : 1];
   __shared__ u32 s_nlist[3];
   __shared__ int s_wmax[BLOCK / kWave];
@@ -2466,10 +2474,10 @@ __global__ void __launch_bounds__(BLOCK) k_fm_vals(FwdArgs a) {
   if (active) rs = row_span(b, r);
   const int len = rs.len;
   const int64_t r0 = (int64_t)blockIdx.x * BLOCK;
-  ListAgg<LOG2, 2> lagg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag32[0][0]),
-                        reinterpret_cast<long long(*)[(1 << LOG2) * 2]>(&s_acc[0][0]),
-                        reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
-                        s_nlist, s_hist, nullptr, 0u};
+  ListAgg<LOG2, 2, 1> lagg{reinterpret_cast<u32(*)[1 << LOG2]>(&s_tag32[0][0]),
+                           reinterpret_cast<long long(*)[(1 << LOG2) * 2]>(&s_acc[0][0]),
+                           reinterpret_cast<unsigned short(*)[(1 << LOG2) / 2]>(&s_list[0][0]),
+                           s_nlist, s_hist, nullptr, 0u};
   int maxlen = 0;
   if constexpr (kGrad) {
     lagg.region = reinterpret_cast<u64*>(reinterpret_cast<uint3*>(a.red_pairs) +
